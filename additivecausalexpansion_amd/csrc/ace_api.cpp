@@ -1,0 +1,884 @@
+// ace_api.cpp -- C ABI (include/ace_hip.h) over the HIP kernels: context,
+// argument checking, layout packing, the drop-in Rcpp-export equivalents
+// and the device-resident para_update pipeline.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "../../include/ace_hip.h"
+#include "ace_internal.h"
+
+using namespace ace;
+
+struct ace_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+};
+
+static std::string g_create_err;
+
+namespace {
+
+const double kNaN = std::numeric_limits<double>::quiet_NaN();
+
+struct Fail {
+  int code;
+};
+
+// RAII device buffer
+struct DBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  DBuf() = default;
+  DBuf(const DBuf &) = delete;
+  DBuf &operator=(const DBuf &) = delete;
+  ~DBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  double *d() const { return static_cast<double *>(p); }
+  int *i() const { return static_cast<int *>(p); }
+};
+
+void ck(ace_ctx *ctx, hipError_t e, const char *what) {
+  if (e == hipSuccess) return;
+  ctx->err = std::string(what) + ": " + hipGetErrorString(e);
+  throw Fail{e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation ? ACE_ERR_OOM
+                                                                          : ACE_ERR_HIP};
+}
+
+void arg(ace_ctx *ctx, bool ok, const char *msg) {
+  if (ok) return;
+  ctx->err = msg;
+  throw Fail{ACE_ERR_ARG};
+}
+
+void alloc(ace_ctx *ctx, DBuf &b, size_t bytes, const char *what) {
+  if (b.bytes >= bytes && b.p) return;
+  b.release();
+  if (bytes == 0) bytes = 16;
+  ck(ctx, hipMalloc(&b.p, bytes), what);
+  b.bytes = bytes;
+}
+
+// Host -> device copies are synchronous (pageable host buffers may be
+// temporaries); every call syncs its stream before returning, so no kernel
+// of a previous call can still be reading the destination.
+void upload(ace_ctx *ctx, DBuf &b, const double *h, size_t count, const char *what) {
+  alloc(ctx, b, count * sizeof(double), what);
+  if (count) ck(ctx, hipMemcpy(b.p, h, count * sizeof(double), hipMemcpyHostToDevice), what);
+}
+
+void download(ace_ctx *ctx, double *h, const double *d, size_t count, const char *what) {
+  if (count) ck(ctx, hipMemcpyAsync(h, d, count * sizeof(double), hipMemcpyDeviceToHost,
+                                    ctx->stream), what);
+}
+
+void sync(ace_ctx *ctx) { ck(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize"); }
+
+int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+struct Shape {
+  int kind, p, B, PM, ZS;
+};
+
+Shape check_shape(ace_ctx *ctx, int kind, int p, int B) {
+  arg(ctx, kind == ACE_KERNEL_SE || kind == ACE_KERNEL_MATERN32, "unknown kernel kind");
+  arg(ctx, p >= 0 && B >= 1, "p must be >= 0 and B >= 1");
+  if (p > PMAX || B > BMAX) {
+    ctx->err = "unsupported shape: p <= 64 and B <= 32 are compiled";
+    throw Fail{ACE_ERR_UNSUPPORTED};
+  }
+  Shape s;
+  s.kind = kind;
+  s.p = p;
+  s.B = B;
+  s.PM = pm_bucket(p < 1 ? 1 : p);
+  s.ZS = B > 1 ? B - 1 : 1;
+  return s;
+}
+
+// column-major X (n x p) -> row-major n x PM, zero padded
+std::vector<double> pack_rows(const double *M, int64_t n, int cols, int width) {
+  std::vector<double> out((size_t)(n * width), 0.0);
+  for (int i = 0; i < cols; ++i)
+    for (int64_t r = 0; r < n; ++r) out[(size_t)(r * width + i)] = M[r + i * n];
+  return out;
+}
+
+// theta tables (b-major), see TabView in ace_internal.h
+std::vector<double> make_tab(const double *theta, const Shape &s) {
+  const int B = s.B, PM = s.PM;
+  std::vector<double> t((size_t)(2 * B * PM + B), 0.0);
+  for (int b = 0; b < B; ++b) {
+    for (int i = 0; i < s.p; ++i) {
+      t[(size_t)(b * PM + i)] = std::exp(-theta[1 + b + B * (i + 1)]);        // Q1 kernel index
+      t[(size_t)(B * PM + b * PM + i)] = std::exp(-theta[2 + B + b + B * i]);  // gradient index
+    }
+    t[(size_t)(2 * B * PM + b)] = theta[2 + b];
+  }
+  return t;
+}
+
+TabView tab_view(const DBuf &b, const Shape &s) {
+  TabView v;
+  v.wk = b.d();
+  v.wg = b.d() + s.B * s.PM;
+  v.lam = b.d() + 2 * s.B * s.PM;
+  return v;
+}
+
+// Device copy of one pair side (X, Z, log|Z|).
+struct SideBufs {
+  DBuf X, Z, LZ;
+  PairSide view(int64_t n) const {
+    PairSide ps;
+    ps.X = X.d();
+    ps.Z = Z.d();
+    ps.LZ = LZ.d();
+    ps.n = n;
+    return ps;
+  }
+};
+
+void upload_side(ace_ctx *ctx, SideBufs &sb, const Shape &s, const double *X, const double *Z,
+                 int64_t n, int64_t nalloc) {
+  std::vector<double> xr = pack_rows(X, n, s.p, s.PM);
+  xr.resize((size_t)(nalloc * s.PM), 0.0);
+  upload(ctx, sb.X, xr.data(), xr.size(), "upload X");
+  std::vector<double> zr((size_t)(nalloc * s.ZS), 0.0);
+  if (s.B > 1 && Z) {
+    std::vector<double> t = pack_rows(Z, n, s.B - 1, s.ZS);
+    std::copy(t.begin(), t.end(), zr.begin());
+  }
+  upload(ctx, sb.Z, zr.data(), zr.size(), "upload Z");
+  alloc(ctx, sb.LZ, zr.size() * sizeof(double), "alloc LZ");
+  if (s.kind == ACE_KERNEL_SE)
+    ck(ctx, launch_log_abs(sb.Z.d(), sb.LZ.d(), (int64_t)zr.size(), ctx->stream), "log_abs");
+}
+
+double host_logsum(const double *w, int64_t n) {
+  double s = 0.0;
+  for (int64_t j = 0; j < n; ++j) s += std::log(w[j]);
+  return s;
+}
+
+// Final composition of the P-gradient from the device sums.
+//   gsum[b*(PM+1)+i] : sum T K_b d_i^2 (SE) / sum T K_b/(1+sqrt(3 r~2)) d_i^2 (Matern)
+//   gsum[b*(PM+1)+PM]: sum T K_b ; gsum[B*(PM+1)] : trace T
+void compose_grad(const Shape &s, const double *theta, const double *gsum, double sum_alpha,
+                  double *grad) {
+  const int B = s.B, PM = s.PM, P = 2 + B * (s.p + 1);
+  for (int j = 0; j < P; ++j) grad[j] = 0.0;
+  grad[0] = -0.5 * gsum[B * (PM + 1)] * std::exp(theta[0]);  // sigma_gradient
+  for (int b = 0; b < B; ++b) grad[2 + b] = -0.5 * gsum[b * (PM + 1) + PM];
+  for (int i = 0; i < s.p; ++i)
+    for (int b = 0; b < B; ++b) {
+      const int j = 2 + B + b + B * i;
+      const double sum = gsum[b * (PM + 1) + i];
+      if (s.kind == ACE_KERNEL_SE) grad[j] = -0.5 * (sum * std::exp(-theta[j]));
+      else grad[j] = -0.25 * 9 * sum * std::exp(-theta[j]);
+    }
+  grad[1] = (s.kind == ACE_KERNEL_SE) ? sum_alpha : 0.0;
+}
+
+}  // namespace
+
+#define ACE_TRY try {
+#define ACE_CATCH \
+  }               \
+  catch (const Fail &f) { return f.code; }
+
+extern "C" {
+
+int ace_abi_version(void) { return ACE_ABI_VERSION; }
+
+int ace_create(int device, ace_ctx **out) {
+  if (!out) return ACE_ERR_ARG;
+  *out = nullptr;
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count <= 0) {
+    g_create_err = std::string("no HIP device available: ") +
+                   (e == hipSuccess ? "count == 0" : hipGetErrorString(e));
+    return ACE_ERR_HIP;
+  }
+  if (device < 0 || device >= count) {
+    g_create_err = "device index out of range";
+    return ACE_ERR_ARG;
+  }
+  e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    g_create_err = std::string("hipSetDevice: ") + hipGetErrorString(e);
+    return ACE_ERR_HIP;
+  }
+  ace_ctx *c = new ace_ctx();
+  c->device = device;
+  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    g_create_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
+    delete c;
+    return ACE_ERR_HIP;
+  }
+  *out = c;
+  return ACE_OK;
+}
+
+void ace_destroy(ace_ctx *ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char *ace_last_error(const ace_ctx *ctx) {
+  if (!ctx) return g_create_err.c_str();
+  return ctx->err.c_str();
+}
+
+// ------------------------------------------------------------ assembly
+int ace_kernmat_sym(ace_ctx *ctx, int kind, int64_t n, int p, int B, const double *X,
+                    const double *Z, const double *theta, double *Kfull, double *Kel) {
+  if (!ctx) return ACE_ERR_ARG;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  Shape s = check_shape(ctx, kind, p, B);
+  arg(ctx, n >= 1 && theta && Kfull && (p == 0 || X) && (B == 1 || Z), "null argument");
+  SideBufs sb;
+  upload_side(ctx, sb, s, X, Z, n, n);
+  std::vector<double> tab = make_tab(theta, s);
+  DBuf dtab, dK, dC;
+  upload(ctx, dtab, tab.data(), tab.size(), "upload tables");
+  alloc(ctx, dK, (size_t)(n * n) * sizeof(double), "alloc Kfull");
+  if (Kel) alloc(ctx, dC, (size_t)(n * n * B) * sizeof(double), "alloc cube");
+  ck(ctx, launch_assembly(1, kind, s.PM, sb.view(n), sb.view(n), n, B, s.ZS, tab_view(dtab, s),
+                          0.0, dK.d(), n, Kel ? dC.d() : nullptr, ctx->stream),
+     "assembly");
+  download(ctx, Kfull, dK.d(), (size_t)(n * n), "download Kfull");
+  if (Kel) download(ctx, Kel, dC.d(), (size_t)(n * n * B), "download cube");
+  sync(ctx);
+  return ACE_OK;
+  ACE_CATCH
+}
+
+int ace_kernmat_cross(ace_ctx *ctx, int kind, int64_t n1, int64_t n2, int p, int B,
+                      const double *X1, const double *X2, const double *Z1, const double *Z2,
+                      const double *theta, double *Kfull, double *Kel) {
+  if (!ctx) return ACE_ERR_ARG;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  Shape s = check_shape(ctx, kind, p, B);
+  arg(ctx, n1 >= 1 && n2 >= 1 && theta && Kfull, "bad shape / null argument");
+  arg(ctx, (p == 0 || (X1 && X2)) && (B == 1 || (Z1 && Z2)), "null argument");
+  SideBufs s1, s2;
+  upload_side(ctx, s1, s, X1, Z1, n1, n1);
+  upload_side(ctx, s2, s, X2, Z2, n2, n2);
+  std::vector<double> tab = make_tab(theta, s);
+  DBuf dtab, dK, dC;
+  upload(ctx, dtab, tab.data(), tab.size(), "upload tables");
+  alloc(ctx, dK, (size_t)(n1 * n2) * sizeof(double), "alloc Kfull");
+  if (Kel) alloc(ctx, dC, (size_t)(n1 * n2 * B) * sizeof(double), "alloc cube");
+  ck(ctx, launch_assembly(2, kind, s.PM, s1.view(n1), s2.view(n2), 0, B, s.ZS,
+                          tab_view(dtab, s), 0.0, dK.d(), n1, Kel ? dC.d() : nullptr,
+                          ctx->stream),
+     "assembly");
+  download(ctx, Kfull, dK.d(), (size_t)(n1 * n2), "download Kfull");
+  if (Kel) download(ctx, Kel, dC.d(), (size_t)(n1 * n2 * B), "download cube");
+  sync(ctx);
+  return ACE_OK;
+  ACE_CATCH
+}
+
+// ------------------------------------------------------------ inverse
+namespace {
+struct SweepWork {
+  DBuf A, P, W, SW, S, piv, flag;
+  int64_t n = 0, npad = 0, naug = 0;
+  void ensure(ace_ctx *ctx, int64_t n_) {
+    n = n_;
+    npad = round_up(n, NB);
+    naug = npad + AUG;
+    alloc(ctx, A, (size_t)(naug * naug) * sizeof(double), "alloc A");
+    alloc(ctx, P, (size_t)(naug * NB) * sizeof(double), "alloc P");
+    alloc(ctx, W, (size_t)(naug * NB) * sizeof(double), "alloc W");
+    alloc(ctx, SW, (size_t)(SUB * SUB) * sizeof(double), "alloc SW");
+    alloc(ctx, S, (size_t)(SUB * NB) * sizeof(double), "alloc S");
+    alloc(ctx, piv, (size_t)npad * sizeof(double), "alloc piv");
+    alloc(ctx, flag, 16, "alloc flag");
+  }
+  SweepBufs bufs() const {
+    SweepBufs b;
+    b.A = A.d();
+    b.ld = naug;
+    b.npad = npad;
+    b.P = P.d();
+    b.W = W.d();
+    b.SW = SW.d();
+    b.S = S.d();
+    b.piv = piv.d();
+    b.flag = flag.i();
+    return b;
+  }
+};
+}  // namespace
+
+int ace_invkernel(ace_ctx *ctx, int64_t n, const double *K, double sigma, double *eigenval,
+                  double *inv) {
+  if (!ctx) return ACE_ERR_ARG;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, n >= 1 && K, "bad shape / null argument");
+  SweepWork w;
+  w.ensure(ctx, n);
+  DBuf dK;
+  upload(ctx, dK, K, (size_t)(n * n), "upload K");
+  ck(ctx, launch_prepare_A(dK.d(), n, std::exp(sigma), w.A.d(), w.naug, w.npad, ctx->stream),
+     "prepare A");
+  ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, 0, nullptr, ctx->stream), "aug init");
+  ck(ctx, hipMemsetAsync(w.flag.p, 0, sizeof(int), ctx->stream), "memset flag");
+  ck(ctx, run_sweep(w.bufs(), ctx->stream, nullptr, 0, nullptr), "sweep");
+  int flag = 0;
+  ck(ctx, hipMemcpyAsync(&flag, w.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
+     "download flag");
+  if (inv) {
+    ck(ctx, launch_sym_from_lower(w.A.d(), w.naug, n, -1.0, dK.d(), n, ctx->stream),
+       "symmetrize");
+    download(ctx, inv, dK.d(), (size_t)(n * n), "download inv");
+  }
+  if (eigenval) download(ctx, eigenval, w.piv.d(), (size_t)n, "download pivots");
+  sync(ctx);
+  if (flag && inv)  // not positive definite: the reference's inverse is NaN
+    for (int64_t j = 0; j < n * n; ++j) inv[j] = kNaN;
+  return ACE_OK;
+  ACE_CATCH
+}
+
+// ------------------------------------------------------------ gradient
+int ace_grad(ace_ctx *ctx, int kind, int64_t n, int p, int B, const double *y, const double *X,
+             const double *Z, const double *Kfull, const double *Kel, const double *inv,
+             const double *eigenval, const double *theta, double *stats, double std_y,
+             double *grad) {
+  if (!ctx) return ACE_ERR_ARG;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  Shape s = check_shape(ctx, kind, p, B);
+  arg(ctx, n >= 1 && y && Kfull && inv && eigenval && theta && stats && grad, "null argument");
+  arg(ctx, (p == 0 || X) && (B == 1 || Z), "null argument");
+  SideBufs sb;
+  upload_side(ctx, sb, s, X, Z, n, n);
+  std::vector<double> tab = make_tab(theta, s);
+  std::vector<double> ybar((size_t)n);
+  for (int64_t r = 0; r < n; ++r) ybar[(size_t)r] = y[r] - theta[1];
+  DBuf dtab, dy, dyb, dinv, dKf, dC, dalpha, ds, dg, dtr, dgs, dsums, dmu;
+  upload(ctx, dtab, tab.data(), tab.size(), "upload tables");
+  upload(ctx, dy, y, (size_t)n, "upload y");
+  upload(ctx, dyb, ybar.data(), (size_t)n, "upload ybar");
+  upload(ctx, dinv, inv, (size_t)(n * n), "upload inv");
+  upload(ctx, dKf, Kfull, (size_t)(n * n), "upload Kfull");
+  if (Kel) upload(ctx, dC, Kel, (size_t)(n * n * B), "upload cube");
+  upload(ctx, dmu, &theta[1], 1, "upload mu");
+  alloc(ctx, dalpha, (size_t)n * sizeof(double), "alloc alpha");
+  alloc(ctx, ds, (size_t)n * sizeof(double), "alloc s");
+  const int64_t nt = grad_ntiles(n);
+  const int ncol = B * (s.PM + 1);
+  alloc(ctx, dg, (size_t)(nt * ncol) * sizeof(double), "alloc gpart");
+  alloc(ctx, dtr, (size_t)nt * sizeof(double), "alloc trpart");
+  alloc(ctx, dgs, (size_t)(ncol + 1) * sizeof(double), "alloc gsum");
+  alloc(ctx, dsums, 8 * sizeof(double), "alloc sums");
+  // alpha = invKmatn * ybar (src/kernel_SE_cpp.cpp:215)
+  ck(ctx, launch_gemv(dinv.d(), n, n, n, dyb.d(), dalpha.d(), ctx->stream), "gemv alpha");
+  ck(ctx, launch_grad(kind, s.PM, sb.view(n), B, s.ZS, tab_view(dtab, s), dinv.d(), n, 1.0,
+                      dalpha.d(), Kel ? dC.d() : nullptr, dg.d(), dtr.d(), nullptr, n,
+                      ctx->stream),
+     "grad");
+  ck(ctx, launch_colsum(dg.d(), nt, ncol, dgs.d(), ctx->stream), "colsum");
+  ck(ctx, launch_colsum(dtr.d(), nt, 1, dgs.d() + ncol, ctx->stream), "colsum tr");
+  // Kfull * alpha for the RMSE (src/kernel_SE_cpp.cpp:238)
+  ck(ctx, launch_gemv(dKf.d(), n, n, n, dalpha.d(), ds.d(), ctx->stream), "gemv K alpha");
+  ck(ctx, launch_final_sums(dy.d(), dmu.d(), dalpha.d(), ds.d(), n, nullptr, 0, dsums.d(),
+                            ctx->stream),
+     "final sums");
+  std::vector<double> gs((size_t)(ncol + 1)), sums(8);
+  download(ctx, gs.data(), dgs.d(), gs.size(), "download gsum");
+  download(ctx, sums.data(), dsums.d(), 4, "download sums");
+  sync(ctx);
+  compose_grad(s, theta, gs.data(), sums[2], grad);
+  const double logdet = host_logsum(eigenval, n);
+  stats[0] = std_y * std::sqrt(sums[0]) / std::sqrt((double)n);
+  stats[1] = -0.5 * (n * std::log(2.0 * M_PI) + logdet + sums[1]);
+  return ACE_OK;
+  ACE_CATCH
+}
+
+int ace_stats(ace_ctx *ctx, int64_t n, const double *y, const double *Kmat, const double *inv,
+              const double *eigenval, double mu, double std_y, double *out) {
+  if (!ctx) return ACE_ERR_ARG;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, n >= 1 && y && Kmat && inv && eigenval && out, "null argument");
+  std::vector<double> ybar((size_t)n);
+  for (int64_t r = 0; r < n; ++r) ybar[(size_t)r] = y[r] - mu;
+  DBuf dy, dyb, dinv, dK, dalpha, ds, dsums, dmu;
+  upload(ctx, dy, y, (size_t)n, "upload y");
+  upload(ctx, dyb, ybar.data(), (size_t)n, "upload ybar");
+  upload(ctx, dinv, inv, (size_t)(n * n), "upload inv");
+  upload(ctx, dK, Kmat, (size_t)(n * n), "upload K");
+  upload(ctx, dmu, &mu, 1, "upload mu");
+  alloc(ctx, dalpha, (size_t)n * sizeof(double), "alloc");
+  alloc(ctx, ds, (size_t)n * sizeof(double), "alloc");
+  alloc(ctx, dsums, 8 * sizeof(double), "alloc");
+  ck(ctx, launch_gemv(dinv.d(), n, n, n, dyb.d(), dalpha.d(), ctx->stream), "gemv");
+  ck(ctx, launch_gemv(dK.d(), n, n, n, dalpha.d(), ds.d(), ctx->stream), "gemv");
+  ck(ctx, launch_final_sums(dy.d(), dmu.d(), dalpha.d(), ds.d(), n, nullptr, 0, dsums.d(),
+                            ctx->stream),
+     "sums");
+  double sums[4];
+  download(ctx, sums, dsums.d(), 4, "download");
+  sync(ctx);
+  out[0] = std_y * std::sqrt(sums[0]) / std::sqrt((double)n);
+  out[1] = -0.5 * (n * std::log(2.0 * M_PI) + host_logsum(eigenval, n) + sums[1]);
+  return ACE_OK;
+  ACE_CATCH
+}
+
+int ace_mu_solution(ace_ctx *ctx, int64_t n, const double *y, const double *inv, double *out) {
+  if (!ctx) return ACE_ERR_ARG;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, n >= 1 && y && inv && out, "null argument");
+  DBuf dy, dinv, dt, dcs;
+  upload(ctx, dy, y, (size_t)n, "upload y");
+  upload(ctx, dinv, inv, (size_t)(n * n), "upload inv");
+  alloc(ctx, dt, (size_t)n * sizeof(double), "alloc");
+  alloc(ctx, dcs, (size_t)n * sizeof(double), "alloc");
+  ck(ctx, launch_gemv(dinv.d(), n, n, n, dy.d(), dt.d(), ctx->stream), "gemv");
+  ck(ctx, launch_colsum(dinv.d(), n, (int)n, dcs.d(), ctx->stream), "colsum");
+  std::vector<double> t((size_t)n), cs((size_t)n);
+  download(ctx, t.data(), dt.d(), (size_t)n, "download");
+  download(ctx, cs.data(), dcs.d(), (size_t)n, "download");
+  sync(ctx);
+  double st = 0.0, sa = 0.0;
+  for (int64_t j = 0; j < n; ++j) {
+    st += t[(size_t)j];
+    sa += cs[(size_t)j];
+  }
+  *out = 0.5 * st / sa;  // Q4
+  return ACE_OK;
+  ACE_CATCH
+}
+
+// ------------------------------------------------------------ prediction
+int ace_pred(ace_ctx *ctx, int64_t nX, int64_t nx, const double *y_X, double sigma, double mu,
+             const double *invK_XX, const double *K_xX, const double *K_xx, double mean_y,
+             double std_y, double *map, double *ci, double *var) {
+  if (!ctx) return ACE_ERR_ARG;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, nX >= 1 && nx >= 1 && y_X && invK_XX && K_xX && K_xx && map && ci && var,
+      "null argument");
+  std::vector<double> w((size_t)nX);
+  for (int64_t c = 0; c < nX; ++c) w[(size_t)c] = y_X[c] - mu;
+  DBuf dinv, dK, dT, dw, da, dq;
+  upload(ctx, dinv, invK_XX, (size_t)(nX * nX), "upload inv");
+  upload(ctx, dK, K_xX, (size_t)(nx * nX), "upload K_xX");
+  upload(ctx, dw, w.data(), (size_t)nX, "upload w");
+  alloc(ctx, dT, (size_t)(nx * nX) * sizeof(double), "alloc tmp");
+  alloc(ctx, da, (size_t)nx * sizeof(double), "alloc");
+  alloc(ctx, dq, (size_t)nx * sizeof(double), "alloc");
+  // tmp = K_xX * invK_XX (src/pred_cpp.cpp:19)
+  ck(ctx, launch_gemm_nn(nx, nX, nX, dK.d(), nx, dinv.d(), nX, dT.d(), nx, ctx->stream), "gemm");
+  ck(ctx, launch_pred_rows(dT.d(), dK.d(), nx, nx, nX, dw.d(), da.d(), dq.d(), ctx->stream),
+     "pred rows");
+  std::vector<double> a((size_t)nx), q((size_t)nx);
+  download(ctx, a.data(), da.d(), (size_t)nx, "download");
+  download(ctx, q.data(), dq.d(), (size_t)nx, "download");
+  sync(ctx);
+  const double es = std::exp(sigma);
+  for (int64_t r = 0; r < nx; ++r) {
+    const double yx = mean_y + std_y * (a[(size_t)r] + mu);
+    const double d = (K_xx[r + r * nx] - q[(size_t)r]) + es;
+    const double sd = std_y * std::sqrt(std::fabs(d));
+    map[r] = yx;
+    ci[r] = yx - 1.96 * sd;
+    ci[r + nx] = yx + 1.96 * sd;
+    var[r] = std::pow(sd, 2);
+  }
+  return ACE_OK;
+  ACE_CATCH
+}
+
+int ace_pred_marginal(ace_ctx *ctx, int64_t nX, int64_t nx, int B, const double *y_X,
+                      const double *Z_x, double sigma, double mu, const double *invK_XX,
+                      const double *K_xX, const double *K_xx, double mean_y, double std_y,
+                      double std_Z, int calculate_ate, double *map, double *ci, double *var,
+                      double *avg) {
+  (void)sigma;
+  (void)mean_y;
+  if (!ctx) return ACE_ERR_ARG;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, nX >= 1 && nx >= 1 && B >= 1 && y_X && invK_XX && K_xX && K_xx && map && ci && var,
+      "null argument");
+  arg(ctx, !calculate_ate || (Z_x && avg), "calculate_ate needs Z_x and avg");
+  std::vector<double> w((size_t)nX);
+  for (int64_t c = 0; c < nX; ++c) w[(size_t)c] = y_X[c] - mu;
+  DBuf dinv, dcX, dcx, dmX, dmx, dT, dw, da, dq;
+  upload(ctx, dinv, invK_XX, (size_t)(nX * nX), "upload inv");
+  upload(ctx, dcX, K_xX, (size_t)(nx * nX * B), "upload K_xX");
+  upload(ctx, dcx, K_xx, (size_t)(nx * nx * B), "upload K_xx");
+  upload(ctx, dw, w.data(), (size_t)nX, "upload w");
+  alloc(ctx, dmX, (size_t)(nx * nX) * sizeof(double), "alloc");
+  alloc(ctx, dmx, (size_t)(nx * nx) * sizeof(double), "alloc");
+  alloc(ctx, dT, (size_t)(nx * nX) * sizeof(double), "alloc");
+  alloc(ctx, da, (size_t)nx * sizeof(double), "alloc");
+  alloc(ctx, dq, (size_t)nx * sizeof(double), "alloc");
+  ck(ctx, launch_marginal_sum(dcX.d(), nx, nX, B, dmX.d(), ctx->stream), "marginal sum");
+  ck(ctx, launch_marginal_sum(dcx.d(), nx, nx, B, dmx.d(), ctx->stream), "marginal sum");
+  ck(ctx, launch_gemm_nn(nx, nX, nX, dmX.d(), nx, dinv.d(), nX, dT.d(), nx, ctx->stream),
+     "gemm");
+  ck(ctx, launch_pred_rows(dT.d(), dmX.d(), nx, nx, nX, dw.d(), da.d(), dq.d(), ctx->stream),
+     "pred rows");
+  std::vector<double> a((size_t)nx), q((size_t)nx), dg((size_t)nx);
+  download(ctx, a.data(), da.d(), (size_t)nx, "download");
+  download(ctx, q.data(), dq.d(), (size_t)nx, "download");
+  ck(ctx, hipMemcpy2DAsync(dg.data(), sizeof(double), dmx.d(), (size_t)(nx + 1) * sizeof(double),
+                           sizeof(double), (size_t)nx, hipMemcpyDeviceToHost, ctx->stream),
+     "download diag");
+  std::vector<double> q3(3), tw((size_t)(3 * nX)), kw((size_t)(3 * nX));
+  DBuf dW3, dq3, dtw, dkw;
+  std::vector<double> zx;
+  if (calculate_ate) {
+    zx.assign(Z_x, Z_x + nx);
+    std::vector<double> W3((size_t)(3 * nx));
+    for (int64_t r = 0; r < nx; ++r) {
+      W3[(size_t)r] = 1.0;
+      W3[(size_t)(nx + r)] = zx[(size_t)r];
+      W3[(size_t)(2 * nx + r)] = (zx[(size_t)r] == 0) ? 1.0 : 0.0;
+    }
+    upload(ctx, dW3, W3.data(), W3.size(), "upload weights");
+    alloc(ctx, dq3, (size_t)(3 * nx + 3) * sizeof(double), "alloc");
+    alloc(ctx, dtw, (size_t)(3 * nX) * sizeof(double), "alloc");
+    alloc(ctx, dkw, (size_t)(3 * nX) * sizeof(double), "alloc");
+    ck(ctx, launch_quad3(dmx.d(), nx, nx, dW3.d(), dq3.d(), ctx->stream), "quad3");
+    for (int j = 0; j < 3; ++j) {
+      ck(ctx, launch_gemv_t(dT.d(), nx, nx, nX, dW3.d() + j * nx, dtw.d() + j * nX, ctx->stream),
+         "gemv_t");
+      ck(ctx, launch_gemv_t(dmX.d(), nx, nx, nX, dW3.d() + j * nx, dkw.d() + j * nX,
+                            ctx->stream),
+         "gemv_t");
+    }
+    download(ctx, q3.data(), dq3.d(), 3, "download");
+    download(ctx, tw.data(), dtw.d(), tw.size(), "download");
+    download(ctx, kw.data(), dkw.d(), kw.size(), "download");
+  }
+  sync(ctx);
+  std::vector<double> yx((size_t)nx);
+  for (int64_t r = 0; r < nx; ++r) {
+    yx[(size_t)r] = std_y * a[(size_t)r] / std_Z;
+    const double d = dg[(size_t)r] - q[(size_t)r];
+    const double sd = std_y * std::sqrt(std::fabs(d)) / std_Z;
+    map[r] = yx[(size_t)r];
+    ci[r] = yx[(size_t)r] - 1.96 * sd;
+    ci[r + nx] = yx[(size_t)r] + 1.96 * sd;
+    var[r] = std::pow(sd, 2);
+  }
+  if (calculate_ate) {
+    // posterior quadratic forms w^T (Km_xx - tmp Km_xX^T) w (src/pred_cpp.cpp:89-106)
+    double post[3];
+    for (int j = 0; j < 3; ++j) {
+      double cross = 0.0;
+      for (int64_t c = 0; c < nX; ++c) cross += tw[(size_t)(j * nX + c)] * kw[(size_t)(j * nX + c)];
+      post[j] = q3[(size_t)j] - cross;
+    }
+    double sy = 0.0, syz = 0.0, sz = 0.0;
+    for (int64_t r = 0; r < nx; ++r) {
+      sy += yx[(size_t)r];
+      syz += yx[(size_t)r] * zx[(size_t)r];
+      sz += zx[(size_t)r];
+    }
+    const double ate = sy / (double)nx;
+    double ate_sd = std_y * std::sqrt(post[0]) / (double)nx;
+    const unsigned int ntx = (unsigned int)sz;  // unsigned int in the reference
+    const double att = syz / ntx;
+    double att_sd = std_y * std::sqrt(post[1]) / ntx;
+    const unsigned int nux = (unsigned int)nx - ntx;
+    const double atu = (ate * nx - att * ntx) / nux;
+    double atu_sd = std_y * std::sqrt(post[2]) / nux;
+    const double m3[3] = {ate, att, atu}, s3[3] = {ate_sd, att_sd, atu_sd};
+    for (int j = 0; j < 3; ++j) {
+      avg[4 * j + 0] = m3[j];
+      avg[4 * j + 1] = m3[j] - 1.96 * s3[j];
+      avg[4 * j + 2] = m3[j] + 1.96 * s3[j];
+      avg[4 * j + 3] = std::pow(s3[j], 2);
+    }
+  }
+  return ACE_OK;
+  ACE_CATCH
+}
+
+}  // extern "C"
+
+// =====================================================================
+// Device-resident model: one para_update per call, nothing materialised
+// beyond A (the swept matrix) and O(n * tiles) partial sums.
+// =====================================================================
+struct ace_model {
+  ace_ctx *ctx = nullptr;
+  Shape s{};
+  int64_t n = 0, npad = 0, naug = 0, ntiles = 0, ntr = 0;
+  double std_y = 1.0;
+  bool has_data = false;
+  SideBufs side;
+  DBuf y, tab, alpha, scal, gpart, trpart, kapart, ka, gsum, sums;
+  SweepWork sw;   // A = resident inverse of the last para_update
+  SweepWork sw2;  // train_stats scratch (keeps sw's inverse, Q6)
+  bool prof = false;
+  hipEvent_t ev_asm[2] = {nullptr, nullptr}, ev_grad[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> ev_upd;
+  double t_ms[3] = {0, 0, 0};
+  int64_t t_launch[3] = {0, 0, 0};
+  double t_work[3] = {0, 0, 0};
+};
+
+namespace {
+
+void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu, bool timed) {
+  ace_ctx *ctx = m->ctx;
+  hipStream_t st = ctx->stream;
+  const Shape &s = m->s;
+  std::vector<double> tab = make_tab(theta, s);
+  ck(ctx, hipMemcpy(m->tab.p, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice),
+     "upload tables");
+  const TabView tv = tab_view(m->tab, s);
+  const PairSide ps = m->side.view(m->n);
+  if (timed) ck(ctx, hipEventRecord(m->ev_asm[0], st), "event");
+  ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, std::exp(theta[0]),
+                          w.A.d(), w.naug, nullptr, st),
+     "assembly");
+  if (timed) ck(ctx, hipEventRecord(m->ev_asm[1], st), "event");
+  ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, m->n, m->y.d(), st), "aug init");
+  ck(ctx, hipMemsetAsync(w.flag.p, 0, sizeof(int), st), "memset flag");
+  int used = 0;
+  ck(ctx, run_sweep(w.bufs(), st, timed ? m->ev_upd.data() : nullptr,
+                    timed ? (int)m->ev_upd.size() : 0, &used),
+     "sweep");
+  ck(ctx, launch_alpha_from_aug(w.A.d(), w.naug, w.npad, m->n, theta[1], use_mu, m->alpha.d(),
+                                m->scal.d(), st),
+     "alpha");
+  if (timed) ck(ctx, hipEventRecord(m->ev_grad[0], st), "event");
+  ck(ctx, launch_grad(s.kind, s.PM, ps, s.B, s.ZS, tv, w.A.d(), w.naug, -1.0, m->alpha.d(),
+                      nullptr, m->gpart.d(), m->trpart.d(), m->kapart.d(), w.npad, st),
+     "grad");
+  if (timed) ck(ctx, hipEventRecord(m->ev_grad[1], st), "event");
+  const int ncol = s.B * (s.PM + 1);
+  ck(ctx, launch_colsum(m->gpart.d(), m->ntiles, ncol, m->gsum.d(), st), "colsum");
+  ck(ctx, launch_colsum(m->trpart.d(), m->ntiles, 1, m->gsum.d() + ncol, st), "colsum");
+  ck(ctx, launch_rowsum(m->kapart.d(), m->ntr, w.npad, m->n, m->ka.d(), st), "rowsum");
+  ck(ctx, launch_final_sums(m->y.d(), m->scal.d() + 4, m->alpha.d(), m->ka.d(), m->n, w.piv.d(),
+                            w.npad, m->sums.d(), st),
+     "final sums");
+  (void)used;
+}
+
+void model_collect_timing(ace_model *m, int nupd) {
+  float ms = 0.f;
+  ck(m->ctx, hipEventElapsedTime(&ms, m->ev_asm[0], m->ev_asm[1]), "elapsed");
+  m->t_ms[1] += ms;
+  m->t_launch[1] += 1;
+  ck(m->ctx, hipEventElapsedTime(&ms, m->ev_grad[0], m->ev_grad[1]), "elapsed");
+  m->t_ms[2] += ms;
+  m->t_launch[2] += 1;
+  for (int j = 0; j + 1 < nupd; j += 2) {
+    ck(m->ctx, hipEventElapsedTime(&ms, m->ev_upd[(size_t)j], m->ev_upd[(size_t)j + 1]),
+       "elapsed");
+    m->t_ms[0] += ms;
+    m->t_launch[0] += 1;
+  }
+  const double n = (double)m->n, pairs = n * (n + 1) / 2, B = m->s.B, p = m->s.p;
+  // algorithmic work: dense n^3 over the update launches,
+  // pair kernels by their flop formulas
+  m->t_work[0] += n * n * n;
+  m->t_work[1] += pairs * B * (3 * p + 3);
+  m->t_work[2] += pairs * (4 * B * p + 2 * p) + (m->s.kind == ACE_KERNEL_MATERN32 ? pairs * B * p : 0);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model **out) {
+  if (!ctx || !out) return ACE_ERR_ARG;
+  *out = nullptr;
+  ace_model *m = new ace_model();
+  m->ctx = ctx;
+  try {
+    ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    m->s = check_shape(ctx, kind, p, B);
+    arg(ctx, n >= 2, "n must be >= 2");
+    m->n = n;
+    m->sw.ensure(ctx, n);
+    m->npad = m->sw.npad;
+    m->naug = m->sw.naug;
+    m->ntiles = grad_ntiles(n);
+    m->ntr = (n + AT - 1) / AT;
+    const Shape &s = m->s;
+    alloc(ctx, m->y, (size_t)m->npad * sizeof(double), "alloc y");
+    alloc(ctx, m->tab, (size_t)(2 * s.B * s.PM + s.B) * sizeof(double), "alloc tab");
+    alloc(ctx, m->alpha, (size_t)m->npad * sizeof(double), "alloc alpha");
+    alloc(ctx, m->scal, 16 * sizeof(double), "alloc scal");
+    alloc(ctx, m->gpart, (size_t)(m->ntiles * s.B * (s.PM + 1)) * sizeof(double), "alloc gpart");
+    alloc(ctx, m->trpart, (size_t)m->ntiles * sizeof(double), "alloc trpart");
+    alloc(ctx, m->kapart, (size_t)(m->ntr * m->npad) * sizeof(double), "alloc kapart");
+    alloc(ctx, m->ka, (size_t)m->npad * sizeof(double), "alloc ka");
+    alloc(ctx, m->gsum, (size_t)(s.B * (s.PM + 1) + 1) * sizeof(double), "alloc gsum");
+    alloc(ctx, m->sums, 8 * sizeof(double), "alloc sums");
+    ck(ctx, hipMemsetAsync(m->sw.A.p, 0, m->sw.A.bytes, ctx->stream), "memset A");
+    const int steps = (int)(m->npad / NB);
+    m->ev_upd.assign((size_t)(2 * steps), nullptr);
+    for (auto &e : m->ev_upd) ck(ctx, hipEventCreate(&e), "event");
+    for (int j = 0; j < 2; ++j) {
+      ck(ctx, hipEventCreate(&m->ev_asm[j]), "event");
+      ck(ctx, hipEventCreate(&m->ev_grad[j]), "event");
+    }
+    sync(ctx);
+  } catch (const Fail &f) {
+    ace_model_destroy(m);
+    return f.code;
+  }
+  *out = m;
+  return ACE_OK;
+}
+
+void ace_model_destroy(ace_model *m) {
+  if (!m) return;
+  (void)hipSetDevice(m->ctx->device);
+  for (auto &e : m->ev_upd)
+    if (e) (void)hipEventDestroy(e);
+  for (int j = 0; j < 2; ++j) {
+    if (m->ev_asm[j]) (void)hipEventDestroy(m->ev_asm[j]);
+    if (m->ev_grad[j]) (void)hipEventDestroy(m->ev_grad[j]);
+  }
+  delete m;
+}
+
+int ace_model_set_data(ace_model *m, const double *y, const double *X, const double *Z,
+                       double std_y) {
+  if (!m) return ACE_ERR_ARG;
+  ace_ctx *ctx = m->ctx;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, y && (m->s.p == 0 || X) && (m->s.B == 1 || Z), "null argument");
+  upload_side(ctx, m->side, m->s, X, Z, m->n, m->npad);
+  std::vector<double> yp((size_t)m->npad, 0.0);
+  std::copy(y, y + m->n, yp.begin());
+  ck(ctx, hipMemcpy(m->y.p, yp.data(), yp.size() * sizeof(double), hipMemcpyHostToDevice),
+     "upload y");
+  m->std_y = std_y;
+  sync(ctx);
+  m->has_data = true;
+  return ACE_OK;
+  ACE_CATCH
+}
+
+int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, double *stats,
+                          double *mu_post) {
+  if (!m) return ACE_ERR_ARG;
+  ace_ctx *ctx = m->ctx;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, m->has_data, "ace_model_set_data() not called");
+  arg(ctx, theta && grad && stats, "null argument");
+  const Shape &s = m->s;
+  const bool timed = m->prof;
+  model_pipeline(m, m->sw, theta, iter == 1 ? 1 : 0, timed);
+  const int ncol = s.B * (s.PM + 1);
+  std::vector<double> gs((size_t)(ncol + 1));
+  double sums[4], scal[5];
+  int flag = 0;
+  download(ctx, gs.data(), m->gsum.d(), gs.size(), "download gsum");
+  download(ctx, sums, m->sums.d(), 4, "download sums");
+  download(ctx, scal, m->scal.d(), 5, "download scal");
+  ck(ctx, hipMemcpyAsync(&flag, m->sw.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
+     "download flag");
+  sync(ctx);
+  if (timed) model_collect_timing(m, (int)m->ev_upd.size());
+  if (iter == 1) theta[1] = scal[3];  // mean_solution before the gradient (R/kernel_SE_R6.R:45)
+  compose_grad(s, theta, gs.data(), sums[2], grad);
+  stats[0] = m->std_y * std::sqrt(sums[0]) / std::sqrt((double)m->n);
+  stats[1] = -0.5 * (m->n * std::log(2.0 * M_PI) + sums[3] + sums[1]);
+  if (mu_post) *mu_post = scal[3];
+  if (flag) {  // not positive definite: the reference's outputs are non-finite
+    const int P = 2 + s.B * (s.p + 1);
+    for (int j = 0; j < P; ++j) grad[j] = kNaN;
+    stats[0] = stats[1] = kNaN;
+    if (mu_post) *mu_post = kNaN;
+  }
+  return ACE_OK;
+  ACE_CATCH
+}
+
+int ace_model_train_stats(ace_model *m, const double *theta, double *stats) {
+  if (!m) return ACE_ERR_ARG;
+  ace_ctx *ctx = m->ctx;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, m->has_data && theta && stats, "null argument / no data");
+  m->sw2.ensure(ctx, m->n);
+  model_pipeline(m, m->sw2, theta, 0, false);
+  double sums[4];
+  int flag = 0;
+  download(ctx, sums, m->sums.d(), 4, "download sums");
+  ck(ctx, hipMemcpyAsync(&flag, m->sw2.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
+     "download flag");
+  sync(ctx);
+  stats[0] = m->std_y * std::sqrt(sums[0]) / std::sqrt((double)m->n);
+  stats[1] = -0.5 * (m->n * std::log(2.0 * M_PI) + sums[3] + sums[1]);
+  if (flag) stats[0] = stats[1] = kNaN;
+  return ACE_OK;
+  ACE_CATCH
+}
+
+int ace_model_get_inverse(ace_model *m, double *inv) {
+  if (!m) return ACE_ERR_ARG;
+  ace_ctx *ctx = m->ctx;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, inv != nullptr, "null argument");
+  DBuf out;
+  alloc(ctx, out, (size_t)(m->n * m->n) * sizeof(double), "alloc inverse");
+  ck(ctx, launch_sym_from_lower(m->sw.A.d(), m->naug, m->n, -1.0, out.d(), m->n, ctx->stream),
+     "symmetrize");
+  download(ctx, inv, out.d(), (size_t)(m->n * m->n), "download inverse");
+  sync(ctx);
+  return ACE_OK;
+  ACE_CATCH
+}
+
+int ace_model_profile(ace_model *m, int enable) {
+  if (!m) return ACE_ERR_ARG;
+  m->prof = enable != 0;
+  for (int j = 0; j < 3; ++j) {
+    m->t_ms[j] = 0;
+    m->t_launch[j] = 0;
+    m->t_work[j] = 0;
+  }
+  return ACE_OK;
+}
+
+int ace_model_kernel_time(ace_model *m, int which, double *ms, int64_t *launches, double *work) {
+  if (!m || which < 0 || which > 2) return ACE_ERR_ARG;
+  if (ms) *ms = m->t_ms[which];
+  if (launches) *launches = m->t_launch[which];
+  if (work) *work = m->t_work[which];
+  return ACE_OK;
+}
+
+}  // extern "C"

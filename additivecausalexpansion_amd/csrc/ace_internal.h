@@ -1,0 +1,128 @@
+// ace_internal.h -- shared declarations between the HIP kernels
+// (ace_kernels.hip, ace_sweep.hip) and the host orchestration (ace_api.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ace {
+
+// Sweep (Gauss-Jordan SPD inversion) blocking; see DESIGN.md §3.
+constexpr int NB = 256;    // outer pivot block = panel width
+constexpr int SUB = 64;    // inner pivot block, eliminated inside LDS
+constexpr int UT = 128;    // update tile (MFMA f64 16x16x4, 4 waves x 64x64)
+constexpr int AUG = 128;   // augmented right-hand-side rows (y, 1) appended to A
+constexpr int AT = 64;     // assembly / gradient pair tile
+constexpr int PMAX = 64;   // largest supported covariate count p
+constexpr int BMAX = 32;   // largest supported component count B
+
+// Feature-count buckets the pair kernels are compiled for.
+int pm_bucket(int p);  // smallest compiled bucket >= p, or -1
+
+// Per-theta tables, b-major: wk[b*PM+i] = exp(-theta[1+b+B*(i+1)]) (kernel
+// index, Q1), wg[b*PM+i] = exp(-theta[2+B+b+B*i]) (gradient index),
+// lam[b] = theta[2+b].  Total 2*B*PM + B doubles.
+struct TabView {
+  const double *wk, *wg, *lam;
+};
+
+// Row-side / column-side operand of a pair kernel (row-major, padded).
+struct PairSide {
+  const double *X;   // nrows x PM
+  const double *Z;   // nrows x ZS   (basis columns 1..B-1)
+  const double *LZ;  // nrows x ZS   log|z| (SE only; may be null for Matern)
+  int64_t n;         // valid rows
+};
+
+// ---- assembly --------------------------------------------------------------
+// mode 0: fused eval -- lower 64-tiles of the n_pad x n_pad block of A (ld),
+//         value K + sig on the diagonal, identity on padding rows/cols.
+// mode 1: symmetric ABI output -- full n x n Kfull (ld = n) + optional cube.
+// mode 2: cross ABI output -- n1 x n2 Kfull + optional cube.
+hipError_t launch_assembly(int mode, int kind, int PM, PairSide rows,
+                           PairSide cols, int64_t npad, int B, int ZS,
+                           TabView tab, double sig, double *out, int64_t ld,
+                           double *cube, hipStream_t st);
+
+// ---- gradient --------------------------------------------------------------
+// T = sA * A[r,c] - alpha_r alpha_c over lower 64-tiles of [0,n).
+// gpart: [(b*(PM+1) + i) * ntiles + tile]  (i < PM: length-scale sums,
+//        i == PM: lambda sums); trpart[tile]: trace of T;
+// kapart (if non-null): [T * npad + x], partial rows of Kfull * alpha.
+// cube (if non-null, ld n): K_b read from the cube instead of recomputed.
+hipError_t launch_grad(int kind, int PM, PairSide side, int B, int ZS,
+                       TabView tab, const double *A, int64_t ld, double sA,
+                       const double *alpha, const double *cube,
+                       double *gpart, double *trpart, double *kapart,
+                       int64_t npad, hipStream_t st);
+int64_t grad_ntiles(int64_t n);
+
+// ---- sweep -----------------------------------------------------------------
+struct SweepBufs {
+  double *A;      // Naug x Naug, col-major, ld = Naug, lower triangle used
+  int64_t ld;     // Naug
+  int64_t npad;   // multiple of NB
+  double *P;      // Naug x NB : -panel (negated copy)
+  double *W;      // Naug x NB : panel being swept
+  double *SW;     // SUB x SUB
+  double *S;      // SUB x NB  : pivot rows before their sub-sweep
+  double *piv;    // npad pivots
+  int *flag;      // set to 1 on a non-positive / non-finite pivot
+};
+// Runs every step; A's K block ends holding -A^-1 (lower), the AUG rows hold
+// (A^-1 R)^T and the corner -R^T A^-1 R.  `update_ms` (nullable) receives
+// per-launch events of the update kernel when `ev` is non-null.
+hipError_t run_sweep(const SweepBufs &b, hipStream_t st, hipEvent_t *ev,
+                     int nev, int *nev_used);
+// flops of one sweep's update-kernel launches (algorithmic, lower tiles)
+double sweep_update_flops(int64_t naug);
+
+// ---- small helpers -----------------------------------------------------------
+hipError_t launch_aug_init(double *A, int64_t ld, int64_t npad, int64_t n,
+                           const double *y, hipStream_t st);
+// alpha = u - mu_eff * v, u/v read from A's AUG rows; mu_eff = theta1, or
+// 0.5*yK1/1K1 when use_mu_solution; writes scal[0..2] = {yKy, yK1, 1K1},
+// scal[3] = mu_solution, scal[4] = mu_eff.
+hipError_t launch_alpha_from_aug(const double *A, int64_t ld, int64_t npad,
+                                 int64_t n, double theta1, int use_mu_solution,
+                                 double *alpha, double *scal, hipStream_t st);
+hipError_t launch_colsum(const double *in, int64_t nrows, int ncols,
+                         double *out, hipStream_t st);
+hipError_t launch_rowsum(const double *in, int64_t ntile_rows, int64_t npad,
+                         int64_t n, double *out, hipStream_t st);
+// sums[0] = sum (ybar - s)^2, sums[1] = sum y*alpha, sums[2] = sum alpha,
+// sums[3] = sum log(piv[0..npiv)), with ybar = y - *mu (device scalar).
+hipError_t launch_final_sums(const double *y, const double *mu, const double *alpha,
+                             const double *s, int64_t n, const double *piv,
+                             int64_t npiv, double *sums, hipStream_t st);
+// y = M x for M (m x k, col-major ld) ; y = M^T x
+hipError_t launch_gemv(const double *M, int64_t ld, int64_t m, int64_t k,
+                       const double *x, double *y, hipStream_t st);
+hipError_t launch_gemv_t(const double *M, int64_t ld, int64_t m, int64_t k,
+                         const double *x, double *y, hipStream_t st);
+// C (m x n) = A (m x k) * B (k x n), col-major, fp64 MFMA.
+hipError_t launch_gemm_nn(int64_t m, int64_t n, int64_t k, const double *A,
+                          int64_t lda, const double *B, int64_t ldb, double *C,
+                          int64_t ldc, hipStream_t st);
+// Copies -A (lower) into a full symmetric n x n matrix (ld_out).
+hipError_t launch_sym_from_lower(const double *A, int64_t ld, int64_t n,
+                                 double scale, double *out, int64_t ld_out,
+                                 hipStream_t st);
+// dst[0:npad, 0:npad] (ld_dst) = src (n x n, ld n) + diag I, identity padding
+hipError_t launch_prepare_A(const double *src, int64_t n, double diag,
+                            double *dst, int64_t ld_dst, int64_t npad,
+                            hipStream_t st);
+hipError_t launch_fill(double *p, int64_t count, double v, hipStream_t st);
+// Sum over b>=1 of cube slices (or slice 0 when B == 1): out m x n.
+hipError_t launch_marginal_sum(const double *cube, int64_t m, int64_t n,
+                               int B, double *out, hipStream_t st);
+// Prediction rows: for r < nx: a = sum_c T[r,c] w[c]; q = sum_c T[r,c] K[r,c]
+hipError_t launch_pred_rows(const double *T, const double *K, int64_t ld,
+                            int64_t nx, int64_t nX, const double *w,
+                            double *a, double *q, hipStream_t st);
+// q[j] = w_j^T M w_j for three weight vectors packed in W (n x 3)
+hipError_t launch_quad3(const double *M, int64_t ld, int64_t n,
+                        const double *W, double *q, hipStream_t st);
+hipError_t launch_log_abs(const double *Z, double *LZ, int64_t count,
+                          hipStream_t st);
+
+}  // namespace ace

@@ -1,0 +1,393 @@
+// ace_pairs.hip -- pair-space kernels of the hot path, written for gfx950.
+//
+//  * k_assembly : reduced-kernel assembly K = sum_b K_b (a1-a4 of SURVEY §8a)
+//  * k_grad     : fused gradient traces -0.5 tr(T dK/dtheta) for every
+//                 hyperparameter, plus the Kfull*alpha rows for the RMSE
+//                 (a7/a8), without materialising the n x n x B cube.
+//
+// Both kernels walk 64x64 pair tiles with 256 threads: lane = row r, the
+// wave id picks 16 columns c = J*64 + wave + 4m, so every column-side
+// operand (x_c, z_c, the per-b weight rows) is wave-uniform and is fetched
+// with scalar loads, and every store to the column-major matrix is one
+// contiguous 512-B segment per wave.  fp64 VALU bound.
+#include "ace_internal.h"
+
+namespace ace {
+
+#define SQRT3 1.7320508075688772
+
+__device__ __forceinline__ double sgn(double x) {
+  return (double)((0.0 < x) - (x < 0.0));
+}
+
+// One slice value K_b for a pair, following the reference expressions:
+//  SE  (src/kernel_SE_cpp.cpp:96, 119 / 39, 53): slice 0 exp(lam - r2);
+//      b>=1: sign(z_lo) sign(z_hi) exp(((lam - r2) + log|z_lo|) + log|z_hi|),
+//      0 if either z is exactly 0 (Q7).
+//  Matern32 (src/kernel_Matern_cpp.cpp:217-227 / 79-86): t = sqrt(r2),
+//      e = (1 + sqrt3 t) exp(lam - sqrt3 t); b>=1: (e z_lo) z_hi, 0 if
+//      z_lo == 0 (and, in the cross kernel, if z_hi == 0).
+// "lo" is the first operand of the reference's product: the smaller index
+// of a symmetric pair (upper-triangle loop), the X1/Z1 side of a cross pair.
+template <int KIND, bool CROSS>
+__device__ __forceinline__ double kval(int b, double r2, double lam, double zlo,
+                                       double zhi, double lzlo, double lzhi) {
+  if (KIND == 0) {
+    if (b == 0) return exp(lam - r2);
+    if (zlo == 0.0 || zhi == 0.0) return 0.0;
+    return (sgn(zlo) * sgn(zhi)) * exp(((lam - r2) + lzlo) + lzhi);
+  } else {
+    const double t = sqrt(r2);
+    const double e = (1.0 + SQRT3 * t) * exp(lam - SQRT3 * t);
+    if (b == 0) return e;
+    if (zlo == 0.0) return 0.0;
+    if (CROSS && zhi == 0.0) return 0.0;
+    return (e * zlo) * zhi;
+  }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Assembly.  MODE 0: fused (lower tiles of A incl. sigma + identity padding)
+//            MODE 1: symmetric full output (+cube), MODE 2: cross (+cube).
+// ---------------------------------------------------------------------------
+template <int PM, int KIND, int MODE>
+__global__ __launch_bounds__(256) void k_assembly(PairSide R, PairSide C, int64_t npad,
+                                                  int B, int ZS, TabView tab, double sig,
+                                                  double *__restrict__ out, int64_t ld,
+                                                  double *__restrict__ cube) {
+  const int I = blockIdx.y, J = blockIdx.x;
+  if (MODE != 2 && J > I) return;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t r = (int64_t)I * AT + lane;
+  const int64_t nR = (MODE == 0) ? npad : R.n;
+  const int64_t nC = (MODE == 0) ? npad : C.n;
+  if (r >= nR) return;
+  const bool rvalid = r < R.n;
+  double xr[PM];
+#pragma unroll
+  for (int i = 0; i < PM; ++i) xr[i] = rvalid ? R.X[r * PM + i] : 0.0;
+  const int64_t cubeld = (MODE == 2) ? R.n : R.n;  // n (sym) or n1 (cross)
+  const int64_t slice = (MODE == 2) ? R.n * C.n : R.n * R.n;
+
+  for (int m = 0; m < AT / 4; ++m) {
+    const int64_t c = (int64_t)J * AT + wv + 4 * m;  // wave-uniform
+    if (c >= nC) break;
+    if (MODE == 1 && I == J && c > r) continue;  // lower half, mirrored below
+    const bool cvalid = c < C.n;
+    if (!(rvalid && cvalid)) {
+      if (MODE == 0) out[r + c * ld] = (r == c) ? 1.0 : 0.0;  // identity padding
+      continue;
+    }
+    double d2[PM];
+#pragma unroll
+    for (int i = 0; i < PM; ++i) {
+      const double d = xr[i] - C.X[c * PM + i];
+      d2[i] = d * d;
+    }
+    const bool rlo = (MODE == 2) || (r < c);  // row is the reference's first operand
+    double kf = 0.0;
+    for (int b = 0; b < B; ++b) {
+      const double *w = tab.wk + b * PM;
+      double r2 = 0.0;
+#pragma unroll
+      for (int i = 0; i < PM; ++i) r2 = fma(d2[i], w[i], r2);
+      double zr = 0.0, zc = 0.0, lzr = 0.0, lzc = 0.0;
+      if (b > 0) {
+        zr = R.Z[r * ZS + b - 1];
+        zc = C.Z[c * ZS + b - 1];
+        if (KIND == 0) {
+          lzr = R.LZ[r * ZS + b - 1];
+          lzc = C.LZ[c * ZS + b - 1];
+        }
+      }
+      const double kb =
+          rlo ? kval<KIND, MODE == 2>(b, r2, tab.lam[b], zr, zc, lzr, lzc)
+              : kval<KIND, MODE == 2>(b, r2, tab.lam[b], zc, zr, lzc, lzr);
+      kf += kb;
+      if (MODE != 0 && cube) {
+        cube[r + c * cubeld + b * slice] = kb;
+        if (MODE == 1 && c != r) cube[c + r * cubeld + b * slice] = kb;
+      }
+    }
+    if (MODE == 0) {
+      out[r + c * ld] = (r == c) ? kf + sig : kf;
+    } else {
+      out[r + c * ld] = kf;
+      if (MODE == 1 && c != r) out[c + r * ld] = kf;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Gradient traces.  T = w_rc (sA A[r,c] - alpha_r alpha_c) on lower pairs,
+// w = 2 off the diagonal, 1 on it (T and dK are symmetric, so the full-matrix
+// trace tr(T dK) = sum_rc T_rc dK_rc, src/include/ace_kernel_utils.hpp:23-26).
+// Per b: lambda sum   sum T K_b                       (src/kernel_SE_cpp.cpp:224-227)
+//        length sums  sum T K_b d_i^2                 (SE, 161-188)
+//                     sum T K_b/(1+sqrt(3 r~2)) d_i^2 (Matern32, kernel_Matern 340-377;
+//                     r~2 uses the gradient-indexed weights wg)
+// ---------------------------------------------------------------------------
+template <int PM, int KIND, bool CUBE, bool KA>
+__global__ __launch_bounds__(256) void k_grad(PairSide S, int B, int ZS, TabView tab,
+                                              const double *__restrict__ A, int64_t ld,
+                                              double sA, const double *__restrict__ alpha,
+                                              const double *__restrict__ cube,
+                                              double *__restrict__ gpart,
+                                              double *__restrict__ trpart,
+                                              double *__restrict__ kapart, int64_t npad,
+                                              int64_t ntiles) {
+  __shared__ double red[4][PM + 2];
+  __shared__ double rowacc[4][AT];
+  __shared__ double colacc[AT];
+  const int64_t t = blockIdx.x;
+  // decode lower-triangle tile index t -> (I, J), I >= J
+  int64_t I = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  while (I * (I + 1) / 2 > t) --I;
+  const int64_t J = t - I * (I + 1) / 2;
+
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n = S.n;
+  const int64_t r = I * AT + lane;
+  const bool rvalid = r < n;
+  const int64_t rr = rvalid ? r : 0;
+
+  double xr[PM];
+#pragma unroll
+  for (int i = 0; i < PM; ++i) xr[i] = rvalid ? S.X[rr * PM + i] : 0.0;
+  const double ar = rvalid ? alpha[rr] : 0.0;
+
+  double T[AT / 4];
+  double kf[AT / 4];
+  unsigned valid = 0;
+  double tr = 0.0;
+#pragma unroll
+  for (int m = 0; m < AT / 4; ++m) {
+    const int64_t c = J * AT + wv + 4 * m;
+    const bool v = rvalid && c < n && !(I == J && c > r);
+    double tv = 0.0;
+    if (v) {
+      tv = sA * A[r + c * ld] - ar * alpha[c];
+      if (c == r) tr += tv;
+      else tv *= 2.0;
+      valid |= 1u << m;
+    }
+    T[m] = tv;
+    kf[m] = 0.0;
+  }
+
+  for (int b = 0; b < B; ++b) {
+    double g[PM];
+#pragma unroll
+    for (int i = 0; i < PM; ++i) g[i] = 0.0;
+    double gl = 0.0;
+    const double *wk = tab.wk + b * PM;
+    const double *wg = tab.wg + b * PM;
+    const double lam = tab.lam[b];
+    double zr = 0.0, lzr = 0.0;
+    if (b > 0) {
+      zr = rvalid ? S.Z[rr * ZS + b - 1] : 0.0;
+      if (KIND == 0) lzr = rvalid ? S.LZ[rr * ZS + b - 1] : 0.0;
+    }
+#pragma unroll 2
+    for (int m = 0; m < AT / 4; ++m) {
+      const int64_t c = J * AT + wv + 4 * m;
+      if (c >= n) break;
+      double d2[PM];
+#pragma unroll
+      for (int i = 0; i < PM; ++i) {
+        const double d = xr[i] - S.X[c * PM + i];
+        d2[i] = d * d;
+      }
+      double kb;
+      if (CUBE) {
+        kb = ((valid >> m) & 1u) ? cube[r + c * n + (int64_t)b * n * n] : 0.0;
+      } else {
+        double r2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < PM; ++i) r2 = fma(d2[i], wk[i], r2);
+        double zc = 0.0, lzc = 0.0;
+        if (b > 0) {
+          zc = S.Z[c * ZS + b - 1];
+          if (KIND == 0) lzc = S.LZ[c * ZS + b - 1];
+        }
+        kb = (r < c) ? kval<KIND, false>(b, r2, lam, zr, zc, lzr, lzc)
+                     : kval<KIND, false>(b, r2, lam, zc, zr, lzc, lzr);
+      }
+      if (KA) kf[m] += kb;
+      const double tm = T[m];
+      gl = fma(tm, kb, gl);
+      double U;
+      if (KIND == 0) {
+        U = tm * kb;
+      } else {
+        double rt2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < PM; ++i) rt2 = fma(d2[i], wg[i], rt2);
+        U = tm * (kb / (1.0 + sqrt(3.0 * rt2)));
+      }
+#pragma unroll
+      for (int i = 0; i < PM; ++i) g[i] = fma(U, d2[i], g[i]);
+    }
+    // block reduction of the PM + 1 partial sums for this b
+#pragma unroll
+    for (int i = 0; i < PM; ++i) {
+      const double s = wave_sum(g[i]);
+      if (lane == 0) red[wv][i] = s;
+    }
+    {
+      const double s = wave_sum(gl);
+      if (lane == 0) red[wv][PM] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < PM + 1) {
+      const int i = threadIdx.x;
+      const double s = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+      gpart[((int64_t)b * (PM + 1) + i) * ntiles + t] = s;
+    }
+    __syncthreads();
+  }
+
+  // trace of T
+  {
+    const double s = wave_sum(tr);
+    if (lane == 0) red[wv][PM + 1] = s;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      trpart[t] = (red[0][PM + 1] + red[1][PM + 1]) + (red[2][PM + 1] + red[3][PM + 1]);
+  }
+
+  if (KA) {
+    // rows of Kfull * alpha: pair (r,c), r >= c, gives K a_c to row r and,
+    // if r != c, K a_r to row c.  Slot [J][r] for rows of I, [I][c] for J.
+    double rowp = 0.0;
+#pragma unroll
+    for (int m = 0; m < AT / 4; ++m) {
+      const int64_t c = J * AT + wv + 4 * m;
+      const bool v = (valid >> m) & 1u;
+      if (v) rowp = fma(kf[m], alpha[c], rowp);
+      const double cp = wave_sum((v && c != r) ? kf[m] * ar : 0.0);
+      if (lane == 0) colacc[wv + 4 * m] = cp;
+    }
+    rowacc[wv][lane] = rowp;
+    __syncthreads();
+    if (threadIdx.x < AT) {
+      const int x = threadIdx.x;
+      const double Rs = (rowacc[0][x] + rowacc[1][x]) + (rowacc[2][x] + rowacc[3][x]);
+      if (I == J) {
+        kapart[I * npad + I * AT + x] = Rs + colacc[x];
+      } else {
+        kapart[J * npad + I * AT + x] = Rs;
+        kapart[I * npad + J * AT + x] = colacc[x];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Dispatch over the compiled feature-count buckets.
+// ---------------------------------------------------------------------------
+static const int kBuckets[] = {4, 8, 12, 16, 20, 24, 32, 48, 64};
+
+int pm_bucket(int p) {
+  for (int b : kBuckets)
+    if (p <= b) return b;
+  return -1;
+}
+
+int64_t grad_ntiles(int64_t n) {
+  const int64_t nt = (n + AT - 1) / AT;
+  return nt * (nt + 1) / 2;
+}
+
+template <int PM>
+static hipError_t asm_pm(int mode, int kind, PairSide R, PairSide C, int64_t npad, int B,
+                         int ZS, TabView tab, double sig, double *out, int64_t ld,
+                         double *cube, hipStream_t st) {
+  dim3 blk(256);
+  dim3 grid;
+  if (mode == 0) {
+    const unsigned nt = (unsigned)(npad / AT);
+    grid = dim3(nt, nt);
+  } else if (mode == 1) {
+    const unsigned nt = (unsigned)((R.n + AT - 1) / AT);
+    grid = dim3(nt, nt);
+  } else {
+    grid = dim3((unsigned)((C.n + AT - 1) / AT), (unsigned)((R.n + AT - 1) / AT));
+  }
+#define ACE_ASM(K, M) \
+  hipLaunchKernelGGL((k_assembly<PM, K, M>), grid, blk, 0, st, R, C, npad, B, ZS, tab, sig, out, ld, cube)
+  if (kind == 0) {
+    if (mode == 0) ACE_ASM(0, 0);
+    else if (mode == 1) ACE_ASM(0, 1);
+    else ACE_ASM(0, 2);
+  } else {
+    if (mode == 0) ACE_ASM(1, 0);
+    else if (mode == 1) ACE_ASM(1, 1);
+    else ACE_ASM(1, 2);
+  }
+#undef ACE_ASM
+  return hipGetLastError();
+}
+
+hipError_t launch_assembly(int mode, int kind, int PM, PairSide R, PairSide C, int64_t npad,
+                           int B, int ZS, TabView tab, double sig, double *out, int64_t ld,
+                           double *cube, hipStream_t st) {
+  switch (PM) {
+#define ACE_CASE(P) \
+  case P: return asm_pm<P>(mode, kind, R, C, npad, B, ZS, tab, sig, out, ld, cube, st);
+    ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
+    ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
+#undef ACE_CASE
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int PM>
+static hipError_t grad_pm(int kind, PairSide S, int B, int ZS, TabView tab, const double *A,
+                          int64_t ld, double sA, const double *alpha, const double *cube,
+                          double *gpart, double *trpart, double *kapart, int64_t npad,
+                          hipStream_t st) {
+  const int64_t nt = grad_ntiles(S.n);
+  dim3 grid((unsigned)nt), blk(256);
+#define ACE_G(K, CB, KA)                                                                   \
+  hipLaunchKernelGGL((k_grad<PM, K, CB, KA>), grid, blk, 0, st, S, B, ZS, tab, A, ld, sA, \
+                     alpha, cube, gpart, trpart, kapart, npad, nt)
+  const bool cb = cube != nullptr, ka = kapart != nullptr;
+  if (cb && ka) return hipErrorInvalidValue;
+  if (kind == 0) {
+    if (cb) ACE_G(0, true, false);
+    else if (ka) ACE_G(0, false, true);
+    else ACE_G(0, false, false);
+  } else {
+    if (cb) ACE_G(1, true, false);
+    else if (ka) ACE_G(1, false, true);
+    else ACE_G(1, false, false);
+  }
+#undef ACE_G
+  return hipGetLastError();
+}
+
+hipError_t launch_grad(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
+                       const double *A, int64_t ld, double sA, const double *alpha,
+                       const double *cube, double *gpart, double *trpart, double *kapart,
+                       int64_t npad, hipStream_t st) {
+  switch (PM) {
+#define ACE_CASE(P) \
+  case P: return grad_pm<P>(kind, S, B, ZS, tab, A, ld, sA, alpha, cube, gpart, trpart, kapart, npad, st);
+    ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
+    ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
+#undef ACE_CASE
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace ace

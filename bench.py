@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""Benchmark: log-marg-lik + gradient evaluations per second (BASELINE.json
+`metric`) on the C2 configuration (n=16384, d=20, Matern32, ns basis B=10,
+fp64) -- the largest configuration in BASELINE.json that fits one GPU.
+
+A step is one `para_update` of the reference (R/kernel_SE_R6.R:40-62): the
+device-resident model assembles the reduced kernel, inverts A = K + e^s I by
+the MFMA Gauss-Jordan sweep (log det from its pivots) and computes every
+gradient and both statistics; the host then takes the Nadam step with
+norm clipping and the mu overwrite, exactly like the R6 class.  Inputs are
+resident in HBM before the timed region.
+
+Multi-GPU (torchrun, one process per GPU): round 1 runs independent replicas
+(DESIGN.md §5): every rank fits its own C2 problem on its own GPU, so per-GPU
+work is fixed ("weak") and value = all ranks' evals / max-over-ranks time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "log-marg-lik+grad evals/sec at n=16384,d=20; Cholesky GF/s vs MFMA peak"
+# MI355X dense fp64 matrix peak (AMD spec: 78.6 TFLOP/s fp64 vector and matrix;
+# MI355X_MICROARCH.md lists no fp64 row, so the spec value is used).
+FP64_MFMA_PEAK_TFLOPS = 78.6
+HBM_PEAK_GBS = 8000.0
+
+
+def _dist_init():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1:
+        return None, rank, world, local
+    import torch
+    import torch.distributed as dist
+    backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+    dist.init_process_group(backend=backend)
+    return dist, rank, world, local
+
+
+def _barrier_sync(dist):
+    if dist is not None:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        dist.barrier()
+
+
+def _allreduce_max(dist, x):
+    if dist is None:
+        return x
+    import torch
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(cfg, timeout=240):
+    """Rank 0 / N=1 only: the oracle leg in a subprocess (bounded)."""
+    from additivecausalexpansion_amd.synthetic import CONFIGS
+    n, p, B, kernel = CONFIGS[cfg]
+    cmd = [sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), "--n", str(n),
+           "--p", str(p), "--B", str(B), "--kernel", kernel, "--sample-n", "1536"]
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, check=True)
+        d = json.loads(out.stdout.strip().splitlines()[-1])
+        return {k: d[k] for k in ("value", "unit", "cores", "kind", "sample")}
+    except Exception as e:  # the baseline is reported, never required
+        return {"value": None, "unit": "evals/s", "cores": None, "kind": "port",
+                "sample": f"failed: {type(e).__name__}: {e}"[:300]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    dist, rank, world, local = _dist_init()
+    import numpy as np
+
+    import additivecausalexpansion_amd as ace
+    from additivecausalexpansion_amd.synthetic import CONFIGS, make_problem
+
+    n, p, B, kernel = CONFIGS[a.config]
+    y, X, Z, theta, std_y = make_problem(n, p, B, seed=1000 + rank)
+    ctx = ace.Context(local)
+    Kc = ace.KernelClass_Matern32_R6 if kernel == "Matern32" else ace.KernelClass_SE_R6
+    k = Kc(p, B, theta, std_y, ctx=ctx)
+    opt = ace.set_optimizer("Nadam", k, 0.01, 0.0, 0.9, 0.999, True, 1.0)
+    model = k._ensure_model(y, X, Z)  # uploads X, Z, y once (resident in HBM)
+
+    it = 0
+    for _ in range(a.warmup):
+        it += 1
+        k.para_update(it, y, X, Z, opt, verbose=False)
+
+    model.profile(True)
+    _barrier_sync(dist)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        it += 1
+        stats = k.para_update(it, y, X, Z, opt, verbose=False)
+    _barrier_sync(dist)
+    dt = time.perf_counter() - t0
+    dt_max = _allreduce_max(dist, dt)
+    upd_ms, upd_n, upd_work = model.kernel_time(0)
+    asm_ms, _, asm_work = model.kernel_time(1)
+    grad_ms, _, grad_work = model.kernel_time(2)
+    model.profile(False)
+
+    if rank == 0:
+        evals = a.steps * world
+        value = evals / dt_max
+        achieved = upd_work / (upd_ms * 1e-3) / 1e12 if upd_ms > 0 else None
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": dt_max / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded SURVEY.md §8d generator; no dataset exists for this metric)",
+            "config": {
+                "workload": (f"{a.config}: n={n}, d={p}, {kernel}, ns basis B={B}, fp64; one "
+                             "para_update (kernel assembly + SPD inverse/log-det + all P gradients "
+                             "+ RMSE/evidence + Nadam step) per step"),
+                "n": n, "p": p, "B": B, "kernel": kernel,
+                "parallelism": "single" if world == 1 else f"replicas x{world}",
+            },
+            "roofline": {
+                "kernel": "k_update (sweep SYRK/GEMM update, v_mfma_f64_16x16x4_f64)",
+                "bound": "mfma",
+                "achieved": achieved,
+                "peak": FP64_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
+                "traffic": None,
+                "launches": upd_n,
+                "avg_launch_ms": upd_ms / upd_n if upd_n else None,
+                "algorithmic_flops_per_launch": upd_work / upd_n if upd_n else None,
+            },
+            "dense_gflops_per_eval_wall": (n ** 3) / (dt_max / a.steps) / 1e9,
+            "phase_ms_per_step": {"update_kernel": upd_ms / a.steps,
+                                  "assembly_kernel": asm_ms / a.steps,
+                                  "gradient_kernel": grad_ms / a.steps},
+            "pair_kernels_tflops": {
+                "assembly": asm_work / (asm_ms * 1e-3) / 1e12 if asm_ms else None,
+                "gradient": grad_work / (grad_ms * 1e-3) / 1e12 if grad_ms else None},
+            "last_stats": [float(stats[0]), float(stats[1])],
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(a.config)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

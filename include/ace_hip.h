@@ -1,0 +1,203 @@
+/*
+ * ace_hip.h -- C ABI of the MI355X-native engine for the `ace` hot path.
+ *
+ * Drop-in boundary: every entry point below replaces one Rcpp-exported
+ * routine of the reference (R package `ace` 0.4.1).  The reference routine
+ * is cited as file:line next to each declaration; the R-side `.Call`
+ * wrapper names are in R/RcppExports.R:4-78 and are kept unchanged by the
+ * Rcpp shim shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - All matrices are column-major fp64 (R / Armadillo layout) with explicit
+ *    64-bit dimensions; cubes are n1 x n2 x B, slice-major (arma::cube).
+ *  - The library never allocates or frees caller memory.  Outputs go to
+ *    caller buffers; buffers documented "in/out" are mutated in place
+ *    exactly as the reference mutates the R vectors it receives by
+ *    non-const reference (SURVEY.md §8b "Ownership").
+ *  - Functions taking an `ace_ctx*` run on the GPU; they return ACE_OK (0)
+ *    or a non-zero status, and ace_last_error() describes the failure.  The
+ *    Rcpp shim turns a non-zero status into Rcpp::stop().
+ *  - A matrix that is not positive definite does NOT raise an error: as in
+ *    the reference (a failed eig_sym only prints, src/kernel_SE_cpp.cpp:144-146)
+ *    the affected outputs come out non-finite, so R's optimizer classes
+ *    stop() on the non-finite gradient (R/optimizer_classes.R:26-29).
+ *  - Host-only functions (optimizers, norm clip, spline basis, normalisation)
+ *    need no context and never touch the GPU.
+ *  - Calls are blocking and not re-entrant per context (the reference runs
+ *    everything synchronously on the R main thread).
+ */
+#ifndef ACE_HIP_H
+#define ACE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACE_ABI_VERSION 1
+
+enum ace_kernel_kind { ACE_KERNEL_SE = 0, ACE_KERNEL_MATERN32 = 1 };
+
+enum ace_status {
+  ACE_OK = 0,
+  ACE_ERR_ARG = 1,         /* invalid argument / shape                          */
+  ACE_ERR_HIP = 2,         /* HIP runtime failure (no device, launch failure)   */
+  ACE_ERR_OOM = 3,         /* device allocation failed                          */
+  ACE_ERR_UNSUPPORTED = 4  /* shape outside the compiled range (p > 64, B > 32) */
+};
+
+typedef struct ace_ctx ace_ctx;
+typedef struct ace_model ace_model;
+
+/* ---------------------------------------------------------------- context */
+int ace_abi_version(void);
+/* Creates a context on HIP device `device` (one process per GPU). */
+int ace_create(int device, ace_ctx **out);
+void ace_destroy(ace_ctx *ctx);
+/* Message of the last failure on this context ("" if none).  NULL ctx gives
+ * the message of the last failed ace_create in this process. */
+const char *ace_last_error(const ace_ctx *ctx);
+
+/* ------------------------------------------------ Rcpp-export equivalents */
+
+/* kernmat_SE_cpp / kernmat_Matern32_cpp (src/kernel_SE_cpp.cpp:9-64,
+ * src/kernel_Matern_cpp.cpp:52-93).  X1 n1 x p, X2 n2 x p, Z1 n1 x (B-1),
+ * Z2 n2 x (B-1), theta P = 2 + B(p+1).  Writes Kfull (n1 x n2, list item
+ * `full`) and, if Kel != NULL, the n1 x n2 x B cube (`elements`). */
+int ace_kernmat_cross(ace_ctx *ctx, int kind, int64_t n1, int64_t n2, int p,
+                      int B, const double *X1, const double *X2,
+                      const double *Z1, const double *Z2, const double *theta,
+                      double *Kfull, double *Kel);
+
+/* kernmat_SE_symmetric_cpp / kernmat_Matern32_symmetric_cpp
+ * (src/kernel_SE_cpp.cpp:67-134, src/kernel_Matern_cpp.cpp:190-240).
+ * Kfull n x n (`full`); Kel n x n x B (`elements`) or NULL. */
+int ace_kernmat_sym(ace_ctx *ctx, int kind, int64_t n, int p, int B,
+                    const double *X, const double *Z, const double *theta,
+                    double *Kfull, double *Kel);
+
+/* invkernel_cpp (src/kernel_SE_cpp.cpp:137-157).  A = K + exp(sigma) I.
+ * inv (n x n) = A^-1.  `eigenval` (n) receives the pivots of A's
+ * symmetric elimination (Cholesky diagonal squared) instead of A's
+ * eigenvalues: every consumer in the reference only uses sum(log(eigenval))
+ * (src/kernel_SE_cpp.cpp:240, src/kernel_Matern_cpp.cpp:463,
+ * src/stats_cpp.cpp:29), and sum(log(pivots)) == log det A.
+ * Either output pointer may be NULL. */
+int ace_invkernel(ace_ctx *ctx, int64_t n, const double *K, double sigma,
+                  double *eigenval, double *inv);
+
+/* grad_SE_cpp / grad_Matern_cpp (src/kernel_SE_cpp.cpp:192-243,
+ * src/kernel_Matern_cpp.cpp:420-467).  Kel (n x n x B) may be NULL: the
+ * engine then recomputes the slices from X, Z, theta on the device (the R6
+ * caller always passes the cube of the same theta).  stats (2) is in/out:
+ * stats[0] = RMSE, stats[1] = log evidence.  grad receives P values. */
+int ace_grad(ace_ctx *ctx, int kind, int64_t n, int p, int B, const double *y,
+             const double *X, const double *Z, const double *Kfull,
+             const double *Kel, const double *inv, const double *eigenval,
+             const double *theta, double *stats, double std_y, double *grad);
+
+/* stats_cpp (src/stats_cpp.cpp:9-32): out[0] = RMSE, out[1] = log evidence. */
+int ace_stats(ace_ctx *ctx, int64_t n, const double *y, const double *Kmat,
+              const double *inv, const double *eigenval, double mu,
+              double std_y, double *out);
+
+/* mu_solution_cpp (src/utilities_cpp.cpp:6-10). */
+int ace_mu_solution(ace_ctx *ctx, int64_t n, const double *y,
+                    const double *inv, double *out);
+
+/* pred_cpp (src/pred_cpp.cpp:8-34).  nX training rows, nx test rows.
+ * K_xX nx x nX, K_xx nx x nx.  map (nx), ci (nx x 2), var (nx). */
+int ace_pred(ace_ctx *ctx, int64_t nX, int64_t nx, const double *y_X,
+             double sigma, double mu, const double *invK_XX,
+             const double *K_xX, const double *K_xx, double mean_y,
+             double std_y, double *map, double *ci, double *var);
+
+/* pred_marginal_cpp (src/pred_cpp.cpp:37-126).  K_xX nx x nX x B,
+ * K_xx nx x nx x B.  When calculate_ate != 0, `avg` (12) receives
+ * [ate.map, ate.ci0, ate.ci1, ate.var, att.map, att.ci0, att.ci1, att.var,
+ *  atu.map, atu.ci0, atu.ci1, atu.var]; otherwise avg may be NULL. */
+int ace_pred_marginal(ace_ctx *ctx, int64_t nX, int64_t nx, int B,
+                      const double *y_X, const double *Z_x, double sigma,
+                      double mu, const double *invK_XX, const double *K_xX,
+                      const double *K_xx, double mean_y, double std_y,
+                      double std_Z, int calculate_ate, double *map, double *ci,
+                      double *var, double *avg);
+
+/* ---------------------------------------------- host-only (no GPU, no ctx) */
+
+/* Nesterov_cpp / Nadam_cpp / Adam_cpp (src/optimizer_cpp.cpp:8-63).  All
+ * vectors are P long and mutated in place; the return value is the
+ * reference's bool: 1 if every gradient is finite, else 0.  Ascent (Q8). */
+int ace_nesterov(int64_t P, double learn_rate, double momentum, double *nu,
+                 const double *grad, double *para);
+int ace_nadam(int64_t P, double iter, double learn_rate, double beta1,
+              double beta2, double eps, double *m, double *v,
+              const double *grad, double *para);
+int ace_adam(int64_t P, double iter, double learn_rate, double beta1,
+             double beta2, double eps, double *m, double *v,
+             const double *grad, double *para);
+
+/* norm_clip_cpp (src/utilities_cpp.cpp:121-129), in place.  Q5: rescales
+ * to unit norm (not to max_length) when ||grads|| > max_length. */
+void ace_norm_clip(int flag, int64_t P, double *grads, double max_length);
+
+/* ncs_basis / ncs_basis_deriv (src/ncs_basis_cpp.cpp:61-99).  knots are
+ * de-duplicated and sorted; design must hold n x (#unique knots) doubles;
+ * *ncols receives #unique knots. */
+int ace_ncs_basis(int64_t n, const double *x, int64_t nknots,
+                  const double *knots, double *design, int64_t *ncols);
+int ace_ncs_basis_deriv(int64_t n, const double *x, int64_t nknots,
+                        const double *knots, double *design, int64_t *ncols);
+
+/* normalize_train (src/utilities_cpp.cpp:13-104): in place on y (n),
+ * X (n x px), Z (n x pz); moments is (1+px+pz) x 3 column-major.
+ * normalize_test (src/utilities_cpp.cpp:108-118): in place on X, Z. */
+int ace_normalize_train(int64_t n, int px, int pz, double *y, double *X,
+                        double *Z, double *moments);
+int ace_normalize_test(int64_t n, int px, int pz, double *X, double *Z,
+                       const double *moments, int64_t moment_rows);
+
+/* ------------------------------- device-resident hot path (one model fit)
+ *
+ * The R6 kernel classes ship Kmat, the n x n x B cube and invKmatn through
+ * R on every iteration (R/kernel_SE_R6.R:26-39, 47-50).  The model below
+ * keeps X, Z, y, the swept matrix and the training inverse resident in HBM
+ * and never materialises the cube: one ace_model_para_update() is the
+ * native work of one para_update (R/kernel_SE_R6.R:40-62,
+ * R/kernel_Matern32_R6.R:142-163) -- kernel assembly, factorisation +
+ * inverse + log-determinant, and every gradient and statistic.
+ */
+int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B,
+                     ace_model **out);
+void ace_model_destroy(ace_model *m);
+/* Uploads y (n), X (n x p), Z (n x (B-1)) and the std_y moment. */
+int ace_model_set_data(ace_model *m, const double *y, const double *X,
+                       const double *Z, double std_y);
+/* One para_update's native work at theta (P, in/out).  If iter == 1,
+ * theta[1] is first overwritten with mu_solution (R/kernel_SE_R6.R:45).
+ * grad (P) receives the gradient, stats (2) the RMSE and log evidence,
+ * *mu_post the mu_solution of this iteration's inverse, which the caller
+ * writes into theta[1] after its optimizer step (R/kernel_SE_R6.R:54).
+ * The inverse stays resident for ace_model_predict. */
+int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad,
+                          double *stats, double *mu_post);
+/* get_train_stats (R/kernel_SE_R6.R:63-74): kernel + inverse at theta and
+ * stats_cpp with mu = theta[1]; the resident inverse is NOT replaced. */
+int ace_model_train_stats(ace_model *m, const double *theta, double *stats);
+/* Copies the resident training inverse (n x n) to the host. */
+int ace_model_get_inverse(ace_model *m, double *inv);
+/* Per-kernel device timing for the roofline report: when enabled, HIP
+ * events bracket every launch of the dense update kernel (`which` = 0),
+ * the assembly kernel (1) and the gradient kernel (2) on the model's
+ * stream.  *ms = summed duration, *launches = count, *work = algorithmic
+ * flops issued by those launches. */
+int ace_model_profile(ace_model *m, int enable);
+int ace_model_kernel_time(ace_model *m, int which, double *ms,
+                          int64_t *launches, double *work);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ACE_HIP_H */

@@ -1,0 +1,92 @@
+"""CPU baseline leg for bench.py (TEST/BENCH INFRASTRUCTURE ONLY).
+
+Times the reference's algorithms on the host for one log-marg-lik + gradient
+evaluation (one para_update's native work) on a BOUNDED sample of the bench
+workload, and extrapolates to the full size:
+  * pair loops (kernmat_*_symmetric_cpp + grad_*_cpp, single-threaded as in
+    the reference): the literal C restatement oracle/ace_ref.c, scaled by n^2;
+  * invkernel_cpp (eig_sym = LAPACK dsyevd, then V D^-1/2 (V D^-1/2)^T):
+    numpy.linalg.eigh + matmul on all host BLAS threads, scaled by n^3.
+Prints one JSON line.  PARITY UNPINNED note: see oracle/ace_oracle.py.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import os
+import subprocess
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=16384, help="full-size n to extrapolate to")
+    ap.add_argument("--sample-n", type=int, default=2048)
+    ap.add_argument("--p", type=int, default=20)
+    ap.add_argument("--B", type=int, default=10)
+    ap.add_argument("--kernel", default="Matern32")
+    a = ap.parse_args()
+
+    import numpy as np
+
+    from additivecausalexpansion_amd.synthetic import make_problem
+
+    so = os.path.join(HERE, "libace_ref.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    L = ctypes.CDLL(so)
+    D = ctypes.POINTER(ctypes.c_double)
+    I64 = ctypes.c_int64
+    L.ref_kernmat_sym.argtypes = [ctypes.c_int, I64, ctypes.c_int, ctypes.c_int, D, D, D, D, D]
+    L.ref_grad.argtypes = [ctypes.c_int, I64, ctypes.c_int, ctypes.c_int, D, D, D, D, D,
+                           ctypes.c_double, D, D, ctypes.c_double, D]
+    P = lambda x: x.ctypes.data_as(D)  # noqa: E731
+    kind = 0 if a.kernel == "SE" else 1
+    n, p, B = a.sample_n, a.p, a.B
+    y, X, Z, th, sy = make_problem(n, p, B, seed=0)
+    X = np.asfortranarray(X)
+    Z = np.asfortranarray(Z)
+    Kf = np.zeros((n, n), order="F")
+    Ke = np.zeros((n, n, B), order="F")
+    t0 = time.perf_counter()
+    L.ref_kernmat_sym(kind, n, p, B, P(X), P(Z), P(th), P(Kf), P(Ke))
+    t_asm = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    A = Kf.copy()
+    A[np.diag_indices(n)] += math.exp(th[0])
+    w, V = np.linalg.eigh(A)
+    Vs = V / np.sqrt(w)[None, :]
+    inv = np.asfortranarray(Vs @ Vs.T)
+    t_inv = time.perf_counter() - t0
+    st = np.zeros(2)
+    g = np.zeros(th.shape[0])
+    t0 = time.perf_counter()
+    L.ref_grad(kind, n, p, B, P(y), P(X), P(Kf), P(Ke), P(inv), float(np.sum(np.log(w))), P(th),
+               P(st), sy, P(g))
+    t_grad = time.perf_counter() - t0
+    s2 = (a.n / n) ** 2
+    s3 = (a.n / n) ** 3
+    t_full = (t_asm + t_grad) * s2 + t_inv * s3
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    try:
+        cpu = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":")[1].strip()
+    except Exception:
+        cpu = "unknown"
+    print(json.dumps({
+        "value": 1.0 / t_full, "unit": "evals/s", "cores": threads, "kind": "port",
+        "sample": (f"one {a.kernel} eval at n={n}, p={p}, B={B} (sample of n={a.n}): pair loops "
+                   f"{t_asm + t_grad:.2f} s single-thread x (n/{n})^2, eigh+inverse {t_inv:.2f} s "
+                   f"on {threads} BLAS threads x (n/{n})^3 -> {t_full:.1f} s per eval; "
+                   f"host CPU: {cpu}"),
+        "sample_seconds": {"assembly": t_asm, "inverse": t_inv, "gradient": t_grad},
+        "extrapolated_seconds_per_eval": t_full}))
+
+
+if __name__ == "__main__":
+    main()

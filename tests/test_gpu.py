@@ -1,0 +1,276 @@
+"""GPU parity tests: every C-ABI entry point against the oracle, on the
+committed golden fixtures and on live oracle runs, plus size-independent
+properties at larger n.  All calls go through libace_hip.so (the HIP path);
+there is no fallback.
+
+Tolerances (north_star: "within 1e-6 relative fp64"):
+  * assembly (pure pair arithmetic, FMA vs separate mul/add and ocml vs
+    glibc exp/log/sqrt): |K - K_ref| <= 1e-12 * max|K_ref|
+  * inverse (Gauss-Jordan sweep vs eigendecomposition, ~cond * eps):
+    |inv - inv_ref| <= 1e-9 * max|inv_ref|
+  * gradients, stats, predictions: |v - v_ref| <= 1e-6 |v_ref| + 1e-9 max|v_ref|
+"""
+import math
+
+import numpy as np
+import pytest
+from conftest import golden, golden_names
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-6
+
+
+def close(a, b, rtol=RTOL, atol_rel=1e-9):
+    a = np.asarray(a, dtype=float)
+    b = np.asarray(b, dtype=float)
+    scale = np.abs(b).max() if b.size else 0.0
+    ok = np.abs(a - b) <= rtol * np.abs(b) + atol_rel * scale
+    if not np.all(ok):
+        i = np.argmax(np.abs(a - b) - rtol * np.abs(b))
+        raise AssertionError(f"mismatch at {np.unravel_index(i, b.shape)}: {a.flat[i]} vs "
+                             f"{b.flat[i]} (max abs err {np.abs(a - b).max():.3e}, scale {scale:.3e})")
+
+
+@pytest.fixture(scope="module")
+def A():
+    import additivecausalexpansion_amd as pkg
+    pkg.default_context()
+    return pkg
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import ace_oracle
+    return ace_oracle
+
+
+def kern_fns(A, kernel):
+    if kernel == "SE":
+        return A.kernmat_SE_symmetric_cpp, A.kernmat_SE_cpp, A.grad_SE_cpp
+    return A.kernmat_Matern32_symmetric_cpp, A.kernmat_Matern32_cpp, A.grad_Matern_cpp
+
+
+# ------------------------------------------------------------------ MFMA layout
+def test_gemm_mfma_layout_asymmetric(A):
+    """A=I and asymmetric B through the MFMA GEMM (pred_cpp's tmp = K_xX inv):
+    catches a transposed C/D fragment map."""
+    rng = np.random.default_rng(0)
+    nX, nx = 37, 150
+    Bm = rng.normal(size=(nX, nX))
+    inv = Bm  # not symmetric on purpose
+    KxX = rng.normal(size=(nx, nX))
+    y = rng.normal(size=nX)
+    out = A.pred_cpp(y, -1.0, 0.2, inv, KxX, np.eye(nx) * 3.0, 0.5, 2.0)
+    tmp = KxX @ inv
+    close(out["map"], 0.5 + 2.0 * (tmp @ (y - 0.2) + 0.2), 1e-12, 1e-12)
+    d = 3.0 - np.sum(tmp * KxX, axis=1) + math.exp(-1.0)
+    close(out["var"], (2.0 * np.sqrt(np.abs(d))) ** 2, 1e-11, 1e-12)
+
+
+# ------------------------------------------------------------------ assembly
+@pytest.mark.parametrize("name", golden_names("asm_"))
+def test_assembly_golden(A, name):
+    d = golden(name)
+    kernel = "SE" if "_SE_" in name else "Matern32"
+    sym, cross, _ = kern_fns(A, kernel)
+    ks = sym(d["X"], d["Z"], d["theta"])
+    close(ks["full"], d["sym_full"], 1e-12, 1e-12)
+    assert np.array_equal(ks["full"], ks["full"].T)  # mirrored exactly
+    kc = cross(d["X2"], d["X"], d["Z2"], d["Z"], d["theta"])
+    close(kc["full"], d["cross_full"], 1e-12, 1e-12)
+    if "sym_elements" in d:
+        close(ks["elements"], d["sym_elements"], 1e-12, 1e-12)
+        close(kc["elements"], d["cross_elements"], 1e-12, 1e-12)
+        # exact zeros of the basis give exact zeros (Q7 branch)
+        zr = d["Z"] == 0
+        for b in range(1, ks["elements"].shape[2]):
+            assert np.all(ks["elements"][zr[:, b - 1], :, b] == 0)
+
+
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+@pytest.mark.parametrize("p", [1, 4, 8, 11, 20, 23, 31, 40, 57, 64])
+def test_assembly_every_feature_bucket(A, O, kernel, p):
+    rng = np.random.default_rng(p)
+    n, B = 70, 3
+    X = rng.uniform(-1, 1, (n, p))
+    Z = rng.normal(size=(n, B - 1))
+    Z[rng.random((n, B - 1)) < 0.3] = 0
+    th = np.concatenate([[-1.0, 0.0], rng.normal(0, .3, B), rng.normal(1.0, .3, B * p)])
+    sym = kern_fns(A, kernel)[0]
+    close(sym(X, Z, th)["full"], O.KERNELS[kernel][0](X, Z, th)["full"], 1e-12, 1e-12)
+
+
+def test_assembly_unsupported_shape_raises(A):
+    with pytest.raises(A.AceError):
+        A.kernmat_SE_symmetric_cpp(np.zeros((5, 65)), np.zeros((5, 1)), np.zeros(2 + 2 * 66))
+
+
+# ------------------------------------------------------------------ inverse
+@pytest.mark.parametrize("name", golden_names("grad_"))
+def test_invkernel_golden(A, name):
+    d = golden(name)
+    r = A.invkernel_cpp(d["Kfull"], d["theta"][0])
+    close(r["inv"], d["inv"], 1e-9, 1e-9)
+    assert np.sum(np.log(r["eigenval"])) == pytest.approx(float(d["logdet"]), rel=1e-10, abs=1e-9)
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 255, 256, 257, 700, 1500])
+def test_invkernel_sizes(A, O, n):
+    """Edge sizes around the 64/128/256 blockings (padding + AUG rows)."""
+    from additivecausalexpansion_amd.synthetic import make_problem
+    y, X, Z, th, _ = make_problem(max(n, 3), 3, 4, seed=n)
+    X, Z = X[:n], Z[:n]
+    K = O.kernmat_SE_symmetric_cpp(X, Z, th)["full"]
+    r = A.invkernel_cpp(K, th[0])
+    ref = O.invkernel_cpp(K, th[0])
+    close(r["inv"], ref["inv"], 1e-9, 1e-9)
+    assert np.sum(np.log(r["eigenval"])) == pytest.approx(np.sum(np.log(ref["eigenval"])),
+                                                          rel=1e-10, abs=1e-9)
+
+
+def test_invkernel_not_positive_definite_gives_nan(A):
+    K = -np.eye(10)
+    r = A.invkernel_cpp(K, -5.0)
+    assert np.all(np.isnan(r["inv"]))
+    assert np.any(r["eigenval"] <= 0)
+
+
+# ------------------------------------------------------------------ gradient + stats
+@pytest.mark.parametrize("name", golden_names("grad_"))
+@pytest.mark.parametrize("with_cube", [True, False])
+def test_grad_golden(A, O, name, with_cube):
+    d = golden(name)
+    kernel = "SE" if "_SE_" in name else "Matern32"
+    sym, _, grad = kern_fns(A, kernel)
+    B = d["Z"].shape[1] + 1
+    cube = O.KERNELS[kernel][0](d["X"], d["Z"], d["theta"])["elements"] if with_cube else None
+    ev = np.exp(np.full(d["y"].shape[0], float(d["logdet"]) / d["y"].shape[0]))
+    stats = np.zeros(2)
+    g = grad(d["y"], d["X"], d["Z"], d["Kfull"], cube, d["inv"], ev, d["theta"], stats, B,
+             float(d["std_y"]))
+    close(g, d["grad"])
+    close(stats, d["stats"])
+    st2 = A.stats_cpp(d["y"], d["Kfull"], d["inv"], ev, d["theta"][1], float(d["std_y"]))
+    close(st2, d["stats_cpp"])
+    assert A.mu_solution_cpp(d["y"], d["inv"]) == pytest.approx(float(d["mu"]), rel=1e-9)
+
+
+# ------------------------------------------------------------------ prediction
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+def test_pred_golden(A, kernel):
+    d = golden(f"pred_{kernel}")
+    th = d["theta"]
+    pr = A.pred_cpp(d["y"], th[0], th[1], d["inv"], d["K_xX"], d["K_xx"], 0.3, 1.9)
+    close(pr["map"], d["map"])
+    close(pr["var"], d["var"])
+    close(pr["ci"], d["ci"])
+    pm = A.pred_marginal_cpp(d["y"], d["Z2"], th[0], th[1], d["inv"], d["cube_xX"], d["cube_xx"],
+                             0.3, 1.9, 0.8, True)
+    close(pm["map"], d["m_map"])
+    close(pm["var"], d["m_var"])
+    got = np.concatenate([[pm[k]["map"], pm[k]["ci"][0], pm[k]["ci"][1], pm[k]["var"]]
+                          for k in ("ate", "att", "atu")])
+    close(got, d["avg"])
+    pm2 = A.pred_marginal_cpp(d["y"], d["Z2"], th[0], th[1], d["inv"], d["cube_xX"],
+                              d["cube_xx"], 0.3, 1.9, 0.8, False)
+    assert "ate" not in pm2
+
+
+# ------------------------------------------------------------------ fused model
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+@pytest.mark.parametrize("n,p,B", [(300, 2, 5), (513, 3, 4), (1000, 20, 10), (130, 1, 2)])
+def test_model_para_update_matches_oracle(A, O, kernel, n, p, B):
+    """One device-resident para_update (kernel + sweep + fused gradient) vs the
+    oracle's kernmat_sym -> invkernel -> grad chain, at iter 1 (mu first) and 2."""
+    from additivecausalexpansion_amd.synthetic import make_problem
+    y, X, Z, th, sy = make_problem(n, p, B, seed=7)
+    m = A.DeviceModel(kernel, n, p, B)
+    m.set_data(y, X, Z, sy)
+    sym, _, grad = O.KERNELS[kernel]
+    for it in (1, 2):
+        t_dev = th.copy()
+        g, st, mu_post = m.para_update(it, t_dev)
+        t_ref = th.copy()
+        Kl = sym(X, Z, t_ref)
+        inv = O.invkernel_cpp(Kl["full"], t_ref[0])
+        if it == 1:
+            t_ref[1] = O.mu_solution_cpp(y, inv["inv"])
+        st_ref = np.zeros(2)
+        g_ref = grad(y, X, Z, Kl["full"], Kl["elements"], inv["inv"], inv["eigenval"], t_ref,
+                     st_ref, B, sy)
+        assert t_dev[1] == pytest.approx(t_ref[1], rel=1e-8, abs=1e-12)
+        close(g, g_ref)
+        close(st, st_ref)
+        assert mu_post == pytest.approx(O.mu_solution_cpp(y, inv["inv"]), rel=1e-8)
+        if it == 1:
+            close(m.inverse(), inv["inv"], 1e-9, 1e-9)
+        th = th + 0.01
+
+
+def test_model_train_stats_keeps_inverse(A, O):
+    from additivecausalexpansion_amd.synthetic import make_problem
+    y, X, Z, th, sy = make_problem(400, 3, 4, seed=3)
+    m = A.DeviceModel("SE", 400, 3, 4)
+    m.set_data(y, X, Z, sy)
+    m.para_update(2, th.copy())
+    inv1 = m.inverse()
+    th2 = th + 0.05
+    st = m.train_stats(th2)
+    K = O.kernmat_SE_symmetric_cpp(X, Z, th2)["full"]
+    inv = O.invkernel_cpp(K, th2[0])
+    close(st, O.stats_cpp(y, K, inv["inv"], inv["eigenval"], th2[1], sy))
+    assert np.array_equal(m.inverse(), inv1)  # Q6: predict keeps the para_update inverse
+
+
+# ------------------------------------------------------------------ training loop
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+def test_training_trajectory_matches_golden(A, kernel):
+    """README config (n=300, d=2, ns n.knots=2, Nadam lr 0.01): 20 iterations of
+    ace.train through the R6 mirror on the device-resident path."""
+    d = golden(f"traj_{kernel}")
+    y, X, Bm = d["y"], np.asfortranarray(d["X"]), np.asfortranarray(d["basis"])
+    B = Bm.shape[1] + 1
+    Kc = A.KernelClass_SE_R6 if kernel == "SE" else A.KernelClass_Matern32_R6
+    k = Kc(2, B, d["theta0"], float(d["moments"][0, 1]))
+    opt = A.set_optimizer("Nadam", k, 0.01, 0.0, 0.9, 0.999, True, 1.0)
+    for it in range(1, 21):
+        st = k.para_update(it, y, X, Bm, opt, verbose=False)
+        close(st, d["stats"][it - 1], 1e-6, 1e-9)
+        close(k.parameters, d["thetas"][it - 1], 1e-6, 1e-9)
+    pr = k.predict(y, X, Bm, X, Bm, float(d["moments"][0, 0]), float(d["moments"][0, 1]))
+    close(pr["map"], d["pred_map"], 1e-6, 1e-9)
+    close(pr["var"], d["pred_var"], 1e-6, 1e-9)
+
+
+def test_ace_train_and_predict_end_to_end(A):
+    from additivecausalexpansion_amd.synthetic import readme_data
+    y, X, Z = readme_data(seed=5, n=200)
+    fit = A.ace_train(y, X, Z, kernel="SE", basis="cubic", n_knots=2, maxiter=30, verbose=False)
+    ev = fit["train_stats"]["stats"][1]
+    assert np.all(np.isfinite(ev)) and ev[-1] > ev[0]
+    pr = A.predict_ace(fit)
+    assert pr["map"].shape == (200,) and np.all(pr["var"] > 0)
+    pm = A.predict_ace(fit, marginal=True)
+    assert pm["map"].shape == (200,)
+    # binary treatment: ATE / ATT / ATU
+    rng = np.random.default_rng(1)
+    zb = (rng.random(200) < 0.5).astype(float)
+    yb = X[:, 0] + 2 * zb + rng.normal(0, .3, 200)
+    fb = A.ace_train(yb, X, zb, maxiter=15, verbose=False)
+    out = A.predict_ace(fb, marginal=True, return_average_treatments=True)
+    assert set(out) >= {"ate", "att", "atu"}
+
+
+# ------------------------------------------------------------------ full-size properties
+def test_sweep_large_residual_and_logdet(A):
+    """n = 4096 (C1 size): ||A A^-1 - I|| small and logdet vs LAPACK slogdet."""
+    from additivecausalexpansion_amd.synthetic import make_problem
+    y, X, Z, th, sy = make_problem(4096, 10, 6, seed=1)
+    K = A.kernmat_SE_symmetric_cpp(X, Z, th)["full"]
+    r = A.invkernel_cpp(K, th[0])
+    Am = K + math.exp(th[0]) * np.eye(4096)
+    R = Am @ r["inv"] - np.eye(4096)
+    assert np.abs(R).max() < 1e-8
+    s, ld = np.linalg.slogdet(Am)
+    assert s > 0 and np.sum(np.log(r["eigenval"])) == pytest.approx(ld, rel=1e-10)
