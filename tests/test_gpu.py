@@ -226,21 +226,52 @@ def test_model_train_stats_keeps_inverse(A, O):
 # ------------------------------------------------------------------ training loop
 @pytest.mark.parametrize("kernel", ["SE", "Matern32"])
 def test_training_trajectory_matches_golden(A, kernel):
-    """README config (n=300, d=2, ns n.knots=2, Nadam lr 0.01): 20 iterations of
-    ace.train through the R6 mirror on the device-resident path."""
+    """README config (n=300, d=2, ns n.knots=2, Nadam lr 0.01), 20 iterations of
+    ace.train through the R6 mirror on the device-resident path.
+
+    (1) anchored: each iteration's native work (para_update at the golden
+        theta_{it-1}) must reproduce the golden stats and raw gradient to 1e-6;
+    (2) free run: the whole loop (device gradients -> host norm clip + Nadam ->
+        mu overwrite) must track the golden trajectory.  Nadam divides by
+        sqrt(v), so last-bit differences in small gradient components are
+        amplified along the loop: theta is held to 1e-5 relative, stats to 1e-6;
+    (3) prediction at the golden theta_T with the golden theta_{T-1} inverse
+        (Q6).  That mix makes the reference's variance |K_xx - q + e^s| a
+        cancellation of terms ~1e3 x larger than the result, so its tolerance is
+        1e-6 of the cancelled terms (std_y^2 (K_xx,rr + q_r)), not of the result.
+    """
     d = golden(f"traj_{kernel}")
     y, X, Bm = d["y"], np.asfortranarray(d["X"]), np.asfortranarray(d["basis"])
     B = Bm.shape[1] + 1
+    sy, my = float(d["moments"][0, 1]), float(d["moments"][0, 0])
     Kc = A.KernelClass_SE_R6 if kernel == "SE" else A.KernelClass_Matern32_R6
-    k = Kc(2, B, d["theta0"], float(d["moments"][0, 1]))
+    # (1) anchored
+    m = A.DeviceModel(kernel, 300, 2, B)
+    m.set_data(y, X, Bm, sy)
+    for it in range(1, 21):
+        th = (d["theta0"] if it == 1 else d["thetas"][it - 2]).copy()
+        g, st, _ = m.para_update(it, th)
+        close(st, d["stats"][it - 1])
+        close(g, d["grads"][it - 1])
+    # (2) free run
+    k = Kc(2, B, d["theta0"], sy)
     opt = A.set_optimizer("Nadam", k, 0.01, 0.0, 0.9, 0.999, True, 1.0)
     for it in range(1, 21):
         st = k.para_update(it, y, X, Bm, opt, verbose=False)
         close(st, d["stats"][it - 1], 1e-6, 1e-9)
-        close(k.parameters, d["thetas"][it - 1], 1e-6, 1e-9)
-    pr = k.predict(y, X, Bm, X, Bm, float(d["moments"][0, 0]), float(d["moments"][0, 1]))
+        close(k.parameters, d["thetas"][it - 1], 1e-5, 1e-9)
+    # (3) prediction (Q6: inverse of theta_{T-1}, kernels at theta_T)
+    k.parameters = d["thetas"][18].copy()
+    k.para_update(20, y, X, Bm, A.set_optimizer("GD", k, 0.0, 0.0, 0.9, 0.999, False, 1.0),
+                  verbose=False)
+    k.parameters = d["thetas"][19].copy()
+    pr = k.predict(y, X, Bm, X, Bm, my, sy)
     close(pr["map"], d["pred_map"], 1e-6, 1e-9)
-    close(pr["var"], d["pred_var"], 1e-6, 1e-9)
+    sym = A.kernmat_SE_symmetric_cpp if kernel == "SE" else A.kernmat_Matern32_symmetric_cpp
+    kxx = np.diag(sym(X, Bm, d["thetas"][19])["full"])
+    terms = sy ** 2 * (2 * np.abs(kxx) + abs(np.exp(d["thetas"][19][0])))
+    assert np.all(np.abs(pr["var"] - d["pred_var"]) <= 1e-6 * terms), \
+        np.max(np.abs(pr["var"] - d["pred_var"]) / terms)
 
 
 def test_ace_train_and_predict_end_to_end(A):
