@@ -17,7 +17,8 @@ using namespace ace;
 
 struct ace_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // main stream (every ABI call syncs it)
+  hipStream_t side = nullptr;    // sweep lookahead: panel factorisation
   std::string err;
 };
 
@@ -223,6 +224,7 @@ int ace_create(int device, ace_ctx **out) {
   ace_ctx *c = new ace_ctx();
   c->device = device;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (e != hipSuccess) {
     g_create_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
     delete c;
@@ -236,6 +238,7 @@ void ace_destroy(ace_ctx *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   delete ctx;
 }
 
@@ -300,32 +303,52 @@ int ace_kernmat_cross(ace_ctx *ctx, int kind, int64_t n1, int64_t n2, int p, int
 // ------------------------------------------------------------ inverse
 namespace {
 struct SweepWork {
-  DBuf A, P, W, SW, S, piv, flag;
+  DBuf A, P0, P1, W0, W1, SW, S, piv, flag;
+  std::vector<hipEvent_t> ev;
   int64_t n = 0, npad = 0, naug = 0;
+  SweepWork() = default;
+  SweepWork(const SweepWork &) = delete;
+  ~SweepWork() {
+    for (auto &e : ev) (void)hipEventDestroy(e);
+  }
   void ensure(ace_ctx *ctx, int64_t n_) {
     n = n_;
     npad = round_up(n, NB);
     naug = npad + AUG;
     alloc(ctx, A, (size_t)(naug * naug) * sizeof(double), "alloc A");
-    alloc(ctx, P, (size_t)(naug * NB) * sizeof(double), "alloc P");
-    alloc(ctx, W, (size_t)(naug * NB) * sizeof(double), "alloc W");
+    for (DBuf *b : {&P0, &P1, &W0, &W1}) alloc(ctx, *b, (size_t)(naug * NB) * sizeof(double), "alloc panel");
     alloc(ctx, SW, (size_t)(SUB * SUB) * sizeof(double), "alloc SW");
     alloc(ctx, S, (size_t)(SUB * NB) * sizeof(double), "alloc S");
     alloc(ctx, piv, (size_t)npad * sizeof(double), "alloc piv");
     alloc(ctx, flag, 16, "alloc flag");
+    const size_t need = (size_t)(2 * (npad / NB) + 1);
+    while (ev.size() < need) {
+      hipEvent_t e;
+      ck(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+      ev.push_back(e);
+    }
   }
   SweepBufs bufs() const {
     SweepBufs b;
     b.A = A.d();
     b.ld = naug;
     b.npad = npad;
-    b.P = P.d();
-    b.W = W.d();
+    b.P[0] = P0.d();
+    b.P[1] = P1.d();
+    b.W[0] = W0.d();
+    b.W[1] = W1.d();
     b.SW = SW.d();
     b.S = S.d();
     b.piv = piv.d();
     b.flag = flag.i();
     return b;
+  }
+  SweepSync sync(ace_ctx *ctx) {
+    SweepSync s;
+    s.side = ctx->side;
+    s.ev = ev.data();
+    s.nev = (int)ev.size();
+    return s;
   }
 };
 }  // namespace
@@ -344,7 +367,8 @@ int ace_invkernel(ace_ctx *ctx, int64_t n, const double *K, double sigma, double
      "prepare A");
   ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, 0, nullptr, ctx->stream), "aug init");
   ck(ctx, hipMemsetAsync(w.flag.p, 0, sizeof(int), ctx->stream), "memset flag");
-  ck(ctx, run_sweep(w.bufs(), ctx->stream, nullptr, 0, nullptr), "sweep");
+  const SweepSync sy = w.sync(ctx);
+  ck(ctx, run_sweep(w.bufs(), ctx->stream, &sy, nullptr), "sweep");
   int flag = 0;
   ck(ctx, hipMemcpyAsync(&flag, w.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
      "download flag");
@@ -643,6 +667,8 @@ struct ace_model {
   bool prof = false;
   hipEvent_t ev_asm[2] = {nullptr, nullptr}, ev_grad[2] = {nullptr, nullptr};
   std::vector<hipEvent_t> ev_upd;
+  std::vector<double> upd_flops;
+  int upd_used = 0;
   double t_ms[3] = {0, 0, 0};
   int64_t t_launch[3] = {0, 0, 0};
   double t_work[3] = {0, 0, 0};
@@ -666,10 +692,13 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   if (timed) ck(ctx, hipEventRecord(m->ev_asm[1], st), "event");
   ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, m->n, m->y.d(), st), "aug init");
   ck(ctx, hipMemsetAsync(w.flag.p, 0, sizeof(int), st), "memset flag");
-  int used = 0;
-  ck(ctx, run_sweep(w.bufs(), st, timed ? m->ev_upd.data() : nullptr,
-                    timed ? (int)m->ev_upd.size() : 0, &used),
-     "sweep");
+  const SweepSync sy = w.sync(ctx);
+  SweepTiming tmg;
+  tmg.ev = m->ev_upd.data();
+  tmg.nev = (int)m->ev_upd.size();
+  tmg.used = &m->upd_used;
+  tmg.flops = m->upd_flops.data();
+  ck(ctx, run_sweep(w.bufs(), st, &sy, timed ? &tmg : nullptr), "sweep");
   ck(ctx, launch_alpha_from_aug(w.A.d(), w.naug, w.npad, m->n, theta[1], use_mu, m->alpha.d(),
                                 m->scal.d(), st),
      "alpha");
@@ -685,10 +714,10 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   ck(ctx, launch_final_sums(m->y.d(), m->scal.d() + 4, m->alpha.d(), m->ka.d(), m->n, w.piv.d(),
                             w.npad, m->sums.d(), st),
      "final sums");
-  (void)used;
 }
 
-void model_collect_timing(ace_model *m, int nupd) {
+void model_collect_timing(ace_model *m) {
+  const int nupd = m->upd_used;
   float ms = 0.f;
   ck(m->ctx, hipEventElapsedTime(&ms, m->ev_asm[0], m->ev_asm[1]), "elapsed");
   m->t_ms[1] += ms;
@@ -701,11 +730,11 @@ void model_collect_timing(ace_model *m, int nupd) {
        "elapsed");
     m->t_ms[0] += ms;
     m->t_launch[0] += 1;
+    m->t_work[0] += m->upd_flops[(size_t)(j / 2)];
   }
   const double n = (double)m->n, pairs = n * (n + 1) / 2, B = m->s.B, p = m->s.p;
-  // algorithmic work: dense n^3 over the update launches,
-  // pair kernels by their flop formulas
-  m->t_work[0] += n * n * n;
+  // work: the update launches' GEMM flops (counted per launch
+  // from its tiles), pair kernels by their algorithmic flop formulas
   m->t_work[1] += pairs * B * (3 * p + 3);
   m->t_work[2] += pairs * (4 * B * p + 2 * p) + (m->s.kind == ACE_KERNEL_MATERN32 ? pairs * B * p : 0);
 }
@@ -743,6 +772,7 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
     ck(ctx, hipMemsetAsync(m->sw.A.p, 0, m->sw.A.bytes, ctx->stream), "memset A");
     const int steps = (int)(m->npad / NB);
     m->ev_upd.assign((size_t)(2 * steps), nullptr);
+    m->upd_flops.assign((size_t)steps, 0.0);
     for (auto &e : m->ev_upd) ck(ctx, hipEventCreate(&e), "event");
     for (int j = 0; j < 2; ++j) {
       ck(ctx, hipEventCreate(&m->ev_asm[j]), "event");
@@ -809,7 +839,7 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, d
   ck(ctx, hipMemcpyAsync(&flag, m->sw.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
      "download flag");
   sync(ctx);
-  if (timed) model_collect_timing(m, (int)m->ev_upd.size());
+  if (timed) model_collect_timing(m);
   if (iter == 1) theta[1] = scal[3];  // mean_solution before the gradient (R/kernel_SE_R6.R:45)
   compose_grad(s, theta, gs.data(), sums[2], grad);
   stats[0] = m->std_y * std::sqrt(sums[0]) / std::sqrt((double)m->n);

@@ -61,20 +61,33 @@ struct SweepBufs {
   double *A;      // Naug x Naug, col-major, ld = Naug, lower triangle used
   int64_t ld;     // Naug
   int64_t npad;   // multiple of NB
-  double *P;      // Naug x NB : -panel (negated copy)
-  double *W;      // Naug x NB : panel being swept
+  double *P[2];   // Naug x NB : -panel (negated copy), double-buffered by step
+  double *W[2];   // Naug x NB : panel being swept, double-buffered by step
   double *SW;     // SUB x SUB
   double *S;      // SUB x NB  : pivot rows before their sub-sweep
   double *piv;    // npad pivots
   int *flag;      // set to 1 on a non-positive / non-finite pivot
 };
+// Lookahead: the panel sweep of step k+1 runs on `side` while the main
+// stream updates the rest of step k.  `ev` needs 2*steps + 1 events.
+struct SweepSync {
+  hipStream_t side;
+  hipEvent_t *ev;
+  int nev;
+};
+// Optional timing of the dominant update launches (k_update<false>): event
+// pairs in ev, executed GEMM flops per timed launch in flops[].
+struct SweepTiming {
+  hipEvent_t *ev;
+  int nev;
+  int *used;
+  double *flops;
+};
 // Runs every step; A's K block ends holding -A^-1 (lower), the AUG rows hold
-// (A^-1 R)^T and the corner -R^T A^-1 R.  `update_ms` (nullable) receives
-// per-launch events of the update kernel when `ev` is non-null.
-hipError_t run_sweep(const SweepBufs &b, hipStream_t st, hipEvent_t *ev,
-                     int nev, int *nev_used);
-// flops of one sweep's update-kernel launches (algorithmic, lower tiles)
-double sweep_update_flops(int64_t naug);
+// (A^-1 R)^T and the corner -R^T A^-1 R.
+hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sync,
+                     const SweepTiming *timing);
+int64_t update_gemm_tiles(int64_t naug, int64_t k0, int kx, bool look);
 
 // ---- small helpers -----------------------------------------------------------
 hipError_t launch_aug_init(double *A, int64_t ld, int64_t npad, int64_t n,

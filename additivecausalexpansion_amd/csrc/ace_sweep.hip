@@ -70,140 +70,147 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
 }
 
 // ---------------------------------------------------------------- pivot
-// Sweeps the 64x64 sub-block s of the panel's pivot rows in LDS:
+// Sweeps the 64x64 sub-block s of the panel's pivot rows:
 //   d = D_tt; D_ij -= D_it D_tj / d; D_it /= d; D_tj /= d; D_tt = -1/d
-// -> SW = -D_s^-1.  Also snapshots the 64 pivot rows (all NB columns) into S
-// before the panel kernel overwrites them.  Records every pivot d.
+// -> SW = -D_s^-1 (exactly symmetric: every product is formed as a*b with
+// a = D_it = D_ti).  Layout: lane = row i, wave w keeps columns 16w..16w+15
+// in registers; per pivot the owning wave publishes column t and lane t of
+// every wave publishes its part of row t through double-buffered LDS
+// vectors, so there is one barrier per pivot.  Also snapshots the 64 pivot
+// rows (all NB columns, row-major) into S before the panel kernel
+// overwrites them, and records every pivot d (Cholesky diagonal squared).
 __global__ __launch_bounds__(256) void k_pivot(const double *__restrict__ W, int64_t ldp,
                                                int64_t k0, int s, double *__restrict__ SW,
                                                double *__restrict__ S, double *__restrict__ piv,
                                                int *__restrict__ flag) {
-  __shared__ double D[SUB][SUB + 1];
+  __shared__ double tileT[64][65];
+  __shared__ double colb[2][SUB];
+  __shared__ double rowb[2][SUB];
   const int64_t p0 = k0 + (int64_t)s * SUB;
-  const int tid = threadIdx.x;
-  for (int e = tid; e < SUB * SUB; e += 256) {
-    const int a = e & 63, b = e >> 6;
-    D[a][b] = W[(p0 + a) + (int64_t)(s * SUB + b) * ldp];
-  }
-  for (int e = tid; e < SUB * NB; e += 256) {
-    const int a = e & 63, j = e >> 6;
-    S[a + j * SUB] = W[(p0 + a) + (int64_t)j * ldp];
-  }
-  __syncthreads();
-  const int i = tid & 63, jb = tid >> 6;
-  for (int t = 0; t < SUB; ++t) {
-    const double d = D[t][t];
-    const double rd = 1.0 / d;
-    const double dit = D[i][t];
-    double v[SUB / 4];
-#pragma unroll
-    for (int q = 0; q < SUB / 4; ++q) {
-      const int j = jb + 4 * q;
-      const double dtj = D[t][j];
-      const double dij = D[i][j];
-      double x;
-      if (i == t) x = (j == t) ? -rd : dtj * rd;
-      else if (j == t) x = dit * rd;
-      else x = fma(-(dit * dtj), rd, dij);
-      v[q] = x;
-    }
-    if (tid == 0) {
-      piv[p0 + t] = d;
-      if (!(d > 0.0) || !isfinite(d)) *flag = 1;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // S[a*NB + j] = W[p0 + a, j]  (transposed through LDS, coalesced both ways)
+  for (int cb = 0; cb < NB / 64; ++cb) {
+    for (int e = tid; e < 4096; e += 256) {
+      const int a = e & 63, b = e >> 6;
+      tileT[a][b] = W[(p0 + a) + (int64_t)(64 * cb + b) * ldp];
     }
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < SUB / 4; ++q) D[i][jb + 4 * q] = v[q];
+    for (int e = tid; e < 4096; e += 256) {
+      const int b = e & 63, a = e >> 6;
+      S[a * NB + 64 * cb + b] = tileT[a][b];
+    }
     __syncthreads();
   }
-  for (int e = tid; e < SUB * SUB; e += 256) {
-    const int a = e & 63, b = e >> 6;
-    SW[a + b * SUB] = D[a][b];
+  double v[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = W[(p0 + lane) + (int64_t)(s * SUB + 16 * w + q) * ldp];
+  bool bad = false;
+  for (int tw = 0; tw < 4; ++tw) {
+#pragma unroll
+    for (int tq = 0; tq < 16; ++tq) {
+      const int t = 16 * tw + tq;
+      const int buf = tq & 1;
+      if (w == tw) colb[buf][lane] = v[tq];
+      if (lane == t) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) rowb[buf][16 * w + q] = v[q];
+      }
+      __syncthreads();
+      const double d = rowb[buf][t];
+      const double rd = 1.0 / d;
+      const double dit = colb[buf][lane];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int j = 16 * w + q;
+        const double dtj = rowb[buf][j];
+        double x;
+        if (lane == t) x = (j == t) ? -rd : dtj * rd;
+        else if (j == t) x = dit * rd;
+        else x = fma(-(dit * dtj), rd, v[q]);
+        v[q] = x;
+      }
+      if (tid == 0) {
+        piv[p0 + t] = d;
+        bad |= !(d > 0.0) || !isfinite(d);
+      }
+    }
   }
+  if (tid == 0 && bad) *flag = 1;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) SW[lane + (16 * w + q) * SUB] = v[q];
 }
 
 // ---------------------------------------------------------------- panel
-// Applies sub-pivot s to 64 rows of the panel W (Naug x NB):
+// Applies sub-pivot s to 64 rows of the panel W (Naug x NB), on MFMA:
 //   other rows : V = -W[:, s] SW (= W_is D_s^-1); W[:, s] = V;
 //                W[:, j] -= V S[:, j]            (j outside s)
 //   pivot rows : V = SW;  W[:, s] = SW;  W[:, j] = -SW S[:, j] (= D_s^-1 S)
+// Wave w owns rows 16w..16w+15.  Phase 1 forms Vn^T = -V^T = SW W_is^T
+// (SW is symmetric) so that its accumulator fragments are directly the B
+// operands of phase 2's D = S_chunk^T Vn^T + W_chunk^T (no LDS round trip).
+constexpr int PLD = 80;  // LDS pitch: 64 + 16 doubles, conflict-free fragment reads
+
 __global__ __launch_bounds__(256) void k_panel(double *__restrict__ W, int64_t ldp, int64_t k0,
                                                int s, const double *__restrict__ SW,
                                                const double *__restrict__ S) {
-  __shared__ double sSW[SUB][SUB + 1];
-  __shared__ double sV[SUB][SUB + 1];
-  __shared__ double sX[SUB][SUB + 1];
+  __shared__ double sSW[SUB][PLD];  // sSW[b][a] = SW(a, b)
+  __shared__ double sS[SUB][PLD];   // sS[t][c]  = S(t, 64 cc + c)
   const int64_t i0 = (int64_t)blockIdx.x * SUB;
   const bool pivrows = (i0 == k0 + (int64_t)s * SUB);
-  const int tid = threadIdx.x;
-  const int ra = tid & 15, cb = tid >> 4;  // rows ra+16q, cols cb+16q
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
   for (int e = tid; e < SUB * SUB; e += 256) {
     const int a = e & 63, b = e >> 6;
-    sSW[a][b] = SW[a + b * SUB];
-    if (!pivrows) sX[a][b] = W[(i0 + a) + (int64_t)(s * SUB + b) * ldp];
+    sSW[b][a] = SW[a + b * SUB];
   }
   __syncthreads();
-  double acc[4][4];
+  const int64_t row = i0 + 16 * w + lr;
+  d4 acc1[4];
   if (pivrows) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) acc[q][qq] = sSW[ra + 16 * q][cb + 16 * qq];
+      for (int j = 0; j < 4; ++j) acc1[ct][j] = -sSW[16 * ct + lk + 4 * j][16 * w + lr];
   } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int ct = 0; ct < 4; ++ct) acc1[ct] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) acc[q][qq] = 0.0;
-    for (int t = 0; t < SUB; ++t) {
-      double xa[4], sb[4];
+    for (int kk = 0; kk < SUB / 4; ++kk) {
+      const double b = W[row + (int64_t)(s * SUB + 4 * kk + lk) * ldp];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) xa[q] = sX[ra + 16 * q][t];
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) sb[qq] = sSW[t][cb + 16 * qq];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) acc[q][qq] = fma(-xa[q], sb[qq], acc[q][qq]);
+      for (int ct = 0; ct < 4; ++ct)
+        acc1[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(sSW[4 * kk + lk][16 * ct + lr], b,
+                                                        acc1[ct], 0, 0, 0);
     }
   }
+  // acc1[ct][j] = Vn[i = row][t' = 16 ct + lk + 4 j];  W[:, s] = V = -Vn
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      sV[ra + 16 * q][cb + 16 * qq] = acc[q][qq];
-      W[(i0 + ra + 16 * q) + (int64_t)(s * SUB + cb + 16 * qq) * ldp] = acc[q][qq];
-    }
-  __syncthreads();
+    for (int j = 0; j < 4; ++j)
+      W[row + (int64_t)(s * SUB + 16 * ct + lk + 4 * j) * ldp] = -acc1[ct][j];
   for (int cc = 0; cc < NB / SUB; ++cc) {
     if (cc == s) continue;
+    __syncthreads();
     for (int e = tid; e < SUB * SUB; e += 256) {
-      const int a = e & 63, b = e >> 6;
-      sX[a][b] = S[a + (int64_t)(cc * SUB + b) * SUB];
+      const int c = e & 63, t = e >> 6;
+      sS[t][c] = S[t * NB + cc * SUB + c];
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int ctc = 0; ctc < 4; ++ctc) {
+      d4 acc;
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq)
-        acc[q][qq] = pivrows ? 0.0
-                             : W[(i0 + ra + 16 * q) + (int64_t)(cc * SUB + cb + 16 * qq) * ldp];
-    for (int t = 0; t < SUB; ++t) {
-      double va[4], sb[4];
+      for (int j = 0; j < 4; ++j)
+        acc[j] = pivrows ? 0.0 : W[row + (int64_t)(cc * SUB + 16 * ctc + lk + 4 * j) * ldp];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) va[q] = sV[ra + 16 * q][t];
+      for (int kk = 0; kk < SUB / 4; ++kk)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sS[4 * kk + lk][16 * ctc + lr],
+                                                   acc1[kk >> 2][kk & 3], acc, 0, 0, 0);
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) sb[qq] = sX[t][cb + 16 * qq];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) acc[q][qq] = fma(-va[q], sb[qq], acc[q][qq]);
+      for (int j = 0; j < 4; ++j)
+        W[row + (int64_t)(cc * SUB + 16 * ctc + lk + 4 * j) * ldp] = acc[j];
     }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq)
-        W[(i0 + ra + 16 * q) + (int64_t)(cc * SUB + cb + 16 * qq) * ldp] = acc[q][qq];
-    __syncthreads();
   }
 }
 
@@ -217,14 +224,38 @@ constexpr int BK = 16;      // panel columns staged per LDS buffer
 constexpr int LDL = 144;    // LDS row pitch (doubles): 128 + 16, bank-conflict free
 constexpr int NCH = NB / BK;
 
+// LOOK = true : only the "cross" tiles of block kx (tiles with I or J in
+//               block kx) -- the lookahead that the next step's panel needs;
+// LOOK = false: every lower tile except the cross of block kx (kx < 0: all).
+template <bool LOOK>
 __global__ __launch_bounds__(256, 2) void k_update(double *__restrict__ A, int64_t ld,
                                                    const double *__restrict__ W,
                                                    const double *__restrict__ Pn, int64_t ldp,
-                                                   int64_t k0) {
+                                                   int64_t k0, int kx) {
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
-  const int J = blockIdx.x, I = blockIdx.y;
-  if (J > I) return;
+  constexpr int KT = NB / UT;
+  int I, J;
+  if (LOOK) {
+    // grid (nT, 2*KT): y < KT -> row kx*KT+y, J = x <= I ; y >= KT -> column
+    // kx*KT+(y-KT), I = x strictly below block kx
+    const int y = blockIdx.y;
+    if (y < KT) {
+      I = kx * KT + y;
+      J = blockIdx.x;
+      if (J > I) return;
+    } else {
+      J = kx * KT + (y - KT);
+      I = blockIdx.x;
+      if (I < (kx + 1) * KT) return;
+    }
+  } else {
+    J = blockIdx.x;
+    I = blockIdx.y;
+    if (J > I) return;
+    if (kx >= 0 && ((I >= kx * KT && I < (kx + 1) * KT) || (J >= kx * KT && J < (kx + 1) * KT)))
+      return;
+  }
   const int kt0 = (int)(k0 / UT), kt1 = kt0 + NB / UT;
   const bool Ik = I >= kt0 && I < kt1, Jk = J >= kt0 && J < kt1;
   const int64_t R0 = (int64_t)I * UT, C0 = (int64_t)J * UT;
@@ -331,52 +362,95 @@ __global__ __launch_bounds__(256, 2) void k_update(double *__restrict__ A, int64
     }
 }
 
-double sweep_update_flops(int64_t naug) {
-  // lower tiles outside the pivot block, 2*UT*UT*NB flops each, summed over steps
-  const int64_t nT = naug / UT;
-  const int64_t steps = (naug - AUG) / NB;
-  const int64_t kt = NB / UT;
-  const int64_t tiles_total = nT * (nT + 1) / 2;
-  // tiles touching block k: kt rows x (column tiles) ... count exactly per step
-  double flops = 0.0;
-  for (int64_t k = 0; k < steps; ++k) {
-    const int64_t kt0 = k * kt, kt1 = kt0 + kt;
-    int64_t touching = 0;
-    for (int64_t I = 0; I < nT; ++I) {
-      const bool Ik = I >= kt0 && I < kt1;
-      if (Ik) touching += I + 1;  // J = 0..I
-      else if (I >= kt1) touching += kt;  // J in block k
-    }
-    flops += (double)(tiles_total - touching) * 2.0 * UT * UT * NB;
+static hipError_t panel_sweep(const SweepBufs &b, int buf, int64_t k0, hipStream_t st) {
+  const int64_t naug = b.ld;
+  hipLaunchKernelGGL(k_gather, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st, b.A, b.ld,
+                     k0, b.P[buf], b.W[buf], b.ld);
+  for (int s = 0; s < NB / SUB; ++s) {
+    hipLaunchKernelGGL(k_pivot, dim3(1), dim3(256), 0, st, b.W[buf], b.ld, k0, s, b.SW, b.S,
+                       b.piv, b.flag);
+    hipLaunchKernelGGL(k_panel, dim3((unsigned)(naug / SUB)), dim3(256), 0, st, b.W[buf], b.ld,
+                       k0, s, b.SW, b.S);
   }
-  return flops;
+  return hipGetLastError();
 }
 
-hipError_t run_sweep(const SweepBufs &b, hipStream_t st, hipEvent_t *ev, int nev,
-                     int *nev_used) {
+int64_t update_gemm_tiles(int64_t naug, int64_t k0, int kx, bool look) {
+  const int64_t nT = naug / UT, KT = NB / UT, kt0 = k0 / UT, kt1 = kt0 + KT;
+  int64_t cnt = 0;
+  for (int64_t I = 0; I < nT; ++I)
+    for (int64_t J = 0; J <= I; ++J) {
+      const bool inx = kx >= 0 && ((I >= kx * KT && I < (kx + 1) * KT) ||
+                                   (J >= kx * KT && J < (kx + 1) * KT));
+      if (inx != look) continue;
+      const bool Ik = I >= kt0 && I < kt1, Jk = J >= kt0 && J < kt1;
+      if (!(Ik || Jk)) ++cnt;
+    }
+  return cnt;
+}
+
+// Step k: panel sweep k (side stream, overlapped with the previous update),
+// then on the main stream the cross tiles of block k+1 (so panel k+1 can
+// start) and the remaining tiles.  P/W are double-buffered by step parity.
+hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
+                     const SweepTiming *tm) {
   const int64_t naug = b.ld;
   const unsigned nT = (unsigned)(naug / UT);
+  const int steps = (int)(b.npad / NB);
+  const bool two = sy && sy->side && sy->nev >= 2 * steps + 1;
+  hipStream_t side = two ? sy->side : st;
   int used = 0;
-  for (int64_t k0 = 0; k0 < b.npad; k0 += NB) {
-    hipLaunchKernelGGL(k_gather, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st, b.A,
-                       b.ld, k0, b.P, b.W, b.ld);
-    for (int s = 0; s < NB / SUB; ++s) {
-      hipLaunchKernelGGL(k_pivot, dim3(1), dim3(256), 0, st, b.W, b.ld, k0, s, b.SW, b.S,
-                         b.piv, b.flag);
-      hipLaunchKernelGGL(k_panel, dim3((unsigned)(naug / SUB)), dim3(256), 0, st, b.W, b.ld,
-                         k0, s, b.SW, b.S);
-    }
-    if (ev && used + 2 <= nev) (void)hipEventRecord(ev[used], st);
-    hipLaunchKernelGGL(k_update, dim3(nT, nT), dim3(256), 0, st, b.A, b.ld, b.W, b.P, b.ld,
-                       k0);
-    if (ev && used + 2 <= nev) {
-      (void)hipEventRecord(ev[used + 1], st);
-      used += 2;
-    }
-    hipError_t e = hipGetLastError();
+  hipError_t e;
+  if (two) {
+    e = hipEventRecord(sy->ev[2 * steps], st);  // inputs ready
+    if (e != hipSuccess) return e;
+    e = hipStreamWaitEvent(side, sy->ev[2 * steps], 0);
     if (e != hipSuccess) return e;
   }
-  if (nev_used) *nev_used = used;
+  e = panel_sweep(b, 0, 0, side);
+  if (e != hipSuccess) return e;
+  if (two) {
+    e = hipEventRecord(sy->ev[0], side);
+    if (e != hipSuccess) return e;
+  }
+  for (int k = 0; k < steps; ++k) {
+    const int buf = k & 1;
+    const int64_t k0 = (int64_t)k * NB;
+    const bool more = k + 1 < steps;
+    if (two) {
+      e = hipStreamWaitEvent(st, sy->ev[2 * k], 0);  // panel k done
+      if (e != hipSuccess) return e;
+    }
+    if (more) {
+      hipLaunchKernelGGL(k_update<true>, dim3(nT, 2 * (NB / UT)), dim3(256), 0, st, b.A, b.ld,
+                         b.W[buf], b.P[buf], b.ld, k0, k + 1);
+      if (two) {
+        e = hipEventRecord(sy->ev[2 * k + 1], st);  // cross of block k+1 updated
+        if (e != hipSuccess) return e;
+        e = hipStreamWaitEvent(side, sy->ev[2 * k + 1], 0);
+        if (e != hipSuccess) return e;
+      }
+      e = panel_sweep(b, buf ^ 1, k0 + NB, side);
+      if (e != hipSuccess) return e;
+      if (two) {
+        e = hipEventRecord(sy->ev[2 * (k + 1)], side);
+        if (e != hipSuccess) return e;
+      }
+    }
+    const bool timed = tm && tm->ev && used + 2 <= tm->nev;
+    if (timed) (void)hipEventRecord(tm->ev[used], st);
+    hipLaunchKernelGGL(k_update<false>, dim3(nT, nT), dim3(256), 0, st, b.A, b.ld, b.W[buf],
+                       b.P[buf], b.ld, k0, more ? k + 1 : -1);
+    if (timed) {
+      (void)hipEventRecord(tm->ev[used + 1], st);
+      if (tm->flops) tm->flops[used / 2] =
+          (double)update_gemm_tiles(naug, k0, more ? k + 1 : -1, false) * 2.0 * UT * UT * NB;
+      used += 2;
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (tm && tm->used) *tm->used = used;
   return hipSuccess;
 }
 
