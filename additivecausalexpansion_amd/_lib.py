@@ -13,7 +13,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libace_hip.so")
+LIB_PATH = os.environ.get("ACE_LIB_PATH") or os.path.join(_HERE, "libace_hip.so")
 
 ACE_KERNEL_SE = 0
 ACE_KERNEL_MATERN32 = 1

@@ -224,7 +224,13 @@ int ace_create(int device, ace_ctx **out) {
   ace_ctx *c = new ace_ctx();
   c->device = device;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+  if (e == hipSuccess) {
+    // the lookahead panel chain is latency-bound: give it the highest priority
+    // so its workgroups take the first free CU slots next to the update kernel
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi);
+  }
   if (e != hipSuccess) {
     g_create_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
     delete c;
@@ -303,7 +309,7 @@ int ace_kernmat_cross(ace_ctx *ctx, int kind, int64_t n1, int64_t n2, int p, int
 // ------------------------------------------------------------ inverse
 namespace {
 struct SweepWork {
-  DBuf A, P0, P1, W0, W1, SW, S, piv, flag;
+  DBuf A, P0, P1, W0, W1, SW, S0, S1, piv, flag;
   std::vector<hipEvent_t> ev;
   int64_t n = 0, npad = 0, naug = 0;
   SweepWork() = default;
@@ -318,7 +324,8 @@ struct SweepWork {
     alloc(ctx, A, (size_t)(naug * naug) * sizeof(double), "alloc A");
     for (DBuf *b : {&P0, &P1, &W0, &W1}) alloc(ctx, *b, (size_t)(naug * NB) * sizeof(double), "alloc panel");
     alloc(ctx, SW, (size_t)(SUB * SUB) * sizeof(double), "alloc SW");
-    alloc(ctx, S, (size_t)(SUB * NB) * sizeof(double), "alloc S");
+    alloc(ctx, S0, (size_t)(SUB * NB) * sizeof(double), "alloc S");
+    alloc(ctx, S1, (size_t)(SUB * NB) * sizeof(double), "alloc S");
     alloc(ctx, piv, (size_t)npad * sizeof(double), "alloc piv");
     alloc(ctx, flag, 16, "alloc flag");
     const size_t need = (size_t)(2 * (npad / NB) + 1);
@@ -338,7 +345,8 @@ struct SweepWork {
     b.W[0] = W0.d();
     b.W[1] = W1.d();
     b.SW = SW.d();
-    b.S = S.d();
+    b.S[0] = S0.d();
+    b.S[1] = S1.d();
     b.piv = piv.d();
     b.flag = flag.i();
     return b;
@@ -397,7 +405,7 @@ int ace_grad(ace_ctx *ctx, int kind, int64_t n, int p, int B, const double *y, c
   arg(ctx, n >= 1 && y && Kfull && inv && eigenval && theta && stats && grad, "null argument");
   arg(ctx, (p == 0 || X) && (B == 1 || Z), "null argument");
   SideBufs sb;
-  upload_side(ctx, sb, s, X, Z, n, n);
+  upload_side(ctx, sb, s, X, Z, n, (n + 63) / 64 * 64);  // k_grad reads whole 64-row tiles
   std::vector<double> tab = make_tab(theta, s);
   std::vector<double> ybar((size_t)n);
   for (int64_t r = 0; r < n; ++r) ybar[(size_t)r] = y[r] - theta[1];
@@ -420,8 +428,7 @@ int ace_grad(ace_ctx *ctx, int kind, int64_t n, int p, int B, const double *y, c
   // alpha = invKmatn * ybar (src/kernel_SE_cpp.cpp:215)
   ck(ctx, launch_gemv(dinv.d(), n, n, n, dyb.d(), dalpha.d(), ctx->stream), "gemv alpha");
   ck(ctx, launch_grad(kind, s.PM, sb.view(n), B, s.ZS, tab_view(dtab, s), dinv.d(), n, 1.0,
-                      dalpha.d(), Kel ? dC.d() : nullptr, dg.d(), dtr.d(), nullptr, n,
-                      ctx->stream),
+                      dalpha.d(), Kel ? dC.d() : nullptr, dg.d(), dtr.d(), ctx->stream),
      "grad");
   ck(ctx, launch_colsum(dg.d(), nt, ncol, dgs.d(), ctx->stream), "colsum");
   ck(ctx, launch_colsum(dtr.d(), nt, 1, dgs.d() + ncol, ctx->stream), "colsum tr");
@@ -661,7 +668,7 @@ struct ace_model {
   double std_y = 1.0;
   bool has_data = false;
   SideBufs side;
-  DBuf y, tab, alpha, scal, gpart, trpart, kapart, ka, gsum, sums;
+  DBuf y, tab, alpha, scal, gpart, trpart, kapart, ka, gsum, sums, kcopy;
   SweepWork sw;   // A = resident inverse of the last para_update
   SweepWork sw2;  // train_stats scratch (keeps sw's inverse, Q6)
   bool prof = false;
@@ -687,7 +694,7 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   const PairSide ps = m->side.view(m->n);
   if (timed) ck(ctx, hipEventRecord(m->ev_asm[0], st), "event");
   ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, std::exp(theta[0]),
-                          w.A.d(), w.naug, nullptr, st),
+                          w.A.d(), w.naug, m->kcopy.d(), st),
      "assembly");
   if (timed) ck(ctx, hipEventRecord(m->ev_asm[1], st), "event");
   ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, m->n, m->y.d(), st), "aug init");
@@ -704,9 +711,11 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
      "alpha");
   if (timed) ck(ctx, hipEventRecord(m->ev_grad[0], st), "event");
   ck(ctx, launch_grad(s.kind, s.PM, ps, s.B, s.ZS, tv, w.A.d(), w.naug, -1.0, m->alpha.d(),
-                      nullptr, m->gpart.d(), m->trpart.d(), m->kapart.d(), w.npad, st),
+                      nullptr, m->gpart.d(), m->trpart.d(), st),
      "grad");
   if (timed) ck(ctx, hipEventRecord(m->ev_grad[1], st), "event");
+  ck(ctx, launch_symv_tiles(m->kcopy.d(), w.naug, m->n, m->alpha.d(), m->kapart.d(), w.npad, st),
+     "symv");
   const int ncol = s.B * (s.PM + 1);
   ck(ctx, launch_colsum(m->gpart.d(), m->ntiles, ncol, m->gsum.d(), st), "colsum");
   ck(ctx, launch_colsum(m->trpart.d(), m->ntiles, 1, m->gsum.d() + ncol, st), "colsum");
@@ -766,6 +775,7 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
     alloc(ctx, m->gpart, (size_t)(m->ntiles * s.B * (s.PM + 1)) * sizeof(double), "alloc gpart");
     alloc(ctx, m->trpart, (size_t)m->ntiles * sizeof(double), "alloc trpart");
     alloc(ctx, m->kapart, (size_t)(m->ntr * m->npad) * sizeof(double), "alloc kapart");
+    alloc(ctx, m->kcopy, (size_t)(m->naug * m->naug) * sizeof(double), "alloc Kfull copy");
     alloc(ctx, m->ka, (size_t)m->npad * sizeof(double), "alloc ka");
     alloc(ctx, m->gsum, (size_t)(s.B * (s.PM + 1) + 1) * sizeof(double), "alloc gsum");
     alloc(ctx, m->sums, 8 * sizeof(double), "alloc sums");

@@ -7,7 +7,10 @@
 namespace ace {
 
 // Sweep (Gauss-Jordan SPD inversion) blocking; see DESIGN.md §3.
-constexpr int NB = 256;    // outer pivot block = panel width
+#ifndef ACE_NB
+#define ACE_NB 256
+#endif
+constexpr int NB = ACE_NB;  // outer pivot block = panel width
 constexpr int SUB = 64;    // inner pivot block, eliminated inside LDS
 constexpr int UT = 128;    // update tile (MFMA f64 16x16x4, 4 waves x 64x64)
 constexpr int AUG = 128;   // augmented right-hand-side rows (y, 1) appended to A
@@ -35,7 +38,8 @@ struct PairSide {
 
 // ---- assembly --------------------------------------------------------------
 // mode 0: fused eval -- lower 64-tiles of the n_pad x n_pad block of A (ld),
-//         value K + sig on the diagonal, identity on padding rows/cols.
+//         value K + sig on the diagonal, identity on padding rows/cols; if
+//         cube is non-null it receives the lower Kfull copy (same ld).
 // mode 1: symmetric ABI output -- full n x n Kfull (ld = n) + optional cube.
 // mode 2: cross ABI output -- n1 x n2 Kfull + optional cube.
 hipError_t launch_assembly(int mode, int kind, int PM, PairSide rows,
@@ -44,17 +48,21 @@ hipError_t launch_assembly(int mode, int kind, int PM, PairSide rows,
                            double *cube, hipStream_t st);
 
 // ---- gradient --------------------------------------------------------------
-// T = sA * A[r,c] - alpha_r alpha_c over lower 64-tiles of [0,n).
-// gpart: [(b*(PM+1) + i) * ntiles + tile]  (i < PM: length-scale sums,
-//        i == PM: lambda sums); trpart[tile]: trace of T;
-// kapart (if non-null): [T * npad + x], partial rows of Kfull * alpha.
+// T = sA * A[r,c] - alpha_r alpha_c over the lower 64x64 tiles of [0,n)
+// (grad_ntiles(n) of them).
+// gpart: [(b*(PM+1) + i) * nsuper + tile]  (i < PM: length-scale sums,
+//        i == PM: lambda sums); trpart[tile]: trace of T.
 // cube (if non-null, ld n): K_b read from the cube instead of recomputed.
 hipError_t launch_grad(int kind, int PM, PairSide side, int B, int ZS,
                        TabView tab, const double *A, int64_t ld, double sA,
                        const double *alpha, const double *cube,
-                       double *gpart, double *trpart, double *kapart,
-                       int64_t npad, hipStream_t st);
+                       double *gpart, double *trpart, hipStream_t st);
 int64_t grad_ntiles(int64_t n);
+// Kfull * alpha partial rows from a lower-triangle copy of Kfull (ld):
+// kapart[T * npad + x] for 64-tile slot T; sum over T with launch_rowsum.
+hipError_t launch_symv_tiles(const double *K, int64_t ld, int64_t n,
+                             const double *alpha, double *kapart, int64_t npad,
+                             hipStream_t st);
 
 // ---- sweep -----------------------------------------------------------------
 struct SweepBufs {
@@ -64,7 +72,7 @@ struct SweepBufs {
   double *P[2];   // Naug x NB : -panel (negated copy), double-buffered by step
   double *W[2];   // Naug x NB : panel being swept, double-buffered by step
   double *SW;     // SUB x SUB
-  double *S;      // SUB x NB  : pivot rows before their sub-sweep
+  double *S[2];   // SUB x NB col-major: pivot rows before their sub-sweep (ping-pong)
   double *piv;    // npad pivots
   int *flag;      // set to 1 on a non-positive / non-finite pivot
 };

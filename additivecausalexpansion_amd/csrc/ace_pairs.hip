@@ -118,6 +118,8 @@ __global__ __launch_bounds__(256) void k_assembly(PairSide R, PairSide C, int64_
     }
     if (MODE == 0) {
       out[r + c * ld] = (r == c) ? kf + sig : kf;
+      if (cube) cube[r + c * ld] = kf;  // Kfull copy for the RMSE product (the sweep
+                                        // overwrites out)
     } else {
       out[r + c * ld] = kf;
       if (MODE == 1 && c != r) out[c + r * ld] = kf;
@@ -133,45 +135,65 @@ __global__ __launch_bounds__(256) void k_assembly(PairSide R, PairSide C, int64_
 //        length sums  sum T K_b d_i^2                 (SE, 161-188)
 //                     sum T K_b/(1+sqrt(3 r~2)) d_i^2 (Matern32, kernel_Matern 340-377;
 //                     r~2 uses the gradient-indexed weights wg)
+// One 64x64 lower tile per workgroup; T stays in registers (16 pairs per
+// lane) while the b loop runs outermost with PM+1 running sums.  The per-b
+// block reduction goes through LDS in [value][thread] order (conflict-free,
+// two levels) instead of 6-step cross-lane shuffles per value.
 // ---------------------------------------------------------------------------
-template <int PM, int KIND, bool CUBE, bool KA>
+// Column-side operands (x_c, z_c, weight rows) are wave-uniform: they are
+// read through the constant address space so they land in SGPRs via scalar
+// loads instead of 64-lane vector loads of one address.
+typedef const __attribute__((address_space(4))) double *cdp;
+
+// Matern32: the gradient-indexed weights of slice b are the kernel weights of
+// slice b+1 (wg[b] == wk[b+1] bit for bit, both exp(-theta[2+B+b+B i]) --
+// SURVEY Q1), so r~2_b = r2_{b+1}.  The b loop runs downwards and keeps
+// r2_{b+1} per pair in registers: one weighted dot product per (pair, b)
+// instead of two; only the last slice uses its own wg row.
+template <int PM, int KIND, bool CUBE>
 __global__ __launch_bounds__(256) void k_grad(PairSide S, int B, int ZS, TabView tab,
                                               const double *__restrict__ A, int64_t ld,
                                               double sA, const double *__restrict__ alpha,
                                               const double *__restrict__ cube,
                                               double *__restrict__ gpart,
-                                              double *__restrict__ trpart,
-                                              double *__restrict__ kapart, int64_t npad,
-                                              int64_t ntiles) {
-  __shared__ double red[4][PM + 2];
-  __shared__ double rowacc[4][AT];
-  __shared__ double colacc[AT];
+                                              double *__restrict__ trpart, int64_t ntiles) {
+  constexpr int NV = PM + 1;
+  constexpr int NM = AT / 4;
+  __shared__ double red[NV][64];
+  __shared__ double red2[NV][4];
+  __shared__ double sT[NM][256];                        // T of each lane's pairs
+  __shared__ double sR[(KIND == 1 && !CUBE) ? NM : 1][256];  // r2_{b+1} per pair
   const int64_t t = blockIdx.x;
-  // decode lower-triangle tile index t -> (I, J), I >= J
   int64_t I = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
   while ((I + 1) * (I + 2) / 2 <= t) ++I;
   while (I * (I + 1) / 2 > t) --I;
   const int64_t J = t - I * (I + 1) / 2;
 
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t n = S.n;
   const int64_t r = I * AT + lane;
   const bool rvalid = r < n;
   const int64_t rr = rvalid ? r : 0;
+  const int64_t c0 = J * AT + wv;  // columns c0 + 4m (rows of X exist up to a multiple of 64)
+  cdp Xc = (cdp)S.X;
+  cdp Zc = (cdp)S.Z;
+  cdp LZc = (cdp)S.LZ;
+  cdp WK = (cdp)tab.wk;
+  cdp WG = (cdp)tab.wg;
+  cdp LAM = (cdp)tab.lam;
 
   double xr[PM];
 #pragma unroll
-  for (int i = 0; i < PM; ++i) xr[i] = rvalid ? S.X[rr * PM + i] : 0.0;
+  for (int i = 0; i < PM; ++i) xr[i] = S.X[rr * PM + i];
   const double ar = rvalid ? alpha[rr] : 0.0;
 
-  double T[AT / 4];
-  double kf[AT / 4];
   unsigned valid = 0;
   double tr = 0.0;
 #pragma unroll
-  for (int m = 0; m < AT / 4; ++m) {
-    const int64_t c = J * AT + wv + 4 * m;
+  for (int m = 0; m < NM; ++m) {
+    const int64_t c = c0 + 4 * m;
     const bool v = rvalid && c < n && !(I == J && c > r);
     double tv = 0.0;
     if (v) {
@@ -180,116 +202,166 @@ __global__ __launch_bounds__(256) void k_grad(PairSide S, int B, int ZS, TabView
       else tv *= 2.0;
       valid |= 1u << m;
     }
-    T[m] = tv;
-    kf[m] = 0.0;
+    sT[m][tid] = tv;  // each lane only ever reads its own column of sT / sR
   }
 
-  for (int b = 0; b < B; ++b) {
+  for (int b = B - 1; b >= 0; --b) {
     double g[PM];
 #pragma unroll
     for (int i = 0; i < PM; ++i) g[i] = 0.0;
     double gl = 0.0;
-    const double *wk = tab.wk + b * PM;
-    const double *wg = tab.wg + b * PM;
-    const double lam = tab.lam[b];
+    cdp wk = WK + b * PM;
+    cdp wg = WG + b * PM;
+    const double lam = LAM[b];
+    const bool last = (b == B - 1);
     double zr = 0.0, lzr = 0.0;
     if (b > 0) {
-      zr = rvalid ? S.Z[rr * ZS + b - 1] : 0.0;
-      if (KIND == 0) lzr = rvalid ? S.LZ[rr * ZS + b - 1] : 0.0;
+      zr = S.Z[rr * ZS + b - 1];
+      if (KIND == 0) lzr = S.LZ[rr * ZS + b - 1];
     }
-#pragma unroll 2
-    for (int m = 0; m < AT / 4; ++m) {
-      const int64_t c = J * AT + wv + 4 * m;
-      if (c >= n) break;
+#pragma unroll 1
+    for (int m = 0; m < NM; ++m) {
+      const int64_t c = c0 + 4 * m;
       double d2[PM];
 #pragma unroll
       for (int i = 0; i < PM; ++i) {
-        const double d = xr[i] - S.X[c * PM + i];
+        const double d = xr[i] - Xc[c * PM + i];
         d2[i] = d * d;
       }
-      double kb;
+      double kb, rt2 = 0.0;
       if (CUBE) {
         kb = ((valid >> m) & 1u) ? cube[r + c * n + (int64_t)b * n * n] : 0.0;
+        if (KIND == 1) {
+#pragma unroll
+          for (int i = 0; i < PM; ++i) rt2 = fma(d2[i], wg[i], rt2);
+        }
       } else {
         double r2 = 0.0;
 #pragma unroll
         for (int i = 0; i < PM; ++i) r2 = fma(d2[i], wk[i], r2);
         double zc = 0.0, lzc = 0.0;
         if (b > 0) {
-          zc = S.Z[c * ZS + b - 1];
-          if (KIND == 0) lzc = S.LZ[c * ZS + b - 1];
+          zc = Zc[c * ZS + b - 1];
+          if (KIND == 0) lzc = LZc[c * ZS + b - 1];
         }
         kb = (r < c) ? kval<KIND, false>(b, r2, lam, zr, zc, lzr, lzc)
                      : kval<KIND, false>(b, r2, lam, zc, zr, lzc, lzr);
+        if (KIND == 1) {
+          if (last) {
+#pragma unroll
+            for (int i = 0; i < PM; ++i) rt2 = fma(d2[i], wg[i], rt2);
+          } else {
+            rt2 = sR[m][tid];
+          }
+          sR[m][tid] = r2;
+        }
       }
-      if (KA) kf[m] += kb;
-      const double tm = T[m];
+      const double tm = sT[m][tid];
       gl = fma(tm, kb, gl);
       double U;
-      if (KIND == 0) {
-        U = tm * kb;
-      } else {
-        double rt2 = 0.0;
-#pragma unroll
-        for (int i = 0; i < PM; ++i) rt2 = fma(d2[i], wg[i], rt2);
-        U = tm * (kb / (1.0 + sqrt(3.0 * rt2)));
-      }
+      if (KIND == 0) U = tm * kb;
+      else U = tm * (kb / (1.0 + sqrt(3.0 * rt2)));
 #pragma unroll
       for (int i = 0; i < PM; ++i) g[i] = fma(U, d2[i], g[i]);
     }
-    // block reduction of the PM + 1 partial sums for this b
+    // block reduction: two xor-shuffle steps fold each wave to 16 lanes, the
+    // 64 survivors go to LDS in [value][slot] order, 4 x 16 -> 4 -> 1
 #pragma unroll
     for (int i = 0; i < PM; ++i) {
-      const double s = wave_sum(g[i]);
-      if (lane == 0) red[wv][i] = s;
+      double v = g[i];
+      v += __shfl_xor(v, 32, 64);
+      v += __shfl_xor(v, 16, 64);
+      if (lane < 16) red[i][wv * 16 + lane] = v;
     }
     {
-      const double s = wave_sum(gl);
-      if (lane == 0) red[wv][PM] = s;
+      double v = gl;
+      v += __shfl_xor(v, 32, 64);
+      v += __shfl_xor(v, 16, 64);
+      if (lane < 16) red[PM][wv * 16 + lane] = v;
     }
     __syncthreads();
-    if (threadIdx.x < PM + 1) {
-      const int i = threadIdx.x;
-      const double s = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
-      gpart[((int64_t)b * (PM + 1) + i) * ntiles + t] = s;
-    }
-    __syncthreads();
-  }
-
-  // trace of T
-  {
-    const double s = wave_sum(tr);
-    if (lane == 0) red[wv][PM + 1] = s;
-    __syncthreads();
-    if (threadIdx.x == 0)
-      trpart[t] = (red[0][PM + 1] + red[1][PM + 1]) + (red[2][PM + 1] + red[3][PM + 1]);
-  }
-
-  if (KA) {
-    // rows of Kfull * alpha: pair (r,c), r >= c, gives K a_c to row r and,
-    // if r != c, K a_r to row c.  Slot [J][r] for rows of I, [I][c] for J.
-    double rowp = 0.0;
+    if (tid < NV * 4) {
+      const int i = tid % NV, sg = tid / NV;
+      double s = 0.0;
 #pragma unroll
-    for (int m = 0; m < AT / 4; ++m) {
-      const int64_t c = J * AT + wv + 4 * m;
-      const bool v = (valid >> m) & 1u;
-      if (v) rowp = fma(kf[m], alpha[c], rowp);
-      const double cp = wave_sum((v && c != r) ? kf[m] * ar : 0.0);
-      if (lane == 0) colacc[wv + 4 * m] = cp;
+      for (int k = 0; k < 16; ++k) s += red[i][16 * sg + k];
+      red2[i][sg] = s;
     }
-    rowacc[wv][lane] = rowp;
     __syncthreads();
-    if (threadIdx.x < AT) {
-      const int x = threadIdx.x;
-      const double Rs = (rowacc[0][x] + rowacc[1][x]) + (rowacc[2][x] + rowacc[3][x]);
-      if (I == J) {
-        kapart[I * npad + I * AT + x] = Rs + colacc[x];
-      } else {
-        kapart[J * npad + I * AT + x] = Rs;
-        kapart[I * npad + J * AT + x] = colacc[x];
-      }
+    if (tid < NV) {
+      const double s = (red2[tid][0] + red2[tid][1]) + (red2[tid][2] + red2[tid][3]);
+      gpart[((int64_t)b * NV + tid) * ntiles + t] = s;
     }
   }
+  // trace of T (diagonal pairs)
+  {
+    double v = tr;
+    v += __shfl_xor(v, 32, 64);
+    v += __shfl_xor(v, 16, 64);
+    if (lane < 16) red[0][wv * 16 + lane] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double s = 0.0;
+    for (int k = 0; k < 64; ++k) s += red[0][k];
+    trpart[t] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kfull * alpha from the lower copy written by the assembly (RMSE,
+// src/kernel_SE_cpp.cpp:238): per 64x64 lower tile, row sums (K a_J) go to
+// slot [J][rows of I] and column sums (K^T a_I) to slot [I][rows of J]; a
+// diagonal tile is symmetrised in LDS and gives only row sums.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_symv_tiles(const double *__restrict__ K, int64_t ld,
+                                                    int64_t n, const double *__restrict__ alpha,
+                                                    double *__restrict__ kapart, int64_t npad) {
+  __shared__ double t[AT][AT + 1];
+  __shared__ double part[4][AT];
+  const int64_t J = blockIdx.x, I = blockIdx.y;
+  if (J > I) return;
+  const int tid = threadIdx.x, x = tid & 63, q = tid >> 6;
+  for (int e = tid; e < AT * AT; e += 256) {
+    const int a = e & 63, c = e >> 6;
+    const int64_t r = I * AT + a, cc = J * AT + c;
+    double v = 0.0;
+    if (r < n && cc < n) v = (I == J && cc > r) ? K[cc + r * ld] : K[r + cc * ld];
+    t[a][c] = v;
+  }
+  __syncthreads();
+  // row sums: thread (x, q) sums columns q, q+4, ...
+  double s = 0.0;
+  for (int c = q; c < AT; c += 4) {
+    const int64_t cc = J * AT + c;
+    s = fma(t[x][c], cc < n ? alpha[cc] : 0.0, s);
+  }
+  part[q][x] = s;
+  __syncthreads();
+  if (tid < AT) {
+    const double rs = (part[0][x] + part[1][x]) + (part[2][x] + part[3][x]);
+    kapart[J * npad + I * AT + x] = rs;
+  }
+  if (I == J) return;
+  __syncthreads();
+  double s2 = 0.0;
+  for (int a = q; a < AT; a += 4) {
+    const int64_t r = I * AT + a;
+    s2 = fma(t[a][x], r < n ? alpha[r] : 0.0, s2);
+  }
+  part[q][x] = s2;
+  __syncthreads();
+  if (tid < AT) {
+    const double cs = (part[0][x] + part[1][x]) + (part[2][x] + part[3][x]);
+    kapart[I * npad + J * AT + x] = cs;
+  }
+}
+
+hipError_t launch_symv_tiles(const double *K, int64_t ld, int64_t n, const double *alpha,
+                             double *kapart, int64_t npad, hipStream_t st) {
+  const unsigned nt = (unsigned)((n + AT - 1) / AT);
+  hipLaunchKernelGGL(k_symv_tiles, dim3(nt, nt), dim3(256), 0, st, K, ld, n, alpha, kapart, npad);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -354,23 +426,19 @@ hipError_t launch_assembly(int mode, int kind, int PM, PairSide R, PairSide C, i
 template <int PM>
 static hipError_t grad_pm(int kind, PairSide S, int B, int ZS, TabView tab, const double *A,
                           int64_t ld, double sA, const double *alpha, const double *cube,
-                          double *gpart, double *trpart, double *kapart, int64_t npad,
-                          hipStream_t st) {
-  const int64_t nt = grad_ntiles(S.n);
-  dim3 grid((unsigned)nt), blk(256);
-#define ACE_G(K, CB, KA)                                                                   \
-  hipLaunchKernelGGL((k_grad<PM, K, CB, KA>), grid, blk, 0, st, S, B, ZS, tab, A, ld, sA, \
-                     alpha, cube, gpart, trpart, kapart, npad, nt)
-  const bool cb = cube != nullptr, ka = kapart != nullptr;
-  if (cb && ka) return hipErrorInvalidValue;
+                          double *gpart, double *trpart, hipStream_t st) {
+  const int64_t nsuper = grad_ntiles(S.n);
+  dim3 grid((unsigned)nsuper), blk(256);
+#define ACE_G(K, CB)                                                                          \
+  hipLaunchKernelGGL((k_grad<PM, K, CB>), grid, blk, 0, st, S, B, ZS, tab, A, ld, sA, alpha, \
+                     cube, gpart, trpart, nsuper)
+  const bool cb = cube != nullptr;
   if (kind == 0) {
-    if (cb) ACE_G(0, true, false);
-    else if (ka) ACE_G(0, false, true);
-    else ACE_G(0, false, false);
+    if (cb) ACE_G(0, true);
+    else ACE_G(0, false);
   } else {
-    if (cb) ACE_G(1, true, false);
-    else if (ka) ACE_G(1, false, true);
-    else ACE_G(1, false, false);
+    if (cb) ACE_G(1, true);
+    else ACE_G(1, false);
   }
 #undef ACE_G
   return hipGetLastError();
@@ -378,11 +446,10 @@ static hipError_t grad_pm(int kind, PairSide S, int B, int ZS, TabView tab, cons
 
 hipError_t launch_grad(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                        const double *A, int64_t ld, double sA, const double *alpha,
-                       const double *cube, double *gpart, double *trpart, double *kapart,
-                       int64_t npad, hipStream_t st) {
+                       const double *cube, double *gpart, double *trpart, hipStream_t st) {
   switch (PM) {
 #define ACE_CASE(P) \
-  case P: return grad_pm<P>(kind, S, B, ZS, tab, A, ld, sA, alpha, cube, gpart, trpart, kapart, npad, st);
+  case P: return grad_pm<P>(kind, S, B, ZS, tab, A, ld, sA, alpha, cube, gpart, trpart, st);
     ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
     ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
 #undef ACE_CASE

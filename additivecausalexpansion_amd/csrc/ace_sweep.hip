@@ -31,7 +31,8 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // ---------------------------------------------------------------- gather
 __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, int64_t ld,
                                                 int64_t k0, double *__restrict__ P,
-                                                double *__restrict__ W, int64_t ldp) {
+                                                double *__restrict__ W, int64_t ldp,
+                                                double *__restrict__ S0) {
   __shared__ double tile[64][65];
   const int64_t i0 = (int64_t)blockIdx.x * 64;
   const int j0 = blockIdx.y * 64;
@@ -67,6 +68,12 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
       W[i + (int64_t)(j0 + b) * ldp] = v;
     }
   }
+  if (i0 == k0) {  // pivot rows of sub-block 0: snapshot for k_pivot / k_panel
+    for (int e = tid; e < 4096; e += 256) {
+      const int a = e & 63, b = e >> 6;
+      S0[a + (int64_t)(j0 + b) * SUB] = W[(i0 + a) + (int64_t)(j0 + b) * ldp];
+    }
+  }
 }
 
 // ---------------------------------------------------------------- pivot
@@ -76,35 +83,21 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
 // a = D_it = D_ti).  Layout: lane = row i, wave w keeps columns 16w..16w+15
 // in registers; per pivot the owning wave publishes column t and lane t of
 // every wave publishes its part of row t through double-buffered LDS
-// vectors, so there is one barrier per pivot.  Also snapshots the 64 pivot
-// rows (all NB columns, row-major) into S before the panel kernel
-// overwrites them, and records every pivot d (Cholesky diagonal squared).
-__global__ __launch_bounds__(256) void k_pivot(const double *__restrict__ W, int64_t ldp,
-                                               int64_t k0, int s, double *__restrict__ SW,
-                                               double *__restrict__ S, double *__restrict__ piv,
-                                               int *__restrict__ flag) {
-  __shared__ double tileT[64][65];
-  __shared__ double colb[2][SUB];
-  __shared__ double rowb[2][SUB];
-  const int64_t p0 = k0 + (int64_t)s * SUB;
+// vectors, so there is one barrier per pivot.  D_s is read from the pivot-row
+// snapshot S (written by k_gather / the previous k_panel); every pivot d
+// (Cholesky diagonal squared) is recorded.
+__global__ __launch_bounds__(256) void k_pivot(const double *__restrict__ S, int s,
+                                               double *__restrict__ SW, double *__restrict__ piv,
+                                               int64_t p0, int *__restrict__ flag) {
+  __shared__ __attribute__((aligned(16))) double colb[2][SUB];
+  __shared__ __attribute__((aligned(16))) double rowb[2][SUB];
+  __shared__ double pv[SUB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // S[a*NB + j] = W[p0 + a, j]  (transposed through LDS, coalesced both ways)
-  for (int cb = 0; cb < NB / 64; ++cb) {
-    for (int e = tid; e < 4096; e += 256) {
-      const int a = e & 63, b = e >> 6;
-      tileT[a][b] = W[(p0 + a) + (int64_t)(64 * cb + b) * ldp];
-    }
-    __syncthreads();
-    for (int e = tid; e < 4096; e += 256) {
-      const int b = e & 63, a = e >> 6;
-      S[a * NB + 64 * cb + b] = tileT[a][b];
-    }
-    __syncthreads();
-  }
   double v[16];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) v[q] = W[(p0 + lane) + (int64_t)(s * SUB + 16 * w + q) * ldp];
-  bool bad = false;
+  for (int q = 0; q < 16; ++q) v[q] = S[lane + (s * SUB + 16 * w + q) * SUB];
+  // no global memory traffic inside the loop: every __syncthreads() is then
+  // a bare s_barrier (a pending global store would add a vmcnt(0) wait)
   for (int tw = 0; tw < 4; ++tw) {
 #pragma unroll
     for (int tq = 0; tq < 16; ++tq) {
@@ -113,29 +106,39 @@ __global__ __launch_bounds__(256) void k_pivot(const double *__restrict__ W, int
       if (w == tw) colb[buf][lane] = v[tq];
       if (lane == t) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) rowb[buf][16 * w + q] = v[q];
+        for (int q = 0; q < 16; q += 2)
+          *reinterpret_cast<double2 *>(&rowb[buf][16 * w + q]) = double2{v[q], v[q + 1]};
       }
       __syncthreads();
       const double d = rowb[buf][t];
       const double rd = 1.0 / d;
       const double dit = colb[buf][lane];
+      double rt[16];
+#pragma unroll
+      for (int q = 0; q < 16; q += 2) {
+        const double2 x = *reinterpret_cast<const double2 *>(&rowb[buf][16 * w + q]);
+        rt[q] = x.x;
+        rt[q + 1] = x.y;
+      }
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int j = 16 * w + q;
-        const double dtj = rowb[buf][j];
+        const double dtj = rt[q];
         double x;
         if (lane == t) x = (j == t) ? -rd : dtj * rd;
         else if (j == t) x = dit * rd;
         else x = fma(-(dit * dtj), rd, v[q]);
         v[q] = x;
       }
-      if (tid == 0) {
-        piv[p0 + t] = d;
-        bad |= !(d > 0.0) || !isfinite(d);
-      }
+      if (tid == 0) pv[t] = d;
     }
   }
-  if (tid == 0 && bad) *flag = 1;
+  __syncthreads();
+  if (tid < SUB) {
+    const double d = pv[tid];
+    piv[p0 + tid] = d;
+    if (!(d > 0.0) || !isfinite(d)) *flag = 1;
+  }
 #pragma unroll
   for (int q = 0; q < 16; ++q) SW[lane + (16 * w + q) * SUB] = v[q];
 }
@@ -148,15 +151,18 @@ __global__ __launch_bounds__(256) void k_pivot(const double *__restrict__ W, int
 // Wave w owns rows 16w..16w+15.  Phase 1 forms Vn^T = -V^T = SW W_is^T
 // (SW is symmetric) so that its accumulator fragments are directly the B
 // operands of phase 2's D = S_chunk^T Vn^T + W_chunk^T (no LDS round trip).
-constexpr int PLD = 80;  // LDS pitch: 64 + 16 doubles, conflict-free fragment reads
+constexpr int PLD = 80;  // LDS pitch for sSW: 64 + 16 doubles, conflict-free fragment reads
+constexpr int SLD = 66;  // LDS pitch for the transposed S chunk (c-major)
 
 __global__ __launch_bounds__(256) void k_panel(double *__restrict__ W, int64_t ldp, int64_t k0,
                                                int s, const double *__restrict__ SW,
-                                               const double *__restrict__ S) {
+                                               const double *__restrict__ S,
+                                               double *__restrict__ Snext, int64_t row0) {
   __shared__ double sSW[SUB][PLD];  // sSW[b][a] = SW(a, b)
-  __shared__ double sS[SUB][PLD];   // sS[t][c]  = S(t, 64 cc + c)
-  const int64_t i0 = (int64_t)blockIdx.x * SUB;
+  __shared__ double sSt[SUB][SLD];  // sSt[c][t] = S(t, 64 cc + c)
+  const int64_t i0 = row0 + (int64_t)blockIdx.x * SUB;
   const bool pivrows = (i0 == k0 + (int64_t)s * SUB);
+  const bool nextrows = (s + 1 < NB / SUB) && (i0 == k0 + (int64_t)(s + 1) * SUB);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
   for (int e = tid; e < SUB * SUB; e += 256) {
@@ -165,6 +171,7 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ W, int64_t l
   }
   __syncthreads();
   const int64_t row = i0 + 16 * w + lr;
+  const int srow = 16 * w + lr;  // row within the block (for Snext)
   d4 acc1[4];
   if (pivrows) {
 #pragma unroll
@@ -174,12 +181,14 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ W, int64_t l
   } else {
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) acc1[ct] = d4{0.0, 0.0, 0.0, 0.0};
+    double bw[SUB / 4];  // all 16 B fragments in flight at once
+#pragma unroll
+    for (int kk = 0; kk < SUB / 4; ++kk) bw[kk] = W[row + (int64_t)(s * SUB + 4 * kk + lk) * ldp];
 #pragma unroll
     for (int kk = 0; kk < SUB / 4; ++kk) {
-      const double b = W[row + (int64_t)(s * SUB + 4 * kk + lk) * ldp];
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct)
-        acc1[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(sSW[4 * kk + lk][16 * ct + lr], b,
+        acc1[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(sSW[4 * kk + lk][16 * ct + lr], bw[kk],
                                                         acc1[ct], 0, 0, 0);
     }
   }
@@ -187,51 +196,139 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ W, int64_t l
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      W[row + (int64_t)(s * SUB + 16 * ct + lk + 4 * j) * ldp] = -acc1[ct][j];
+    for (int j = 0; j < 4; ++j) {
+      const int col = s * SUB + 16 * ct + lk + 4 * j;
+      W[row + (int64_t)col * ldp] = -acc1[ct][j];
+      if (nextrows) Snext[srow + col * SUB] = -acc1[ct][j];
+    }
   for (int cc = 0; cc < NB / SUB; ++cc) {
     if (cc == s) continue;
+    // issue this chunk's accumulator loads before the staging barrier
+    d4 accs[4];
+#pragma unroll
+    for (int ctc = 0; ctc < 4; ++ctc)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        accs[ctc][j] = pivrows ? 0.0 : W[row + (int64_t)(cc * SUB + 16 * ctc + lk + 4 * j) * ldp];
     __syncthreads();
     for (int e = tid; e < SUB * SUB; e += 256) {
-      const int c = e & 63, t = e >> 6;
-      sS[t][c] = S[t * NB + cc * SUB + c];
+      const int t = e & 63, c = e >> 6;
+      sSt[c][t] = S[t + (cc * SUB + c) * SUB];
     }
     __syncthreads();
 #pragma unroll
     for (int ctc = 0; ctc < 4; ++ctc) {
-      d4 acc;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[j] = pivrows ? 0.0 : W[row + (int64_t)(cc * SUB + 16 * ctc + lk + 4 * j) * ldp];
+      d4 acc = accs[ctc];
 #pragma unroll
       for (int kk = 0; kk < SUB / 4; ++kk)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sS[4 * kk + lk][16 * ctc + lr],
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sSt[16 * ctc + lr][4 * kk + lk],
                                                    acc1[kk >> 2][kk & 3], acc, 0, 0, 0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        W[row + (int64_t)(cc * SUB + 16 * ctc + lk + 4 * j) * ldp] = acc[j];
+      for (int j = 0; j < 4; ++j) {
+        const int col = cc * SUB + 16 * ctc + lk + 4 * j;
+        W[row + (int64_t)col * ldp] = acc[j];
+        if (nextrows) Snext[srow + col * SUB] = acc[j];
+      }
     }
   }
 }
 
+// ---------------------------------------------------------------- panel GEMM
+// After the four sub-sweeps restricted to the pivot rows, W[k0:k0+NB, :]
+// holds W_kk = -D^-1 (symmetric).  Every other row of the panel is then one
+// GEMM:  W_i = A_ik D^-1 = Pn_i W_kk  (Pn = -P).  Computed transposed,
+// Out^T[c][i] = sum_k W_kk[c][k] Pn[i][k], so that fragment lanes walk
+// consecutive rows of W.  64 rows x NB columns per 512-thread workgroup,
+// 8 waves = 4 row strips x 2 column halves, 8 MFMA fragments each.
+constexpr int GBKP = 8;            // k per LDS stage
+constexpr int GLB = NB + 16;       // pitch of the W_kk stage  [k][c]
+constexpr int GLA = SUB + 16;      // pitch of the Pn stage    [k][i]
+
+__global__ __launch_bounds__(512) void k_panel_gemm(double *__restrict__ W,
+                                                    const double *__restrict__ Pn, int64_t ldp,
+                                                    int64_t k0) {
+  __shared__ __attribute__((aligned(16))) double sB[2][GBKP][GLB];
+  __shared__ __attribute__((aligned(16))) double sA[2][GBKP][GLA];
+  const int64_t i0 = (int64_t)blockIdx.x * SUB;
+  if (i0 >= k0 && i0 < k0 + NB) return;  // pivot rows are already final
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wi = wv & 3, wc = wv >> 2;
+  const int lr = lane & 15, lk = lane >> 4;
+  constexpr int CT = NB / 2 / 16;  // c-tiles per wave
+  d4 acc[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) acc[ct] = d4{0.0, 0.0, 0.0, 0.0};
+  // staging maps: B: 8 k x NB c  (NB/128 double2 per thread); A: 8 k x 64 i (1 per thread)
+  const int bk = tid >> 6, bc = (tid & 63) * (NB / 64);
+  const int ak = tid >> 6, ai = tid & 63;
+  constexpr int NBQ = NB / 128;  // double2 per thread for the B stage
+  double2 rb[NBQ];
+  double ra;
+  auto load = [&](int kc) {
+#pragma unroll
+    for (int e = 0; e < NBQ; ++e)
+      rb[e] = *reinterpret_cast<const double2 *>(W + (k0 + bc + 2 * e) + (int64_t)(kc + bk) * ldp);
+    ra = Pn[(i0 + ai) + (int64_t)(kc + ak) * ldp];
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < NBQ; ++e) *reinterpret_cast<double2 *>(&sB[buf][bk][bc + 2 * e]) = rb[e];
+    sA[buf][ak][ai] = ra;
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  constexpr int NCHP = NB / GBKP;
+  for (int ch = 0; ch < NCHP; ++ch) {
+    const int cur = ch & 1;
+    if (ch + 1 < NCHP) load((ch + 1) * GBKP);
+#pragma unroll
+    for (int kk = 0; kk < GBKP / 4; ++kk) {
+      const double b = sA[cur][4 * kk + lk][16 * wi + lr];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+        acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+            sB[cur][4 * kk + lk][(NB / 2) * wc + 16 * ct + lr], b, acc[ct], 0, 0, 0);
+    }
+    if (ch + 1 < NCHP) store(cur ^ 1);
+    __syncthreads();
+  }
+  const int64_t row = i0 + 16 * wi + lr;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      W[row + (int64_t)((NB / 2) * wc + 16 * ct + lk + 4 * j) * ldp] = acc[ct][j];
+}
+
 // ---------------------------------------------------------------- update
-// One 128x128 lower tile (I, J) of A.  Tiles outside block k:
-//   A_IJ += Pn_J-rows x W_I-rows^T over the NB panel columns  (Pn = -P)
-// computed as D = Pn W^T + C with the MFMA's D[row=c][col=r] so that the
-// 16 lanes of a fragment walk consecutive rows of the column-major A.
-// Tiles of block k receive the swept panel W (transposed for the row block).
-constexpr int BK = 16;      // panel columns staged per LDS buffer
+// One 128x128 lower tile (I, J) of A per 512-thread workgroup.  Tiles
+// outside block k:  A_IJ += Pn_J-rows x W_I-rows^T over the NB panel
+// columns (Pn = -P), computed as D = Pn W^T + C with the MFMA's
+// D[row=c][col=r] so that the 16 lanes of a fragment walk consecutive rows
+// of the column-major A.  8 waves, each a 64(r) x 32(c) block of 4x2
+// v_mfma_f64_16x16x4_f64 fragments: 32 accumulator doubles per lane, so
+// 4 waves fit per SIMD (61 TF/s vs 46 TF/s for 4 waves of 64x64 -- the
+// latency of the LDS fragment reads is hidden by the other waves,
+// tools/bench_update.hip).  Tiles of block k receive the swept panel W
+// (transposed for the row block).
+#ifndef ACE_BK
+#define ACE_BK 16
+#endif
+constexpr int BK = ACE_BK;  // panel columns staged per LDS buffer
 constexpr int LDL = 144;    // LDS row pitch (doubles): 128 + 16, bank-conflict free
 constexpr int NCH = NB / BK;
+constexpr int UTHREADS = 512;
+static_assert(BK == 16, "staging maps 512 threads x 4 doubles onto a 128 x 16 chunk");
 
 // LOOK = true : only the "cross" tiles of block kx (tiles with I or J in
 //               block kx) -- the lookahead that the next step's panel needs;
 // LOOK = false: every lower tile except the cross of block kx (kx < 0: all).
 template <bool LOOK>
-__global__ __launch_bounds__(256, 2) void k_update(double *__restrict__ A, int64_t ld,
-                                                   const double *__restrict__ W,
-                                                   const double *__restrict__ Pn, int64_t ldp,
-                                                   int64_t k0, int kx) {
+__global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, int64_t ld,
+                                                        const double *__restrict__ W,
+                                                        const double *__restrict__ Pn,
+                                                        int64_t ldp, int64_t k0, int kx) {
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
   constexpr int KT = NB / UT;
@@ -256,7 +353,7 @@ __global__ __launch_bounds__(256, 2) void k_update(double *__restrict__ A, int64
     if (kx >= 0 && ((I >= kx * KT && I < (kx + 1) * KT) || (J >= kx * KT && J < (kx + 1) * KT)))
       return;
   }
-  const int kt0 = (int)(k0 / UT), kt1 = kt0 + NB / UT;
+  const int kt0 = (int)(k0 / UT), kt1 = kt0 + KT;
   const bool Ik = I >= kt0 && I < kt1, Jk = J >= kt0 && J < kt1;
   const int64_t R0 = (int64_t)I * UT, C0 = (int64_t)J * UT;
   const int tid = threadIdx.x;
@@ -268,19 +365,19 @@ __global__ __launch_bounds__(256, 2) void k_update(double *__restrict__ A, int64
       for (int sa = 0; sa < 2; ++sa)
         for (int sb = 0; sb < 2; ++sb) {
           __syncthreads();
-          for (int e = tid; e < 4096; e += 256) {
+          for (int e = tid; e < 4096; e += UTHREADS) {
             const int c = e & 63, a = e >> 6;
             tileT[a * 65 + c] = W[(C0 + 64 * sb + c) + (R0 - k0 + 64 * sa + a) * ldp];
           }
           __syncthreads();
-          for (int e = tid; e < 4096; e += 256) {
+          for (int e = tid; e < 4096; e += UTHREADS) {
             const int a = e & 63, c = e >> 6;
             A[(R0 + 64 * sa + a) + (C0 + 64 * sb + c) * ld] = tileT[a * 65 + c];
           }
         }
     } else {
       // column block k (and the diagonal block): A[r, k0+j] = W[r, j]
-      for (int e = tid; e < UT * UT; e += 256) {
+      for (int e = tid; e < UT * UT; e += UTHREADS) {
         const int a = e & (UT - 1), c = e >> 7;
         A[(R0 + a) + (C0 + c) * ld] = W[(R0 + a) + (C0 - k0 + c) * ldp];
       }
@@ -289,74 +386,72 @@ __global__ __launch_bounds__(256, 2) void k_update(double *__restrict__ A, int64
   }
 
   const int lane = tid & 63, wv = tid >> 6;
-  const int wr = wv & 1, wc = wv >> 1;
+  const int wr = wv & 1, wc = wv >> 1;  // rows 64*wr.., cols 32*wc..
   const int lr = lane & 15, lk = lane >> 4;
-  d4 acc[4][4];
+  d4 acc[2][4];
 #pragma unroll
-  for (int ci = 0; ci < 4; ++ci)
+  for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
     for (int ri = 0; ri < 4; ++ri) {
       const int64_t r = R0 + 64 * wr + 16 * ri + lr;
-      const int64_t c = C0 + 64 * wc + 16 * ci + lk;
+      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[ci][ri][j] = A[r + (c + 4 * j) * ld];
     }
-
-  const int sk = tid >> 4, sm = (tid & 15) * 8;
+  // staging: each thread moves 4 doubles of W and 4 of Pn per chunk
+  const int sk = tid >> 5, sm = (tid & 31) * 4;
   const double *gW = W + (R0 + sm) + (int64_t)sk * ldp;
   const double *gP = Pn + (C0 + sm) + (int64_t)sk * ldp;
-  double2 rw[4], rp[4];
+  double2 rw[2], rp[2];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < 2; ++e) {
     rw[e] = *reinterpret_cast<const double2 *>(gW + 2 * e);
     rp[e] = *reinterpret_cast<const double2 *>(gP + 2 * e);
   }
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < 2; ++e) {
     *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2 * e]) = rw[e];
     *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2 * e]) = rp[e];
   }
   __syncthreads();
-
   for (int ch = 0; ch < NCH; ++ch) {
     const int cur = ch & 1;
     if (ch + 1 < NCH) {
       const int64_t off = (int64_t)(ch + 1) * BK * ldp;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < 2; ++e) {
         rw[e] = *reinterpret_cast<const double2 *>(gW + off + 2 * e);
         rp[e] = *reinterpret_cast<const double2 *>(gP + off + 2 * e);
       }
     }
 #pragma unroll
     for (int kk = 0; kk < BK / 4; ++kk) {
-      double a[4], b[4];
+      double a[2], b[4];
 #pragma unroll
-      for (int ci = 0; ci < 4; ++ci) a[ci] = sP[cur][4 * kk + lk][64 * wc + 16 * ci + lr];
+      for (int ci = 0; ci < 2; ++ci) a[ci] = sP[cur][4 * kk + lk][32 * wc + 16 * ci + lr];
 #pragma unroll
       for (int ri = 0; ri < 4; ++ri) b[ri] = sW[cur][4 * kk + lk][64 * wr + 16 * ri + lr];
 #pragma unroll
-      for (int ci = 0; ci < 4; ++ci)
+      for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
         for (int ri = 0; ri < 4; ++ri)
           acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
     }
     if (ch + 1 < NCH) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < 2; ++e) {
         *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2 * e]) = rw[e];
         *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2 * e]) = rp[e];
       }
     }
     __syncthreads();
   }
-
 #pragma unroll
-  for (int ci = 0; ci < 4; ++ci)
+  for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
     for (int ri = 0; ri < 4; ++ri) {
       const int64_t r = R0 + 64 * wr + 16 * ri + lr;
-      const int64_t c = C0 + 64 * wc + 16 * ci + lk;
+      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
       for (int j = 0; j < 4; ++j) A[r + (c + 4 * j) * ld] = acc[ci][ri][j];
     }
@@ -365,13 +460,17 @@ __global__ __launch_bounds__(256, 2) void k_update(double *__restrict__ A, int64
 static hipError_t panel_sweep(const SweepBufs &b, int buf, int64_t k0, hipStream_t st) {
   const int64_t naug = b.ld;
   hipLaunchKernelGGL(k_gather, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st, b.A, b.ld,
-                     k0, b.P[buf], b.W[buf], b.ld);
+                     k0, b.P[buf], b.W[buf], b.ld, b.S[0]);
+  // sweep the NB x NB pivot block in place (4 workgroups per sub-step)
   for (int s = 0; s < NB / SUB; ++s) {
-    hipLaunchKernelGGL(k_pivot, dim3(1), dim3(256), 0, st, b.W[buf], b.ld, k0, s, b.SW, b.S,
-                       b.piv, b.flag);
-    hipLaunchKernelGGL(k_panel, dim3((unsigned)(naug / SUB)), dim3(256), 0, st, b.W[buf], b.ld,
-                       k0, s, b.SW, b.S);
+    hipLaunchKernelGGL(k_pivot, dim3(1), dim3(256), 0, st, b.S[s & 1], s, b.SW, b.piv,
+                       k0 + (int64_t)s * SUB, b.flag);
+    hipLaunchKernelGGL(k_panel, dim3(NB / SUB), dim3(256), 0, st, b.W[buf], b.ld, k0, s, b.SW,
+                       b.S[s & 1], b.S[(s + 1) & 1], k0);
   }
+  // every other panel row: W_i = Pn_i W_kk
+  hipLaunchKernelGGL(k_panel_gemm, dim3((unsigned)(naug / SUB)), dim3(512), 0, st, b.W[buf],
+                     b.P[buf], b.ld, k0);
   return hipGetLastError();
 }
 
@@ -422,7 +521,7 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
       if (e != hipSuccess) return e;
     }
     if (more) {
-      hipLaunchKernelGGL(k_update<true>, dim3(nT, 2 * (NB / UT)), dim3(256), 0, st, b.A, b.ld,
+      hipLaunchKernelGGL(k_update<true>, dim3(nT, 2 * (NB / UT)), dim3(UTHREADS), 0, st, b.A, b.ld,
                          b.W[buf], b.P[buf], b.ld, k0, k + 1);
       if (two) {
         e = hipEventRecord(sy->ev[2 * k + 1], st);  // cross of block k+1 updated
@@ -439,7 +538,7 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
     }
     const bool timed = tm && tm->ev && used + 2 <= tm->nev;
     if (timed) (void)hipEventRecord(tm->ev[used], st);
-    hipLaunchKernelGGL(k_update<false>, dim3(nT, nT), dim3(256), 0, st, b.A, b.ld, b.W[buf],
+    hipLaunchKernelGGL(k_update<false>, dim3(nT, nT), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[buf],
                        b.P[buf], b.ld, k0, more ? k + 1 : -1);
     if (timed) {
       (void)hipEventRecord(tm->ev[used + 1], st);
