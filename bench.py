@@ -68,6 +68,21 @@ def _allreduce_max(dist, x):
     return float(t.item())
 
 
+def pmc_traffic(kernel="k_update<false>"):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN_pmc_traffic.json, written by tools/pmc_traffic.py from two
+    separate rocprofv3 --pmc passes of this bench).  None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+        return d["kernels"][kernel]["traffic"], os.path.relpath(files[-1], ROOT)
+    except (KeyError, ValueError, OSError):
+        return None, None
+
+
 def cpu_baseline(cfg, timeout=240):
     """Rank 0 / N=1 only: the oracle leg in a subprocess (bounded)."""
     from additivecausalexpansion_amd.synthetic import CONFIGS
@@ -126,6 +141,7 @@ def main():
     model.profile(False)
 
     if rank == 0:
+        traffic, traffic_src = pmc_traffic()
         evals = a.steps * world
         value = evals / dt_max
         achieved = upd_work / (upd_ms * 1e-3) / 1e12 if upd_ms > 0 else None
@@ -156,7 +172,9 @@ def main():
                 "peak": FP64_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": traffic_src,
                 "launches": upd_n,
                 "avg_launch_ms": upd_ms / upd_n if upd_n else None,
                 "algorithmic_flops_per_launch": upd_work / upd_n if upd_n else None,

@@ -1,0 +1,61 @@
+"""Per-launch HBM traffic of the bench's dominant kernel from rocprofv3 PMC passes.
+
+Usage (on the GPU box, two separate passes -- FETCH_SIZE and WRITE_SIZE do not
+fit one pass on gfx950, MI355X_MICROARCH.md "TCC" row):
+  rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f -o run -- python3 bench.py ...
+  rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w -o run -- python3 bench.py ...
+  python tools/pmc_traffic.py gpurun_out/pmc_f gpurun_out/pmc_w > profiles/rNN_pmc_traffic.json
+
+FETCH_SIZE / WRITE_SIZE are reported in KiB per dispatch.  On gfx950 FETCH_SIZE
+counts half the bytes of wide (16 B/lane) coalesced reads, so it is doubled
+(the guide's HBM section); WRITE_SIZE is exact for 16-B stores.  The
+calibration kernel k_gather (reads one naug x 256 panel, writes two) is
+reported beside it so the correction can be checked on a known byte count.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNELS = {
+    "k_update<false>": "k_update<false>",
+    "k_update<true>": "k_update<true>",
+    "k_gather": "ace::k_gather",
+    "k_grad": "ace::k_grad",
+    "k_assembly": "ace::k_assembly",
+    "k_symv_tiles": "ace::k_symv_tiles",
+}
+
+
+def read(d, counter):
+    vals = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] != counter:
+                    continue
+                for short, key in KERNELS.items():
+                    if key in row["Kernel_Name"]:
+                        vals[short].append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    fdir, wdir = sys.argv[1], sys.argv[2]
+    fetch = read(fdir, "FETCH_SIZE")
+    write = read(wdir, "WRITE_SIZE")
+    out = {"unit": "bytes per launch", "fetch_correction": 2.0, "kernels": {}}
+    for k in KERNELS:
+        if not fetch.get(k) or not write.get(k):
+            continue
+        f = sum(fetch[k]) / len(fetch[k]) * 1024.0
+        w = sum(write[k]) / len(write[k]) * 1024.0
+        out["kernels"][k] = {"launches": len(fetch[k]), "fetch_raw": f, "fetch": 2.0 * f,
+                             "write": w, "traffic": 2.0 * f + w}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
