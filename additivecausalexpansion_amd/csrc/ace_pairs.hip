@@ -309,6 +309,231 @@ __global__ __launch_bounds__(256) void k_grad(PairSide S, int B, int ZS, TabView
 }
 
 // ---------------------------------------------------------------------------
+// Fused gradient (no cube): slices are taken two at a time so each pair's
+// d_i^2 is formed once per two slices, and for Matern32 the factor
+// 1 + sqrt(3 r~2_b) is the (1 + sqrt3 t) already formed by slice b+1's kernel
+// value (wg[b] == wk[b+1], see above), cached per pair in LDS across passes.
+// Per (pair, slice): p FMAs for r2, one sqrt + exp (+ one reciprocal for
+// Matern), p FMAs into the running sums.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double rcp_nr(double f) {
+  double q = __builtin_amdgcn_rcp(f);
+  double e = fma(-f, q, 1.0);
+  q = fma(q, e, q);
+  e = fma(-f, q, 1.0);
+  return fma(q, e, q);
+}
+
+// kernel value of slice b plus (Matern) its factor 1 + sqrt3 * sqrt(r2)
+template <int KIND>
+__device__ __forceinline__ double kval_f(int b, double r2, double lam, double zlo, double zhi,
+                                         double lzlo, double lzhi, double &f) {
+  if (KIND == 0) {
+    f = 1.0;
+    return kval<0, false>(b, r2, lam, zlo, zhi, lzlo, lzhi);
+  } else {
+    const double t = sqrt(r2);
+    f = 1.0 + SQRT3 * t;
+    const double e = f * exp(lam - SQRT3 * t);
+    if (b == 0) return e;
+    if (zlo == 0.0) return 0.0;
+    return (e * zlo) * zhi;
+  }
+}
+
+template <int PM>
+__device__ __forceinline__ void grad_block_reduce(const double (&g)[PM], double gl,
+                                                  double (*red)[64], double (*red2)[4],
+                                                  int tid, int lane, int wv,
+                                                  double *__restrict__ out, int64_t stride) {
+  constexpr int NV = PM + 1;
+#pragma unroll
+  for (int i = 0; i < PM; ++i) {
+    double v = g[i];
+    v += __shfl_xor(v, 32, 64);
+    v += __shfl_xor(v, 16, 64);
+    if (lane < 16) red[i][wv * 16 + lane] = v;
+  }
+  {
+    double v = gl;
+    v += __shfl_xor(v, 32, 64);
+    v += __shfl_xor(v, 16, 64);
+    if (lane < 16) red[PM][wv * 16 + lane] = v;
+  }
+  __syncthreads();
+  if (tid < NV * 4) {
+    const int i = tid % NV, sg = tid / NV;
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[i][16 * sg + k];
+    red2[i][sg] = s;
+  }
+  __syncthreads();
+  if (tid < NV) out[tid * stride] = (red2[tid][0] + red2[tid][1]) + (red2[tid][2] + red2[tid][3]);
+}
+
+template <int PM, int KIND>
+__global__ __launch_bounds__(256) void k_grad2(PairSide S, int B, int ZS, TabView tab,
+                                               const double *__restrict__ A, int64_t ld,
+                                               double sA, const double *__restrict__ alpha,
+                                               double *__restrict__ gpart,
+                                               double *__restrict__ trpart, int64_t ntiles) {
+  constexpr int NV = PM + 1;
+  constexpr int NM = AT / 4;
+  __shared__ double red[NV][64];
+  __shared__ double red2[NV][4];
+  __shared__ double sT[NM][256];                      // T of each lane's pairs
+  __shared__ double sF[KIND == 1 ? NM : 1][256];      // Matern: 1 + sqrt3 t of slice b+1
+  const int64_t t = blockIdx.x;
+  int64_t I = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  while (I * (I + 1) / 2 > t) --I;
+  const int64_t J = t - I * (I + 1) / 2;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t n = S.n;
+  const int64_t r = I * AT + lane;
+  const bool rvalid = r < n;
+  const int64_t rr = rvalid ? r : 0;
+  const int64_t c0 = J * AT + wv;
+  cdp Xc = (cdp)S.X;
+  cdp Zc = (cdp)S.Z;
+  cdp LZc = (cdp)S.LZ;
+  cdp WK = (cdp)tab.wk;
+  cdp WG = (cdp)tab.wg;
+  cdp LAM = (cdp)tab.lam;
+
+  double xr[PM];
+#pragma unroll
+  for (int i = 0; i < PM; ++i) xr[i] = S.X[rr * PM + i];
+  const double ar = rvalid ? alpha[rr] : 0.0;
+
+  double tr = 0.0;
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const int64_t c = c0 + 4 * m;
+    const bool v = rvalid && c < n && !(I == J && c > r);
+    double tv = 0.0;
+    if (v) {
+      tv = sA * A[r + c * ld] - ar * alpha[c];
+      if (c == r) tr += tv;
+      else tv *= 2.0;
+    }
+    sT[m][tid] = tv;  // each lane only reads back its own column of sT / sF
+  }
+
+  for (int b1 = B - 1; b1 >= 0; b1 -= 2) {
+    const int b0 = b1 - 1;  // may be -1 (odd B): second slice skipped
+    const bool two = b0 >= 0;
+    double g1[PM], g0[PM];
+#pragma unroll
+    for (int i = 0; i < PM; ++i) g1[i] = g0[i] = 0.0;
+    double gl1 = 0.0, gl0 = 0.0;
+    cdp wk1 = WK + b1 * PM;
+    cdp wk0 = WK + (two ? b0 : b1) * PM;
+    cdp wgl = WG + b1 * PM;  // used only when b1 == B-1 (its r~2 has its own row)
+    const double lam1 = LAM[b1], lam0 = LAM[two ? b0 : b1];
+    const bool last = (b1 == B - 1);
+    double zr1 = 0.0, lzr1 = 0.0, zr0 = 0.0, lzr0 = 0.0;
+    if (b1 > 0) {
+      zr1 = S.Z[rr * ZS + b1 - 1];
+      if (KIND == 0) lzr1 = S.LZ[rr * ZS + b1 - 1];
+    }
+    if (b0 > 0) {
+      zr0 = S.Z[rr * ZS + b0 - 1];
+      if (KIND == 0) lzr0 = S.LZ[rr * ZS + b0 - 1];
+    }
+#pragma unroll 1
+    for (int m = 0; m < NM; ++m) {
+      const int64_t c = c0 + 4 * m;
+      const bool rlo = r < c;
+      double d2[PM];
+#pragma unroll
+      for (int i = 0; i < PM; ++i) {
+        const double d = xr[i] - Xc[c * PM + i];
+        d2[i] = d * d;
+      }
+      const double tm = sT[m][tid];
+      // slice b1
+      double U1, f1;
+      {
+        double r2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < PM; ++i) r2 = fma(d2[i], wk1[i], r2);
+        double zc = 0.0, lzc = 0.0;
+        if (b1 > 0) {
+          zc = Zc[c * ZS + b1 - 1];
+          if (KIND == 0) lzc = LZc[c * ZS + b1 - 1];
+        }
+        const double kb = rlo ? kval_f<KIND>(b1, r2, lam1, zr1, zc, lzr1, lzc, f1)
+                              : kval_f<KIND>(b1, r2, lam1, zc, zr1, lzc, lzr1, f1);
+        gl1 = fma(tm, kb, gl1);
+        if (KIND == 0) {
+          U1 = tm * kb;
+        } else {
+          double fn;
+          if (last) {
+            double rt2 = 0.0;
+#pragma unroll
+            for (int i = 0; i < PM; ++i) rt2 = fma(d2[i], wgl[i], rt2);
+            fn = 1.0 + sqrt(3.0 * rt2);
+          } else {
+            fn = sF[m][tid];
+          }
+          U1 = (tm * kb) * rcp_nr(fn);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < PM; ++i) g1[i] = fma(U1, d2[i], g1[i]);
+      if (two) {
+        double r2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < PM; ++i) r2 = fma(d2[i], wk0[i], r2);
+        double zc = 0.0, lzc = 0.0;
+        if (b0 > 0) {
+          zc = Zc[c * ZS + b0 - 1];
+          if (KIND == 0) lzc = LZc[c * ZS + b0 - 1];
+        }
+        double f0;
+        const double kb = rlo ? kval_f<KIND>(b0, r2, lam0, zr0, zc, lzr0, lzc, f0)
+                              : kval_f<KIND>(b0, r2, lam0, zc, zr0, lzc, lzr0, f0);
+        gl0 = fma(tm, kb, gl0);
+        double U0;
+        if (KIND == 0) {
+          U0 = tm * kb;
+        } else {
+          U0 = (tm * kb) * rcp_nr(f1);
+          sF[m][tid] = f0;
+        }
+#pragma unroll
+        for (int i = 0; i < PM; ++i) g0[i] = fma(U0, d2[i], g0[i]);
+      }
+    }
+    grad_block_reduce<PM>(g1, gl1, red, red2, tid, lane, wv, gpart + (int64_t)b1 * NV * ntiles + t,
+                          ntiles);
+    if (two)
+      grad_block_reduce<PM>(g0, gl0, red, red2, tid, lane, wv,
+                            gpart + (int64_t)b0 * NV * ntiles + t, ntiles);
+  }
+  // trace of T (diagonal pairs)
+  {
+    double v = tr;
+    v += __shfl_xor(v, 32, 64);
+    v += __shfl_xor(v, 16, 64);
+    __syncthreads();
+    if (lane < 16) red[0][wv * 16 + lane] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double s = 0.0;
+    for (int k = 0; k < 64; ++k) s += red[0][k];
+    trpart[t] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Kfull * alpha from the lower copy written by the assembly (RMSE,
 // src/kernel_SE_cpp.cpp:238): per 64x64 lower tile, row sums (K a_J) go to
 // slot [J][rows of I] and column sums (K^T a_I) to slot [I][rows of J]; a
@@ -433,12 +658,15 @@ static hipError_t grad_pm(int kind, PairSide S, int B, int ZS, TabView tab, cons
   hipLaunchKernelGGL((k_grad<PM, K, CB>), grid, blk, 0, st, S, B, ZS, tab, A, ld, sA, alpha, \
                      cube, gpart, trpart, nsuper)
   const bool cb = cube != nullptr;
-  if (kind == 0) {
-    if (cb) ACE_G(0, true);
-    else ACE_G(0, false);
+  if (cb) {
+    if (kind == 0) ACE_G(0, true);
+    else ACE_G(1, true);
+  } else if (kind == 0) {
+    hipLaunchKernelGGL((k_grad2<PM, 0>), grid, blk, 0, st, S, B, ZS, tab, A, ld, sA, alpha,
+                       gpart, trpart, nsuper);
   } else {
-    if (cb) ACE_G(1, true);
-    else ACE_G(1, false);
+    hipLaunchKernelGGL((k_grad2<PM, 1>), grid, blk, 0, st, S, B, ZS, tab, A, ld, sA, alpha,
+                       gpart, trpart, nsuper);
   }
 #undef ACE_G
   return hipGetLastError();

@@ -347,9 +347,13 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
       if (I < (kx + 1) * KT) return;
     }
   } else {
-    J = blockIdx.x;
-    I = blockIdx.y;
-    if (J > I) return;
+    // 1-D grid over the lower tiles in row-major order (no dead blocks)
+    const int t = blockIdx.x;
+    int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((i + 1) * (i + 2) / 2 <= t) ++i;
+    while (i * (i + 1) / 2 > t) --i;
+    I = i;
+    J = t - i * (i + 1) / 2;
     if (kx >= 0 && ((I >= kx * KT && I < (kx + 1) * KT) || (J >= kx * KT && J < (kx + 1) * KT)))
       return;
   }
@@ -457,6 +461,126 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
     }
 }
 
+// Lookahead update: only the tiles with I or J in block kx (the next panel).
+// About 2 n/128 tiles -- one workgroup per CU at 128 x 128 -- so it uses
+// 64 x 64 tiles (4 waves of 32 x 32) for 4x the workgroups; same math and
+// write-back rule as k_update.
+constexpr int XT = 64;
+constexpr int XL = XT + 8;  // LDS pitch
+__global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_t ld,
+                                                  const double *__restrict__ W,
+                                                  const double *__restrict__ Pn, int64_t ldp,
+                                                  int64_t k0, int kx) {
+  __shared__ __attribute__((aligned(16))) double sW[2][BK][XL];
+  __shared__ __attribute__((aligned(16))) double sP[2][BK][XL];
+  constexpr int KX = NB / XT;  // 64-tiles per block
+  int I, J;
+  const int y = blockIdx.y;
+  if (y < KX) {
+    I = kx * KX + y;
+    J = blockIdx.x;
+    if (J > I) return;
+  } else {
+    J = kx * KX + (y - KX);
+    I = blockIdx.x;
+    if (I < (kx + 1) * KX) return;
+  }
+  const int kt0 = (int)(k0 / XT), kt1 = kt0 + KX;
+  const bool Ik = I >= kt0 && I < kt1, Jk = J >= kt0 && J < kt1;
+  const int64_t R0 = (int64_t)I * XT, C0 = (int64_t)J * XT;
+  const int tid = threadIdx.x;
+  if (Ik || Jk) {
+    if (Ik && !Jk) {
+      double *tileT = &sW[0][0][0];  // 64 x 65 scratch (fits in sW)
+      for (int e = tid; e < 4096; e += 256) {
+        const int c = e & 63, a = e >> 6;
+        tileT[a * 65 + c] = W[(C0 + c) + (R0 - k0 + a) * ldp];
+      }
+      __syncthreads();
+      for (int e = tid; e < 4096; e += 256) {
+        const int a = e & 63, c = e >> 6;
+        A[(R0 + a) + (C0 + c) * ld] = tileT[a * 65 + c];
+      }
+    } else {
+      for (int e = tid; e < XT * XT; e += 256) {
+        const int a = e & (XT - 1), c = e >> 6;
+        A[(R0 + a) + (C0 + c) * ld] = W[(R0 + a) + (C0 - k0 + c) * ldp];
+      }
+    }
+    return;
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+  const int wr = wv & 1, wc = wv >> 1;  // rows 32*wr.., cols 32*wc..
+  const int lr = lane & 15, lk = lane >> 4;
+  d4 acc[2][2];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) {
+      const int64_t r = R0 + 32 * wr + 16 * ri + lr;
+      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[ci][ri][j] = A[r + (c + 4 * j) * ld];
+    }
+  // staging: 256 threads x (4 doubles of W, 4 of Pn) per 64 x 16 chunk
+  const int sk = tid >> 4, sm = (tid & 15) * 4;
+  const double *gW = W + (R0 + sm) + (int64_t)sk * ldp;
+  const double *gP = Pn + (C0 + sm) + (int64_t)sk * ldp;
+  double2 rw[2], rp[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    rw[e] = *reinterpret_cast<const double2 *>(gW + 2 * e);
+    rp[e] = *reinterpret_cast<const double2 *>(gP + 2 * e);
+  }
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2 * e]) = rw[e];
+    *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2 * e]) = rp[e];
+  }
+  __syncthreads();
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int cur = ch & 1;
+    if (ch + 1 < NCH) {
+      const int64_t off = (int64_t)(ch + 1) * BK * ldp;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        rw[e] = *reinterpret_cast<const double2 *>(gW + off + 2 * e);
+        rp[e] = *reinterpret_cast<const double2 *>(gP + off + 2 * e);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double a[2], b[2];
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci) a[ci] = sP[cur][4 * kk + lk][32 * wc + 16 * ci + lr];
+#pragma unroll
+      for (int ri = 0; ri < 2; ++ri) b[ri] = sW[cur][4 * kk + lk][32 * wr + 16 * ri + lr];
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+        for (int ri = 0; ri < 2; ++ri)
+          acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
+    }
+    if (ch + 1 < NCH) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2 * e]) = rw[e];
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2 * e]) = rp[e];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) {
+      const int64_t r = R0 + 32 * wr + 16 * ri + lr;
+      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) A[r + (c + 4 * j) * ld] = acc[ci][ri][j];
+    }
+}
+
 static hipError_t panel_sweep(const SweepBufs &b, int buf, int64_t k0, hipStream_t st) {
   const int64_t naug = b.ld;
   hipLaunchKernelGGL(k_gather, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st, b.A, b.ld,
@@ -521,8 +645,8 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
       if (e != hipSuccess) return e;
     }
     if (more) {
-      hipLaunchKernelGGL(k_update<true>, dim3(nT, 2 * (NB / UT)), dim3(UTHREADS), 0, st, b.A, b.ld,
-                         b.W[buf], b.P[buf], b.ld, k0, k + 1);
+      hipLaunchKernelGGL(k_update_x, dim3((unsigned)(naug / XT), 2 * (NB / XT)), dim3(256), 0, st,
+                         b.A, b.ld, b.W[buf], b.P[buf], b.ld, k0, k + 1);
       if (two) {
         e = hipEventRecord(sy->ev[2 * k + 1], st);  // cross of block k+1 updated
         if (e != hipSuccess) return e;
@@ -538,8 +662,8 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
     }
     const bool timed = tm && tm->ev && used + 2 <= tm->nev;
     if (timed) (void)hipEventRecord(tm->ev[used], st);
-    hipLaunchKernelGGL(k_update<false>, dim3(nT, nT), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[buf],
-                       b.P[buf], b.ld, k0, more ? k + 1 : -1);
+    hipLaunchKernelGGL(k_update<false>, dim3(nT * (nT + 1) / 2), dim3(UTHREADS), 0, st, b.A, b.ld,
+                       b.W[buf], b.P[buf], b.ld, k0, more ? k + 1 : -1);
     if (timed) {
       (void)hipEventRecord(tm->ev[used + 1], st);
       if (tm->flops) tm->flops[used / 2] =
