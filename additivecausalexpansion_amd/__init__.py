@@ -9,8 +9,8 @@ from .native import (  # noqa: F401
     kernmat_SE_symmetric_cpp, mu_solution_cpp, ncs_basis, ncs_basis_deriv, norm_clip_cpp,
     normalize_test, normalize_train, pred_cpp, pred_marginal_cpp, stats_cpp)
 from .model import (  # noqa: F401
-    DeviceModel, KernelClass_Matern32_R6, KernelClass_SE_R6, optAdam, optNadam, optNesterov,
-    set_optimizer)
+    DeviceModel, KernelClass_Matern32_R6, KernelClass_SE_R6, comm_unique_id, optAdam, optNadam,
+    optNesterov, set_optimizer)
 from .train import (  # noqa: F401
     AceFit, ace_train, linear_spline, ns_spline, predict_ace, set_basis,
     set_initial_parameters, square_spline)

@@ -66,7 +66,14 @@ SIGNATURES = {
     "ace_model_kernel_time": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(_I64),
                                              ctypes.POINTER(ctypes.c_double)]),
+    "ace_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "ace_model_create_sharded": (ctypes.c_int, [_vp, ctypes.c_int, _I64, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_char_p, ctypes.POINTER(_vp)]),
+    "ace_model_shard_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int),
+                                            ctypes.POINTER(ctypes.c_int)]),
 }
+UNIQUE_ID_BYTES = 128
 
 STATUS = {0: "ACE_OK", 1: "ACE_ERR_ARG", 2: "ACE_ERR_HIP", 3: "ACE_ERR_OOM",
           4: "ACE_ERR_UNSUPPORTED"}

@@ -8,12 +8,12 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SOURCES = ["csrc/ace_pairs.hip", "csrc/ace_sweep.hip", "csrc/ace_util.hip",
-           "csrc/ace_api.cpp", "csrc/ace_host.cpp"]
-HEADERS = ["csrc/ace_internal.h", "../include/ace_hip.h"]
+           "csrc/ace_api.cpp", "csrc/ace_host.cpp", "csrc/ace_shard.cpp"]
+HEADERS = ["csrc/ace_internal.h", "csrc/ace_common.h", "../include/ace_hip.h"]
 OUT = os.path.join(HERE, "libace_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-         "-Wno-unused-result"]
+         "-Wno-unused-result", "-ldl"]
 
 
 def needs_build():

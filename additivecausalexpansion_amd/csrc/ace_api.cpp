@@ -11,192 +11,13 @@
 #include <vector>
 
 #include "../../include/ace_hip.h"
+#include "ace_common.h"
 #include "ace_internal.h"
 
 using namespace ace;
 
-struct ace_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;  // main stream (every ABI call syncs it)
-  hipStream_t side = nullptr;    // sweep lookahead: panel factorisation
-  std::string err;
-};
+std::string g_create_err;
 
-static std::string g_create_err;
-
-namespace {
-
-const double kNaN = std::numeric_limits<double>::quiet_NaN();
-
-struct Fail {
-  int code;
-};
-
-// RAII device buffer
-struct DBuf {
-  void *p = nullptr;
-  size_t bytes = 0;
-  DBuf() = default;
-  DBuf(const DBuf &) = delete;
-  DBuf &operator=(const DBuf &) = delete;
-  ~DBuf() { release(); }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-  }
-  double *d() const { return static_cast<double *>(p); }
-  int *i() const { return static_cast<int *>(p); }
-};
-
-void ck(ace_ctx *ctx, hipError_t e, const char *what) {
-  if (e == hipSuccess) return;
-  ctx->err = std::string(what) + ": " + hipGetErrorString(e);
-  throw Fail{e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation ? ACE_ERR_OOM
-                                                                          : ACE_ERR_HIP};
-}
-
-void arg(ace_ctx *ctx, bool ok, const char *msg) {
-  if (ok) return;
-  ctx->err = msg;
-  throw Fail{ACE_ERR_ARG};
-}
-
-void alloc(ace_ctx *ctx, DBuf &b, size_t bytes, const char *what) {
-  if (b.bytes >= bytes && b.p) return;
-  b.release();
-  if (bytes == 0) bytes = 16;
-  ck(ctx, hipMalloc(&b.p, bytes), what);
-  b.bytes = bytes;
-}
-
-// Host -> device copies are synchronous (pageable host buffers may be
-// temporaries); every call syncs its stream before returning, so no kernel
-// of a previous call can still be reading the destination.
-void upload(ace_ctx *ctx, DBuf &b, const double *h, size_t count, const char *what) {
-  alloc(ctx, b, count * sizeof(double), what);
-  if (count) ck(ctx, hipMemcpy(b.p, h, count * sizeof(double), hipMemcpyHostToDevice), what);
-}
-
-void download(ace_ctx *ctx, double *h, const double *d, size_t count, const char *what) {
-  if (count) ck(ctx, hipMemcpyAsync(h, d, count * sizeof(double), hipMemcpyDeviceToHost,
-                                    ctx->stream), what);
-}
-
-void sync(ace_ctx *ctx) { ck(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize"); }
-
-int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
-
-struct Shape {
-  int kind, p, B, PM, ZS;
-};
-
-Shape check_shape(ace_ctx *ctx, int kind, int p, int B) {
-  arg(ctx, kind == ACE_KERNEL_SE || kind == ACE_KERNEL_MATERN32, "unknown kernel kind");
-  arg(ctx, p >= 0 && B >= 1, "p must be >= 0 and B >= 1");
-  if (p > PMAX || B > BMAX) {
-    ctx->err = "unsupported shape: p <= 64 and B <= 32 are compiled";
-    throw Fail{ACE_ERR_UNSUPPORTED};
-  }
-  Shape s;
-  s.kind = kind;
-  s.p = p;
-  s.B = B;
-  s.PM = pm_bucket(p < 1 ? 1 : p);
-  s.ZS = B > 1 ? B - 1 : 1;
-  return s;
-}
-
-// column-major X (n x p) -> row-major n x PM, zero padded
-std::vector<double> pack_rows(const double *M, int64_t n, int cols, int width) {
-  std::vector<double> out((size_t)(n * width), 0.0);
-  for (int i = 0; i < cols; ++i)
-    for (int64_t r = 0; r < n; ++r) out[(size_t)(r * width + i)] = M[r + i * n];
-  return out;
-}
-
-// theta tables (b-major), see TabView in ace_internal.h
-std::vector<double> make_tab(const double *theta, const Shape &s) {
-  const int B = s.B, PM = s.PM;
-  std::vector<double> t((size_t)(2 * B * PM + B), 0.0);
-  for (int b = 0; b < B; ++b) {
-    for (int i = 0; i < s.p; ++i) {
-      t[(size_t)(b * PM + i)] = std::exp(-theta[1 + b + B * (i + 1)]);        // Q1 kernel index
-      t[(size_t)(B * PM + b * PM + i)] = std::exp(-theta[2 + B + b + B * i]);  // gradient index
-    }
-    t[(size_t)(2 * B * PM + b)] = theta[2 + b];
-  }
-  return t;
-}
-
-TabView tab_view(const DBuf &b, const Shape &s) {
-  TabView v;
-  v.wk = b.d();
-  v.wg = b.d() + s.B * s.PM;
-  v.lam = b.d() + 2 * s.B * s.PM;
-  return v;
-}
-
-// Device copy of one pair side (X, Z, log|Z|).
-struct SideBufs {
-  DBuf X, Z, LZ;
-  PairSide view(int64_t n) const {
-    PairSide ps;
-    ps.X = X.d();
-    ps.Z = Z.d();
-    ps.LZ = LZ.d();
-    ps.n = n;
-    return ps;
-  }
-};
-
-void upload_side(ace_ctx *ctx, SideBufs &sb, const Shape &s, const double *X, const double *Z,
-                 int64_t n, int64_t nalloc) {
-  std::vector<double> xr = pack_rows(X, n, s.p, s.PM);
-  xr.resize((size_t)(nalloc * s.PM), 0.0);
-  upload(ctx, sb.X, xr.data(), xr.size(), "upload X");
-  std::vector<double> zr((size_t)(nalloc * s.ZS), 0.0);
-  if (s.B > 1 && Z) {
-    std::vector<double> t = pack_rows(Z, n, s.B - 1, s.ZS);
-    std::copy(t.begin(), t.end(), zr.begin());
-  }
-  upload(ctx, sb.Z, zr.data(), zr.size(), "upload Z");
-  alloc(ctx, sb.LZ, zr.size() * sizeof(double), "alloc LZ");
-  if (s.kind == ACE_KERNEL_SE)
-    ck(ctx, launch_log_abs(sb.Z.d(), sb.LZ.d(), (int64_t)zr.size(), ctx->stream), "log_abs");
-}
-
-double host_logsum(const double *w, int64_t n) {
-  double s = 0.0;
-  for (int64_t j = 0; j < n; ++j) s += std::log(w[j]);
-  return s;
-}
-
-// Final composition of the P-gradient from the device sums.
-//   gsum[b*(PM+1)+i] : sum T K_b d_i^2 (SE) / sum T K_b/(1+sqrt(3 r~2)) d_i^2 (Matern)
-//   gsum[b*(PM+1)+PM]: sum T K_b ; gsum[B*(PM+1)] : trace T
-void compose_grad(const Shape &s, const double *theta, const double *gsum, double sum_alpha,
-                  double *grad) {
-  const int B = s.B, PM = s.PM, P = 2 + B * (s.p + 1);
-  for (int j = 0; j < P; ++j) grad[j] = 0.0;
-  grad[0] = -0.5 * gsum[B * (PM + 1)] * std::exp(theta[0]);  // sigma_gradient
-  for (int b = 0; b < B; ++b) grad[2 + b] = -0.5 * gsum[b * (PM + 1) + PM];
-  for (int i = 0; i < s.p; ++i)
-    for (int b = 0; b < B; ++b) {
-      const int j = 2 + B + b + B * i;
-      const double sum = gsum[b * (PM + 1) + i];
-      if (s.kind == ACE_KERNEL_SE) grad[j] = -0.5 * (sum * std::exp(-theta[j]));
-      else grad[j] = -0.25 * 9 * sum * std::exp(-theta[j]);
-    }
-  grad[1] = (s.kind == ACE_KERNEL_SE) ? sum_alpha : 0.0;
-}
-
-}  // namespace
-
-#define ACE_TRY try {
-#define ACE_CATCH \
-  }               \
-  catch (const Fail &f) { return f.code; }
 
 extern "C" {
 
@@ -679,6 +500,7 @@ struct ace_model {
   double t_ms[3] = {0, 0, 0};
   int64_t t_launch[3] = {0, 0, 0};
   double t_work[3] = {0, 0, 0};
+  ShardModel *shard = nullptr;  // block-column-sharded model (ace_shard.cpp)
 };
 
 namespace {
@@ -800,6 +622,7 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
 void ace_model_destroy(ace_model *m) {
   if (!m) return;
   (void)hipSetDevice(m->ctx->device);
+  if (m->shard) shard_destroy(m->shard);
   for (auto &e : m->ev_upd)
     if (e) (void)hipEventDestroy(e);
   for (int j = 0; j < 2; ++j) {
@@ -816,6 +639,12 @@ int ace_model_set_data(ace_model *m, const double *y, const double *X, const dou
   ACE_TRY
   ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
   arg(ctx, y && (m->s.p == 0 || X) && (m->s.B == 1 || Z), "null argument");
+  if (m->shard) {
+    shard_set_data(m->shard, y, X, Z);
+    m->std_y = std_y;
+    m->has_data = true;
+    return ACE_OK;
+  }
   upload_side(ctx, m->side, m->s, X, Z, m->n, m->npad);
   std::vector<double> yp((size_t)m->npad, 0.0);
   std::copy(y, y + m->n, yp.begin());
@@ -838,18 +667,23 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, d
   arg(ctx, theta && grad && stats, "null argument");
   const Shape &s = m->s;
   const bool timed = m->prof;
-  model_pipeline(m, m->sw, theta, iter == 1 ? 1 : 0, timed);
   const int ncol = s.B * (s.PM + 1);
   std::vector<double> gs((size_t)(ncol + 1));
   double sums[4], scal[5];
   int flag = 0;
-  download(ctx, gs.data(), m->gsum.d(), gs.size(), "download gsum");
-  download(ctx, sums, m->sums.d(), 4, "download sums");
-  download(ctx, scal, m->scal.d(), 5, "download scal");
-  ck(ctx, hipMemcpyAsync(&flag, m->sw.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
-     "download flag");
-  sync(ctx);
-  if (timed) model_collect_timing(m);
+  if (m->shard) {
+    shard_eval(m->shard, theta, iter == 1 ? 1 : 0, 0, timed, gs.data(), sums, scal, &flag);
+    if (timed) shard_collect_timing(m->shard, m->t_ms, m->t_launch, m->t_work);
+  } else {
+    model_pipeline(m, m->sw, theta, iter == 1 ? 1 : 0, timed);
+    download(ctx, gs.data(), m->gsum.d(), gs.size(), "download gsum");
+    download(ctx, sums, m->sums.d(), 4, "download sums");
+    download(ctx, scal, m->scal.d(), 5, "download scal");
+    ck(ctx, hipMemcpyAsync(&flag, m->sw.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
+       "download flag");
+    sync(ctx);
+    if (timed) model_collect_timing(m);
+  }
   if (iter == 1) theta[1] = scal[3];  // mean_solution before the gradient (R/kernel_SE_R6.R:45)
   compose_grad(s, theta, gs.data(), sums[2], grad);
   stats[0] = m->std_y * std::sqrt(sums[0]) / std::sqrt((double)m->n);
@@ -871,14 +705,20 @@ int ace_model_train_stats(ace_model *m, const double *theta, double *stats) {
   ACE_TRY
   ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
   arg(ctx, m->has_data && theta && stats, "null argument / no data");
-  m->sw2.ensure(ctx, m->n);
-  model_pipeline(m, m->sw2, theta, 0, false);
   double sums[4];
   int flag = 0;
-  download(ctx, sums, m->sums.d(), 4, "download sums");
-  ck(ctx, hipMemcpyAsync(&flag, m->sw2.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
-     "download flag");
-  sync(ctx);
+  if (m->shard) {
+    std::vector<double> gs((size_t)(m->s.B * (m->s.PM + 1) + 1));
+    double scal[5];
+    shard_eval(m->shard, theta, 0, 1, false, gs.data(), sums, scal, &flag);
+  } else {
+    m->sw2.ensure(ctx, m->n);
+    model_pipeline(m, m->sw2, theta, 0, false);
+    download(ctx, sums, m->sums.d(), 4, "download sums");
+    ck(ctx, hipMemcpyAsync(&flag, m->sw2.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
+       "download flag");
+    sync(ctx);
+  }
   stats[0] = m->std_y * std::sqrt(sums[0]) / std::sqrt((double)m->n);
   stats[1] = -0.5 * (m->n * std::log(2.0 * M_PI) + sums[3] + sums[1]);
   if (flag) stats[0] = stats[1] = kNaN;
@@ -892,6 +732,10 @@ int ace_model_get_inverse(ace_model *m, double *inv) {
   ACE_TRY
   ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
   arg(ctx, inv != nullptr, "null argument");
+  if (m->shard) {
+    shard_get_inverse(m->shard, inv);
+    return ACE_OK;
+  }
   DBuf out;
   alloc(ctx, out, (size_t)(m->n * m->n) * sizeof(double), "alloc inverse");
   ck(ctx, launch_sym_from_lower(m->sw.A.d(), m->naug, m->n, -1.0, out.d(), m->n, ctx->stream),
@@ -918,6 +762,48 @@ int ace_model_kernel_time(ace_model *m, int which, double *ms, int64_t *launches
   if (ms) *ms = m->t_ms[which];
   if (launches) *launches = m->t_launch[which];
   if (work) *work = m->t_work[which];
+  return ACE_OK;
+}
+
+int ace_comm_unique_id(unsigned char *id) {
+  if (!id) return ACE_ERR_ARG;
+  try {
+    shard_unique_id(id);
+  } catch (const std::exception &e) {
+    g_create_err = e.what();
+    return ACE_ERR_HIP;
+  }
+  return ACE_OK;
+}
+
+int ace_model_create_sharded(ace_ctx *ctx, int kind, int64_t n, int p, int B, int world,
+                             int rank, const unsigned char *id, ace_model **out) {
+  if (!ctx || !out) return ACE_ERR_ARG;
+  *out = nullptr;
+  ace_model *m = new ace_model();
+  m->ctx = ctx;
+  try {
+    ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    m->s = check_shape(ctx, kind, p, B);
+    arg(ctx, n >= 2, "n must be >= 2");
+    arg(ctx, world >= 1 && world <= 64 && rank >= 0 && rank < world, "bad world / rank");
+    arg(ctx, id != nullptr || rank == 0, "simulated group (id == NULL) is created as rank 0");
+    m->n = n;
+    m->npad = round_up(n, NB);
+    m->naug = m->npad + AUG;
+    m->shard = shard_create(ctx, m->s, n, world, rank, id);
+  } catch (const Fail &f) {
+    ace_model_destroy(m);
+    return f.code;
+  }
+  *out = m;
+  return ACE_OK;
+}
+
+int ace_model_shard_info(const ace_model *m, int *world, int *rank) {
+  if (!m) return ACE_ERR_ARG;
+  if (world) *world = m->shard ? shard_world(m->shard) : 1;
+  if (rank) *rank = m->shard ? shard_rank(m->shard) : 0;
   return ACE_OK;
 }
 

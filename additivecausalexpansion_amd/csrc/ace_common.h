@@ -1,0 +1,214 @@
+// ace_common.h -- host-side helpers shared by the C ABI (ace_api.cpp) and the
+// sharded model (ace_shard.cpp): the context, device buffers, argument and
+// error handling, theta tables, pair-side uploads and gradient composition.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "../../include/ace_hip.h"
+#include "ace_internal.h"
+
+struct ace_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;  // main stream (every ABI call syncs it)
+  hipStream_t side = nullptr;    // sweep lookahead: panel factorisation
+  std::string err;
+};
+
+extern std::string g_create_err;
+
+namespace ace_host {
+using namespace ace;
+
+inline const double kNaN = std::numeric_limits<double>::quiet_NaN();
+
+struct Fail {
+  int code;
+};
+
+// RAII device buffer
+struct DBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  DBuf() = default;
+  DBuf(const DBuf &) = delete;
+  DBuf &operator=(const DBuf &) = delete;
+  ~DBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  double *d() const { return static_cast<double *>(p); }
+  int *i() const { return static_cast<int *>(p); }
+};
+
+inline void ck(ace_ctx *ctx, hipError_t e, const char *what) {
+  if (e == hipSuccess) return;
+  ctx->err = std::string(what) + ": " + hipGetErrorString(e);
+  throw Fail{e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation ? ACE_ERR_OOM
+                                                                          : ACE_ERR_HIP};
+}
+
+inline void arg(ace_ctx *ctx, bool ok, const char *msg) {
+  if (ok) return;
+  ctx->err = msg;
+  throw Fail{ACE_ERR_ARG};
+}
+
+inline void alloc(ace_ctx *ctx, DBuf &b, size_t bytes, const char *what) {
+  if (b.bytes >= bytes && b.p) return;
+  b.release();
+  if (bytes == 0) bytes = 16;
+  ck(ctx, hipMalloc(&b.p, bytes), what);
+  b.bytes = bytes;
+}
+
+// Host -> device copies are synchronous (pageable host buffers may be
+// temporaries); every call syncs its stream before returning, so no kernel
+// of a previous call can still be reading the destination.
+inline void upload(ace_ctx *ctx, DBuf &b, const double *h, size_t count, const char *what) {
+  alloc(ctx, b, count * sizeof(double), what);
+  if (count) ck(ctx, hipMemcpy(b.p, h, count * sizeof(double), hipMemcpyHostToDevice), what);
+}
+
+inline void download(ace_ctx *ctx, double *h, const double *d, size_t count, const char *what) {
+  if (count) ck(ctx, hipMemcpyAsync(h, d, count * sizeof(double), hipMemcpyDeviceToHost,
+                                    ctx->stream), what);
+}
+
+inline void sync(ace_ctx *ctx) { ck(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize"); }
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+struct Shape {
+  int kind, p, B, PM, ZS;
+};
+
+inline Shape check_shape(ace_ctx *ctx, int kind, int p, int B) {
+  arg(ctx, kind == ACE_KERNEL_SE || kind == ACE_KERNEL_MATERN32, "unknown kernel kind");
+  arg(ctx, p >= 0 && B >= 1, "p must be >= 0 and B >= 1");
+  if (p > PMAX || B > BMAX) {
+    ctx->err = "unsupported shape: p <= 64 and B <= 32 are compiled";
+    throw Fail{ACE_ERR_UNSUPPORTED};
+  }
+  Shape s;
+  s.kind = kind;
+  s.p = p;
+  s.B = B;
+  s.PM = pm_bucket(p < 1 ? 1 : p);
+  s.ZS = B > 1 ? B - 1 : 1;
+  return s;
+}
+
+// column-major X (n x p) -> row-major n x PM, zero padded
+inline std::vector<double> pack_rows(const double *M, int64_t n, int cols, int width) {
+  std::vector<double> out((size_t)(n * width), 0.0);
+  for (int i = 0; i < cols; ++i)
+    for (int64_t r = 0; r < n; ++r) out[(size_t)(r * width + i)] = M[r + i * n];
+  return out;
+}
+
+// theta tables (b-major), see TabView in ace_internal.h
+inline std::vector<double> make_tab(const double *theta, const Shape &s) {
+  const int B = s.B, PM = s.PM;
+  std::vector<double> t((size_t)(2 * B * PM + B), 0.0);
+  for (int b = 0; b < B; ++b) {
+    for (int i = 0; i < s.p; ++i) {
+      t[(size_t)(b * PM + i)] = std::exp(-theta[1 + b + B * (i + 1)]);        // Q1 kernel index
+      t[(size_t)(B * PM + b * PM + i)] = std::exp(-theta[2 + B + b + B * i]);  // gradient index
+    }
+    t[(size_t)(2 * B * PM + b)] = theta[2 + b];
+  }
+  return t;
+}
+
+inline TabView tab_view(const DBuf &b, const Shape &s) {
+  TabView v;
+  v.wk = b.d();
+  v.wg = b.d() + s.B * s.PM;
+  v.lam = b.d() + 2 * s.B * s.PM;
+  return v;
+}
+
+// Device copy of one pair side (X, Z, log|Z|).
+struct SideBufs {
+  DBuf X, Z, LZ;
+  PairSide view(int64_t n) const {
+    PairSide ps;
+    ps.X = X.d();
+    ps.Z = Z.d();
+    ps.LZ = LZ.d();
+    ps.n = n;
+    return ps;
+  }
+};
+
+inline void upload_side(ace_ctx *ctx, SideBufs &sb, const Shape &s, const double *X, const double *Z,
+                 int64_t n, int64_t nalloc) {
+  std::vector<double> xr = pack_rows(X, n, s.p, s.PM);
+  xr.resize((size_t)(nalloc * s.PM), 0.0);
+  upload(ctx, sb.X, xr.data(), xr.size(), "upload X");
+  std::vector<double> zr((size_t)(nalloc * s.ZS), 0.0);
+  if (s.B > 1 && Z) {
+    std::vector<double> t = pack_rows(Z, n, s.B - 1, s.ZS);
+    std::copy(t.begin(), t.end(), zr.begin());
+  }
+  upload(ctx, sb.Z, zr.data(), zr.size(), "upload Z");
+  alloc(ctx, sb.LZ, zr.size() * sizeof(double), "alloc LZ");
+  if (s.kind == ACE_KERNEL_SE)
+    ck(ctx, launch_log_abs(sb.Z.d(), sb.LZ.d(), (int64_t)zr.size(), ctx->stream), "log_abs");
+}
+
+inline double host_logsum(const double *w, int64_t n) {
+  double s = 0.0;
+  for (int64_t j = 0; j < n; ++j) s += std::log(w[j]);
+  return s;
+}
+
+// Final composition of the P-gradient from the device sums.
+//   gsum[b*(PM+1)+i] : sum T K_b d_i^2 (SE) / sum T K_b/(1+sqrt(3 r~2)) d_i^2 (Matern)
+//   gsum[b*(PM+1)+PM]: sum T K_b ; gsum[B*(PM+1)] : trace T
+inline void compose_grad(const Shape &s, const double *theta, const double *gsum, double sum_alpha,
+                  double *grad) {
+  const int B = s.B, PM = s.PM, P = 2 + B * (s.p + 1);
+  for (int j = 0; j < P; ++j) grad[j] = 0.0;
+  grad[0] = -0.5 * gsum[B * (PM + 1)] * std::exp(theta[0]);  // sigma_gradient
+  for (int b = 0; b < B; ++b) grad[2 + b] = -0.5 * gsum[b * (PM + 1) + PM];
+  for (int i = 0; i < s.p; ++i)
+    for (int b = 0; b < B; ++b) {
+      const int j = 2 + B + b + B * i;
+      const double sum = gsum[b * (PM + 1) + i];
+      if (s.kind == ACE_KERNEL_SE) grad[j] = -0.5 * (sum * std::exp(-theta[j]));
+      else grad[j] = -0.25 * 9 * sum * std::exp(-theta[j]);
+    }
+  grad[1] = (s.kind == ACE_KERNEL_SE) ? sum_alpha : 0.0;
+}
+
+}  // namespace ace_host
+using namespace ace_host;
+
+#define ACE_TRY try {
+#define ACE_CATCH \
+  }               \
+  catch (const Fail &f) { return f.code; }
+
+// ---- sharded model (ace_shard.cpp); errors throw Fail with ctx->err set ----
+struct ShardModel;
+void shard_unique_id(unsigned char *id);  // throws std::runtime_error
+ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int rank,
+                         const unsigned char *id);
+void shard_destroy(ShardModel *m);
+void shard_set_data(ShardModel *m, const double *y, const double *X, const double *Z);
+void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool timed,
+                double *gsum, double *sums, double *scal, int *flag);
+void shard_get_inverse(ShardModel *m, double *inv);
+void shard_collect_timing(ShardModel *m, double *t_ms, int64_t *t_launch, double *t_work);
+int shard_world(const ShardModel *m);
+int shard_rank(const ShardModel *m);

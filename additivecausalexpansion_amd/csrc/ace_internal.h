@@ -21,6 +21,23 @@ constexpr int BMAX = 32;   // largest supported component count B
 // Feature-count buckets the pair kernels are compiled for.
 int pm_bucket(int p);  // smallest compiled bucket >= p, or -1
 
+// ---- column sharding ---------------------------------------------------------
+// The sharded model (ace_shard.cpp) distributes A by NB-wide column blocks,
+// block-cyclic over G ranks: block j lives on rank j % G, as local block
+// j / G of a naug-row, column-major local array (same ld, same row index).
+// Every kernel that touches A maps a global column through lcol(); G == 1 is
+// the identity, which is the single-GPU layout.
+__host__ __device__ __forceinline__ int64_t lcol(int64_t c, int G) {
+  return G == 1 ? c : (c / NB / G) * NB + c % NB;
+}
+__host__ __device__ __forceinline__ bool owns_col(int64_t c, int G, int r) {
+  return G == 1 || (c / NB) % G == r;
+}
+// A pair / update tile (row tile I, column tile J) of a per-rank tile list.
+struct Tile {
+  int I, J;
+};
+
 // Per-theta tables, b-major: wk[b*PM+i] = exp(-theta[1+b+B*(i+1)]) (kernel
 // index, Q1), wg[b*PM+i] = exp(-theta[2+B+b+B*i]) (gradient index),
 // lam[b] = theta[2+b].  Total 2*B*PM + B doubles.
@@ -45,7 +62,8 @@ struct PairSide {
 hipError_t launch_assembly(int mode, int kind, int PM, PairSide rows,
                            PairSide cols, int64_t npad, int B, int ZS,
                            TabView tab, double sig, double *out, int64_t ld,
-                           double *cube, hipStream_t st);
+                           double *cube, hipStream_t st, const Tile *tiles = nullptr,
+                           int64_t ntiles = 0, int G = 1);
 
 // ---- gradient --------------------------------------------------------------
 // T = sA * A[r,c] - alpha_r alpha_c over the lower 64x64 tiles of [0,n)
@@ -56,13 +74,15 @@ hipError_t launch_assembly(int mode, int kind, int PM, PairSide rows,
 hipError_t launch_grad(int kind, int PM, PairSide side, int B, int ZS,
                        TabView tab, const double *A, int64_t ld, double sA,
                        const double *alpha, const double *cube,
-                       double *gpart, double *trpart, hipStream_t st);
+                       double *gpart, double *trpart, hipStream_t st,
+                       const Tile *tiles = nullptr, int64_t ntiles = 0, int G = 1);
 int64_t grad_ntiles(int64_t n);
 // Kfull * alpha partial rows from a lower-triangle copy of Kfull (ld):
 // kapart[T * npad + x] for 64-tile slot T; sum over T with launch_rowsum.
 hipError_t launch_symv_tiles(const double *K, int64_t ld, int64_t n,
                              const double *alpha, double *kapart, int64_t npad,
-                             hipStream_t st);
+                             hipStream_t st, const Tile *tiles = nullptr,
+                             int64_t ntiles = 0, int G = 1);
 
 // ---- sweep -----------------------------------------------------------------
 struct SweepBufs {
@@ -97,9 +117,44 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sync,
                      const SweepTiming *timing);
 int64_t update_gemm_tiles(int64_t naug, int64_t k0, int kx, bool look);
 
+// ---- sharded sweep (one rank's view; ace_shard.cpp drives the steps) --------
+// Step k on rank r:  shard_pack -> [exchange: broadcast `low` from rank k%G,
+// all-gather `send` -> `recv`] -> shard_unpack_chain (panel k on every rank,
+// pivot chain run redundantly, W for the rows r consumes) -> updates.
+struct ShardSweep {
+  double *A;          // local column blocks, naug x (nloc * NB), ld = naug
+  int64_t ld;         // naug
+  int64_t npad;
+  int G, r;
+  double *P[2], *W[2];  // naug x NB: Pn = -panel (all rows), W (own rows)
+  double *SW;
+  double *S[2];
+  double *piv;        // npad pivots (every rank records all of them)
+  int *flag;
+  double *low;        // (naug - k0) x NB broadcast block
+  double *send;       // shard_row_slots(k, G) x NB x NB own row pieces
+  double *recv;       // G x shard_row_slots(k, G) x NB x NB
+  const Tile *tiles;  // own 128-tiles (row-major lower), device
+  int64_t ntiles;
+};
+int shard_row_slots(int k, int G);
+hipError_t shard_pack(const ShardSweep &b, int k, hipStream_t st);
+hipError_t shard_unpack_chain(const ShardSweep &b, int k, int buf, hipStream_t st);
+// cross tiles of block k+1 with panel k (buffer buf)
+hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t st);
+// every own tile except the cross of block kx (kx < 0: none)
+hipError_t shard_update_main(const ShardSweep &b, int k, int buf, int kx, hipStream_t st);
+
 // ---- small helpers -----------------------------------------------------------
 hipError_t launch_aug_init(double *A, int64_t ld, int64_t npad, int64_t n,
-                           const double *y, hipStream_t st);
+                           const double *y, hipStream_t st, int G = 1, int rank = 0);
+// sharded: vec = [u | v | yKy, yK1, 1K1] of the rank's own columns (zeros elsewhere)
+hipError_t launch_aug_extract(const double *A, int64_t ld, int64_t npad, int G,
+                              int rank, double *vec, hipStream_t st);
+hipError_t launch_alpha_from_vec(const double *vec, int64_t npad, int64_t n,
+                                 double theta1, int use_mu_solution, double *alpha,
+                                 double *scal, hipStream_t st);
+hipError_t launch_add(const double *x, double *y, int64_t count, hipStream_t st);
 // alpha = u - mu_eff * v, u/v read from A's AUG rows; mu_eff = theta1, or
 // 0.5*yK1/1K1 when use_mu_solution; writes scal[0..2] = {yKy, yK1, 1K1},
 // scal[3] = mu_solution, scal[4] = mu_eff.

@@ -60,9 +60,20 @@ template <int PM, int KIND, int MODE>
 __global__ __launch_bounds__(256) void k_assembly(PairSide R, PairSide C, int64_t npad,
                                                   int B, int ZS, TabView tab, double sig,
                                                   double *__restrict__ out, int64_t ld,
-                                                  double *__restrict__ cube) {
-  const int I = blockIdx.y, J = blockIdx.x;
+                                                  double *__restrict__ cube,
+                                                  const Tile *__restrict__ tiles, int G) {
+  int I = blockIdx.y, J = blockIdx.x;
+  if (MODE == 0 && tiles) {  // sharded: the rank's own lower tiles, 1-D grid
+    const Tile tt = tiles[blockIdx.x];
+    I = tt.I;
+    J = tt.J;
+  }
   if (MODE != 2 && J > I) return;
+  if (MODE == 0 && G > 1) {  // local column storage (ace_internal.h lcol)
+    const int64_t coff = lcol((int64_t)J * AT, G) - (int64_t)J * AT;
+    out += coff * ld;
+    if (cube) cube += coff * ld;
+  }
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t r = (int64_t)I * AT + lane;
@@ -156,7 +167,8 @@ __global__ __launch_bounds__(256) void k_grad(PairSide S, int B, int ZS, TabView
                                               double sA, const double *__restrict__ alpha,
                                               const double *__restrict__ cube,
                                               double *__restrict__ gpart,
-                                              double *__restrict__ trpart, int64_t ntiles) {
+                                              double *__restrict__ trpart, int64_t ntiles,
+                                              const Tile *__restrict__ tiles, int G) {
   constexpr int NV = PM + 1;
   constexpr int NM = AT / 4;
   __shared__ double red[NV][64];
@@ -164,10 +176,18 @@ __global__ __launch_bounds__(256) void k_grad(PairSide S, int B, int ZS, TabView
   __shared__ double sT[NM][256];                        // T of each lane's pairs
   __shared__ double sR[(KIND == 1 && !CUBE) ? NM : 1][256];  // r2_{b+1} per pair
   const int64_t t = blockIdx.x;
-  int64_t I = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-  while ((I + 1) * (I + 2) / 2 <= t) ++I;
-  while (I * (I + 1) / 2 > t) --I;
-  const int64_t J = t - I * (I + 1) / 2;
+  int64_t I, J;
+  if (tiles) {  // sharded: the rank's own lower tiles
+    const Tile tt = tiles[t];
+    I = tt.I;
+    J = tt.J;
+    A += (lcol(J * AT, G) - J * AT) * ld;
+  } else {
+    I = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    while (I * (I + 1) / 2 > t) --I;
+    J = t - I * (I + 1) / 2;
+  }
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -377,7 +397,8 @@ __global__ __launch_bounds__(256) void k_grad2(PairSide S, int B, int ZS, TabVie
                                                const double *__restrict__ A, int64_t ld,
                                                double sA, const double *__restrict__ alpha,
                                                double *__restrict__ gpart,
-                                               double *__restrict__ trpart, int64_t ntiles) {
+                                               double *__restrict__ trpart, int64_t ntiles,
+                                               const Tile *__restrict__ tiles, int G) {
   constexpr int NV = PM + 1;
   constexpr int NM = AT / 4;
   __shared__ double red[NV][64];
@@ -385,10 +406,18 @@ __global__ __launch_bounds__(256) void k_grad2(PairSide S, int B, int ZS, TabVie
   __shared__ double sT[NM][256];                      // T of each lane's pairs
   __shared__ double sF[KIND == 1 ? NM : 1][256];      // Matern: 1 + sqrt3 t of slice b+1
   const int64_t t = blockIdx.x;
-  int64_t I = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-  while ((I + 1) * (I + 2) / 2 <= t) ++I;
-  while (I * (I + 1) / 2 > t) --I;
-  const int64_t J = t - I * (I + 1) / 2;
+  int64_t I, J;
+  if (tiles) {  // sharded: the rank's own lower tiles
+    const Tile tt = tiles[t];
+    I = tt.I;
+    J = tt.J;
+    A += (lcol(J * AT, G) - J * AT) * ld;
+  } else {
+    I = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    while (I * (I + 1) / 2 > t) --I;
+    J = t - I * (I + 1) / 2;
+  }
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -541,10 +570,17 @@ __global__ __launch_bounds__(256) void k_grad2(PairSide S, int B, int ZS, TabVie
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_symv_tiles(const double *__restrict__ K, int64_t ld,
                                                     int64_t n, const double *__restrict__ alpha,
-                                                    double *__restrict__ kapart, int64_t npad) {
+                                                    double *__restrict__ kapart, int64_t npad,
+                                                    const Tile *__restrict__ tiles, int G) {
   __shared__ double t[AT][AT + 1];
   __shared__ double part[4][AT];
-  const int64_t J = blockIdx.x, I = blockIdx.y;
+  int64_t J = blockIdx.x, I = blockIdx.y;
+  if (tiles) {
+    const Tile tt = tiles[blockIdx.x];
+    I = tt.I;
+    J = tt.J;
+    K += (lcol(J * AT, G) - J * AT) * ld;
+  }
   if (J > I) return;
   const int tid = threadIdx.x, x = tid & 63, q = tid >> 6;
   for (int e = tid; e < AT * AT; e += 256) {
@@ -583,9 +619,17 @@ __global__ __launch_bounds__(256) void k_symv_tiles(const double *__restrict__ K
 }
 
 hipError_t launch_symv_tiles(const double *K, int64_t ld, int64_t n, const double *alpha,
-                             double *kapart, int64_t npad, hipStream_t st) {
+                             double *kapart, int64_t npad, hipStream_t st, const Tile *tiles,
+                             int64_t ntiles, int G) {
   const unsigned nt = (unsigned)((n + AT - 1) / AT);
-  hipLaunchKernelGGL(k_symv_tiles, dim3(nt, nt), dim3(256), 0, st, K, ld, n, alpha, kapart, npad);
+  if (tiles) {
+    if (ntiles > 0)
+      hipLaunchKernelGGL(k_symv_tiles, dim3((unsigned)ntiles), dim3(256), 0, st, K, ld, n, alpha,
+                         kapart, npad, tiles, G);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_symv_tiles, dim3(nt, nt), dim3(256), 0, st, K, ld, n, alpha, kapart, npad,
+                     tiles, G);
   return hipGetLastError();
 }
 
@@ -608,10 +652,13 @@ int64_t grad_ntiles(int64_t n) {
 template <int PM>
 static hipError_t asm_pm(int mode, int kind, PairSide R, PairSide C, int64_t npad, int B,
                          int ZS, TabView tab, double sig, double *out, int64_t ld,
-                         double *cube, hipStream_t st) {
+                         double *cube, hipStream_t st, const Tile *tiles, int64_t ntiles, int G) {
   dim3 blk(256);
   dim3 grid;
-  if (mode == 0) {
+  if (mode == 0 && tiles) {
+    if (ntiles == 0) return hipSuccess;
+    grid = dim3((unsigned)ntiles);
+  } else if (mode == 0) {
     const unsigned nt = (unsigned)(npad / AT);
     grid = dim3(nt, nt);
   } else if (mode == 1) {
@@ -621,7 +668,8 @@ static hipError_t asm_pm(int mode, int kind, PairSide R, PairSide C, int64_t npa
     grid = dim3((unsigned)((C.n + AT - 1) / AT), (unsigned)((R.n + AT - 1) / AT));
   }
 #define ACE_ASM(K, M) \
-  hipLaunchKernelGGL((k_assembly<PM, K, M>), grid, blk, 0, st, R, C, npad, B, ZS, tab, sig, out, ld, cube)
+  hipLaunchKernelGGL((k_assembly<PM, K, M>), grid, blk, 0, st, R, C, npad, B, ZS, tab, sig, out, ld, \
+                     cube, tiles, G)
   if (kind == 0) {
     if (mode == 0) ACE_ASM(0, 0);
     else if (mode == 1) ACE_ASM(0, 1);
@@ -637,10 +685,12 @@ static hipError_t asm_pm(int mode, int kind, PairSide R, PairSide C, int64_t npa
 
 hipError_t launch_assembly(int mode, int kind, int PM, PairSide R, PairSide C, int64_t npad,
                            int B, int ZS, TabView tab, double sig, double *out, int64_t ld,
-                           double *cube, hipStream_t st) {
+                           double *cube, hipStream_t st, const Tile *tiles, int64_t ntiles,
+                           int G) {
   switch (PM) {
 #define ACE_CASE(P) \
-  case P: return asm_pm<P>(mode, kind, R, C, npad, B, ZS, tab, sig, out, ld, cube, st);
+  case P:           \
+    return asm_pm<P>(mode, kind, R, C, npad, B, ZS, tab, sig, out, ld, cube, st, tiles, ntiles, G);
     ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
     ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
 #undef ACE_CASE
@@ -651,22 +701,24 @@ hipError_t launch_assembly(int mode, int kind, int PM, PairSide R, PairSide C, i
 template <int PM>
 static hipError_t grad_pm(int kind, PairSide S, int B, int ZS, TabView tab, const double *A,
                           int64_t ld, double sA, const double *alpha, const double *cube,
-                          double *gpart, double *trpart, hipStream_t st) {
-  const int64_t nsuper = grad_ntiles(S.n);
+                          double *gpart, double *trpart, hipStream_t st, const Tile *tiles,
+                          int64_t ntiles, int G) {
+  const int64_t nsuper = tiles ? ntiles : grad_ntiles(S.n);
+  if (nsuper == 0) return hipSuccess;
   dim3 grid((unsigned)nsuper), blk(256);
 #define ACE_G(K, CB)                                                                          \
   hipLaunchKernelGGL((k_grad<PM, K, CB>), grid, blk, 0, st, S, B, ZS, tab, A, ld, sA, alpha, \
-                     cube, gpart, trpart, nsuper)
+                     cube, gpart, trpart, nsuper, tiles, G)
   const bool cb = cube != nullptr;
   if (cb) {
     if (kind == 0) ACE_G(0, true);
     else ACE_G(1, true);
   } else if (kind == 0) {
     hipLaunchKernelGGL((k_grad2<PM, 0>), grid, blk, 0, st, S, B, ZS, tab, A, ld, sA, alpha,
-                       gpart, trpart, nsuper);
+                       gpart, trpart, nsuper, tiles, G);
   } else {
     hipLaunchKernelGGL((k_grad2<PM, 1>), grid, blk, 0, st, S, B, ZS, tab, A, ld, sA, alpha,
-                       gpart, trpart, nsuper);
+                       gpart, trpart, nsuper, tiles, G);
   }
 #undef ACE_G
   return hipGetLastError();
@@ -674,10 +726,13 @@ static hipError_t grad_pm(int kind, PairSide S, int B, int ZS, TabView tab, cons
 
 hipError_t launch_grad(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                        const double *A, int64_t ld, double sA, const double *alpha,
-                       const double *cube, double *gpart, double *trpart, hipStream_t st) {
+                       const double *cube, double *gpart, double *trpart, hipStream_t st,
+                       const Tile *tiles, int64_t ntiles, int G) {
   switch (PM) {
 #define ACE_CASE(P) \
-  case P: return grad_pm<P>(kind, S, B, ZS, tab, A, ld, sA, alpha, cube, gpart, trpart, st);
+  case P:           \
+    return grad_pm<P>(kind, S, B, ZS, tab, A, ld, sA, alpha, cube, gpart, trpart, st, tiles, \
+                      ntiles, G);
     ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
     ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
 #undef ACE_CASE

@@ -1,0 +1,564 @@
+// ace_shard.cpp -- block-column-sharded para_update across GPUs.
+//
+// Layout: A (naug x naug, lower triangle, the AUG rows [y; 1] appended) is
+// split into NB-wide column blocks, block j on rank j % G, stored as local
+// block j / G of a naug x (nloc NB) column-major array with the global row
+// index (ace_internal.h lcol).  The Kfull copy for the RMSE uses the same
+// layout.  X, Z, y are replicated (<= 26 MB at C4).
+//
+// One evaluation on rank r:
+//   assembly      own lower 64-tiles (+ identity padding, sigma diagonal)
+//   sweep step k  pack -> exchange -> unpack + pivot chain -> update
+//                 exchange = RCCL group { broadcast of panel rows >= k0 from
+//                 rank k % G, all-gather of the row pieces A[k, j<k] }; the
+//                 NB x NB pivot sweep runs redundantly on every rank (it is
+//                 one workgroup of latency) so no second collective carries
+//                 D^-1 or the pivots.  Lookahead as on one GPU: the cross of
+//                 block k+1 is updated first, then pack/exchange/chain of
+//                 panel k+1 run on the side stream under the bulk update.
+//   alpha         AUG rows of own columns -> all-reduce (u, v, corner)
+//   gradient      own 64-tiles of T = -A^-1 - alpha alpha^T; Kfull*alpha
+//                 partial rows from own tiles of the Kfull copy
+//   reduce        one all-reduce of [gradient sums | Kfull*alpha]
+// Every rank then holds identical sums and composes the same P-gradient.
+//
+// The communicator is RCCL (one process per GPU, loaded with dlopen so the
+// library has no link-time RCCL dependency and shares the RCCL a host
+// process such as PyTorch has already loaded) or, with id == NULL, an
+// in-process group that simulates all G ranks on one device with device
+// copies -- the validation mode: same kernels, same packing, same
+// collective semantics.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <memory>
+#include <stdexcept>
+
+#include "ace_common.h"
+#include "ace_internal.h"
+
+using namespace ace;
+
+namespace {
+
+// ------------------------------------------------------------------ RCCL
+struct Rccl {
+  bool ok = false;
+  std::string err;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*Broadcast)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t,
+                            hipStream_t) = nullptr;
+  ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t,
+                            hipStream_t) = nullptr;
+  ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t,
+                            ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  const char *(*GetErrorString)(ncclResult_t) = nullptr;
+
+  Rccl() {
+    // an RCCL already in the process (e.g. PyTorch's) is reused by soname
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      err = std::string("cannot load librccl.so.1: ") + dlerror();
+      return;
+    }
+#define ACE_SYM(f, name)                                              \
+  f = reinterpret_cast<decltype(f)>(dlsym(h, name));                  \
+  if (!f) {                                                           \
+    err = std::string("librccl.so.1 lacks ") + name;                  \
+    return;                                                           \
+  }
+    ACE_SYM(GetUniqueId, "ncclGetUniqueId");
+    ACE_SYM(CommInitRank, "ncclCommInitRank");
+    ACE_SYM(CommDestroy, "ncclCommDestroy");
+    ACE_SYM(Broadcast, "ncclBroadcast");
+    ACE_SYM(AllGather, "ncclAllGather");
+    ACE_SYM(AllReduce, "ncclAllReduce");
+    ACE_SYM(GroupStart, "ncclGroupStart");
+    ACE_SYM(GroupEnd, "ncclGroupEnd");
+    ACE_SYM(GetErrorString, "ncclGetErrorString");
+#undef ACE_SYM
+    ok = true;
+  }
+};
+
+Rccl &rccl() {
+  static Rccl r;
+  return r;
+}
+
+void nck(ace_ctx *ctx, ncclResult_t e, const char *what) {
+  if (e == ncclSuccess) return;
+  ctx->err = std::string(what) + ": " + rccl().GetErrorString(e);
+  throw Fail{ACE_ERR_HIP};
+}
+
+// ------------------------------------------------------------------ rank
+struct RankState {
+  int r = 0;
+  DBuf A[2], kcopy;  // A[1]: train_stats scratch (keeps A[0]'s inverse, Q6)
+  DBuf P[2], W[2], SW, S[2], piv, flag, low, send, recv;
+  DBuf tupd, tasm, tgrad;  // device tile lists
+  int64_t nupd = 0, nasm = 0, ngrad = 0, ndiag = 0;
+  std::vector<Tile> hupd;  // host copy (flop accounting)
+  DBuf y, tab, alpha, scal, gpart, trpart, kapart, red, sums, augvec;
+  SideBufs side;
+};
+
+}  // namespace
+
+struct ShardModel {
+  ace_ctx *ctx = nullptr;
+  Shape s{};
+  int64_t n = 0, npad = 0, naug = 0, ntr = 0;
+  int G = 1, rank = 0;
+  bool sim = true;
+  ncclComm_t comm = nullptr;
+  std::vector<std::unique_ptr<RankState>> ranks;  // 1 (RCCL) or G (simulated)
+  std::vector<hipEvent_t> ev;                      // lookahead events
+  // timing of local rank 0 (update launches, assembly, gradient)
+  std::vector<hipEvent_t> ev_upd;
+  std::vector<double> upd_flops;
+  hipEvent_t ev_asm[2] = {nullptr, nullptr}, ev_grad[2] = {nullptr, nullptr};
+  int upd_used = 0;
+  ~ShardModel() {
+    for (auto e : ev) (void)hipEventDestroy(e);
+    for (auto e : ev_upd) (void)hipEventDestroy(e);
+    for (int j = 0; j < 2; ++j) {
+      if (ev_asm[j]) (void)hipEventDestroy(ev_asm[j]);
+      if (ev_grad[j]) (void)hipEventDestroy(ev_grad[j]);
+    }
+    if (comm) (void)rccl().CommDestroy(comm);
+  }
+};
+
+namespace {
+
+int64_t ncols_local(int64_t naug, int G, int r) {
+  const int64_t nblk = (naug + NB - 1) / NB;  // column blocks incl. the AUG block
+  int64_t cnt = 0;
+  for (int64_t j = r; j < nblk; j += G) ++cnt;
+  return cnt * NB;
+}
+
+// own lower tiles of size T over [0, ntile*T) in row-major order
+std::vector<Tile> own_tiles(int64_t ntile, int T, int G, int r) {
+  std::vector<Tile> t;
+  for (int64_t I = 0; I < ntile; ++I)
+    for (int64_t J = 0; J <= I; ++J)
+      if (owns_col(J * T, G, r)) t.push_back(Tile{(int)I, (int)J});
+  return t;
+}
+
+void upload_tiles(ace_ctx *ctx, DBuf &b, const std::vector<Tile> &t) {
+  alloc(ctx, b, std::max<size_t>(t.size(), 1) * sizeof(Tile), "alloc tiles");
+  if (!t.empty())
+    ck(ctx, hipMemcpy(b.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
+       "upload tiles");
+}
+
+ShardSweep sweep_view(const ShardModel &m, RankState &R, int which) {
+  ShardSweep b;
+  b.A = R.A[which].d();
+  b.ld = m.naug;
+  b.npad = m.npad;
+  b.G = m.G;
+  b.r = R.r;
+  for (int j = 0; j < 2; ++j) {
+    b.P[j] = R.P[j].d();
+    b.W[j] = R.W[j].d();
+    b.S[j] = R.S[j].d();
+  }
+  b.SW = R.SW.d();
+  b.piv = R.piv.d();
+  b.flag = R.flag.i();
+  b.low = R.low.d();
+  b.send = R.send.d();
+  b.recv = R.recv.d();
+  b.tiles = reinterpret_cast<const Tile *>(R.tupd.p);
+  b.ntiles = R.nupd;
+  return b;
+}
+
+// GEMM flops of one k_update launch on a tile list (tiles outside block k
+// and outside the cross of kx)
+double update_flops(const std::vector<Tile> &tl, int64_t k0, int kx) {
+  const int KT = NB / UT, kt0 = (int)(k0 / UT), kt1 = kt0 + KT;
+  int64_t cnt = 0;
+  for (const Tile &t : tl) {
+    if (kx >= 0 && ((t.I >= kx * KT && t.I < (kx + 1) * KT) || (t.J >= kx * KT && t.J < (kx + 1) * KT)))
+      continue;
+    const bool Ik = t.I >= kt0 && t.I < kt1, Jk = t.J >= kt0 && t.J < kt1;
+    if (!(Ik || Jk)) ++cnt;
+  }
+  return (double)cnt * 2.0 * UT * UT * NB;
+}
+
+// ---- collectives over the local ranks -------------------------------------
+// Panel exchange of step k on stream st.
+void exchange(ShardModel &m, int k, hipStream_t st) {
+  ace_ctx *ctx = m.ctx;
+  const int64_t k0 = (int64_t)k * NB;
+  const size_t nlow = (size_t)((m.naug - k0) * NB);
+  const int slots = shard_row_slots(k, m.G);
+  const size_t nrow = (size_t)slots * NB * NB;
+  const int root = k % m.G;
+  if (!m.sim) {
+    RankState &R = *m.ranks[0];
+    nck(ctx, rccl().GroupStart(), "ncclGroupStart");
+    nck(ctx, rccl().Broadcast(R.low.p, R.low.p, nlow, ncclDouble, root, m.comm, st),
+        "ncclBroadcast");
+    if (nrow > 0)
+      nck(ctx, rccl().AllGather(R.send.p, R.recv.p, nrow, ncclDouble, m.comm, st),
+          "ncclAllGather");
+    nck(ctx, rccl().GroupEnd(), "ncclGroupEnd");
+    return;
+  }
+  RankState &src = *m.ranks[(size_t)root];
+  for (auto &Rp : m.ranks) {
+    RankState &R = *Rp;
+    if (R.r != root)
+      ck(ctx, hipMemcpyAsync(R.low.p, src.low.p, nlow * sizeof(double), hipMemcpyDeviceToDevice, st),
+         "sim broadcast");
+    if (nrow > 0)
+      for (auto &Sp : m.ranks)
+        ck(ctx, hipMemcpyAsync(R.recv.d() + (size_t)Sp->r * nrow, Sp->send.p, nrow * sizeof(double),
+                               hipMemcpyDeviceToDevice, st),
+           "sim all-gather");
+  }
+}
+
+// In-place sum over ranks of `count` doubles at offset `off` of buffer `which`
+// (0: augvec, 1: red).
+void allreduce(ShardModel &m, int which, int64_t count, hipStream_t st) {
+  ace_ctx *ctx = m.ctx;
+  auto buf = [&](RankState &R) { return which == 0 ? R.augvec.d() : R.red.d(); };
+  if (!m.sim) {
+    double *b = buf(*m.ranks[0]);
+    nck(ctx, rccl().AllReduce(b, b, (size_t)count, ncclDouble, ncclSum, m.comm, st),
+        "ncclAllReduce");
+    return;
+  }
+  if (m.G == 1) return;
+  double *acc = buf(*m.ranks[0]);
+  for (size_t j = 1; j < m.ranks.size(); ++j)
+    ck(ctx, launch_add(buf(*m.ranks[j]), acc, count, st), "sim all-reduce");
+  for (size_t j = 1; j < m.ranks.size(); ++j)
+    ck(ctx, hipMemcpyAsync(buf(*m.ranks[j]), acc, (size_t)count * sizeof(double),
+                           hipMemcpyDeviceToDevice, st),
+       "sim all-reduce");
+}
+
+// ---- the sharded sweep -------------------------------------------------------
+void run_sweep_sharded(ShardModel &m, int which, bool timed) {
+  ace_ctx *ctx = m.ctx;
+  hipStream_t st = ctx->stream;
+  // the simulated group runs everything in order on one stream
+  hipStream_t side = m.sim ? st : ctx->side;
+  const int steps = (int)(m.npad / NB);
+  std::vector<ShardSweep> v;
+  for (auto &R : m.ranks) v.push_back(sweep_view(m, *R, which));
+  auto rec = [&](int idx, hipStream_t s) {
+    if (!m.sim) ck(ctx, hipEventRecord(m.ev[(size_t)idx], s), "event");
+  };
+  auto wait = [&](hipStream_t s, int idx) {
+    if (!m.sim) ck(ctx, hipStreamWaitEvent(s, m.ev[(size_t)idx], 0), "event wait");
+  };
+  auto prepare = [&](int k, int buf) {  // panel k into buffer buf, on `side`
+    for (auto &b : v) ck(ctx, shard_pack(b, k, side), "shard pack");
+    exchange(m, k, side);
+    for (auto &b : v) ck(ctx, shard_unpack_chain(b, k, buf, side), "shard panel");
+  };
+  rec(2 * steps, st);  // inputs ready
+  wait(side, 2 * steps);
+  prepare(0, 0);
+  rec(0, side);
+  m.upd_used = 0;
+  for (int k = 0; k < steps; ++k) {
+    const int buf = k & 1;
+    const bool more = k + 1 < steps;
+    wait(st, 2 * k);  // panel k ready
+    if (more) {
+      for (auto &b : v) ck(ctx, shard_update_cross(b, k, buf, st), "shard cross update");
+      rec(2 * k + 1, st);
+      wait(side, 2 * k + 1);
+      prepare(k + 1, buf ^ 1);
+      rec(2 * (k + 1), side);
+    }
+    const bool tm = timed && m.upd_used + 2 <= (int)m.ev_upd.size();
+    for (size_t j = 0; j < v.size(); ++j) {
+      if (tm && j == 0) ck(ctx, hipEventRecord(m.ev_upd[(size_t)m.upd_used], st), "event");
+      ck(ctx, shard_update_main(v[j], k, buf, more ? k + 1 : -1, st), "shard update");
+      if (tm && j == 0) {
+        ck(ctx, hipEventRecord(m.ev_upd[(size_t)m.upd_used + 1], st), "event");
+        m.upd_flops[(size_t)m.upd_used / 2] =
+            update_flops(m.ranks[0]->hupd, (int64_t)k * NB, more ? k + 1 : -1);
+        m.upd_used += 2;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// ---- entry points used by ace_api.cpp ------------------------------------------
+void shard_unique_id(unsigned char *id) {
+  Rccl &R = rccl();
+  if (!R.ok) throw std::runtime_error(R.err);
+  ncclUniqueId u;
+  if (R.GetUniqueId(&u) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
+  std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+}
+
+ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int rank,
+                         const unsigned char *id) {
+  std::unique_ptr<ShardModel> m(new ShardModel());
+  m->ctx = ctx;
+  m->s = s;
+  m->n = n;
+  m->npad = round_up(n, NB);
+  m->naug = m->npad + AUG;
+  m->ntr = (n + AT - 1) / AT;
+  m->G = world;
+  m->rank = rank;
+  m->sim = id == nullptr;
+  const int64_t naug = m->naug, npad = m->npad;
+  if (!m->sim) {
+    if (!rccl().ok) {
+      ctx->err = rccl().err;
+      throw Fail{ACE_ERR_HIP};
+    }
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    nck(ctx, rccl().CommInitRank(&m->comm, world, u, rank), "ncclCommInitRank");
+  }
+  const int nlocal = m->sim ? world : 1;
+  const int steps = (int)(npad / NB);
+  const int maxslots = shard_row_slots(steps, world);
+  const int ncol = s.B * (s.PM + 1);
+  for (int j = 0; j < nlocal; ++j) {
+    std::unique_ptr<RankState> R(new RankState());
+    R->r = m->sim ? j : rank;
+    const int64_t nloc = ncols_local(naug, world, R->r);
+    alloc(ctx, R->A[0], (size_t)(naug * nloc) * sizeof(double), "alloc local A");
+    alloc(ctx, R->kcopy, (size_t)(naug * nloc) * sizeof(double), "alloc local Kfull copy");
+    ck(ctx, hipMemsetAsync(R->A[0].p, 0, R->A[0].bytes, ctx->stream), "memset A");
+    ck(ctx, hipMemsetAsync(R->kcopy.p, 0, R->kcopy.bytes, ctx->stream), "memset Kfull copy");
+    for (int b = 0; b < 2; ++b) {
+      alloc(ctx, R->P[b], (size_t)(naug * NB) * sizeof(double), "alloc panel");
+      alloc(ctx, R->W[b], (size_t)(naug * NB) * sizeof(double), "alloc panel");
+      alloc(ctx, R->S[b], (size_t)(SUB * NB) * sizeof(double), "alloc S");
+    }
+    alloc(ctx, R->SW, (size_t)(SUB * SUB) * sizeof(double), "alloc SW");
+    alloc(ctx, R->piv, (size_t)npad * sizeof(double), "alloc piv");
+    alloc(ctx, R->flag, 16, "alloc flag");
+    alloc(ctx, R->low, (size_t)(naug * NB) * sizeof(double), "alloc exchange");
+    alloc(ctx, R->send, (size_t)std::max(1, maxslots) * NB * NB * sizeof(double), "alloc exchange");
+    alloc(ctx, R->recv, (size_t)world * std::max(1, maxslots) * NB * NB * sizeof(double),
+          "alloc exchange");
+    R->hupd = own_tiles(naug / UT, UT, world, R->r);
+    R->nupd = (int64_t)R->hupd.size();
+    upload_tiles(ctx, R->tupd, R->hupd);
+    const std::vector<Tile> ta = own_tiles(npad / AT, AT, world, R->r);
+    R->nasm = (int64_t)ta.size();
+    upload_tiles(ctx, R->tasm, ta);
+    const std::vector<Tile> tg = own_tiles(m->ntr, AT, world, R->r);
+    R->ngrad = (int64_t)tg.size();
+    for (const Tile &t : tg) R->ndiag += t.I == t.J;
+    upload_tiles(ctx, R->tgrad, tg);
+    alloc(ctx, R->y, (size_t)npad * sizeof(double), "alloc y");
+    alloc(ctx, R->tab, (size_t)(2 * s.B * s.PM + s.B) * sizeof(double), "alloc tab");
+    alloc(ctx, R->alpha, (size_t)npad * sizeof(double), "alloc alpha");
+    alloc(ctx, R->scal, 16 * sizeof(double), "alloc scal");
+    alloc(ctx, R->gpart, (size_t)(std::max<int64_t>(R->ngrad, 1) * ncol) * sizeof(double),
+          "alloc gpart");
+    alloc(ctx, R->trpart, (size_t)std::max<int64_t>(R->ngrad, 1) * sizeof(double), "alloc trpart");
+    alloc(ctx, R->kapart, (size_t)(m->ntr * npad) * sizeof(double), "alloc kapart");
+    alloc(ctx, R->red, (size_t)(ncol + 1 + npad) * sizeof(double), "alloc reduction");
+    alloc(ctx, R->sums, 8 * sizeof(double), "alloc sums");
+    alloc(ctx, R->augvec, (size_t)(2 * npad + 8) * sizeof(double), "alloc aug vector");
+    m->ranks.push_back(std::move(R));
+  }
+  if (!m->sim) {
+    m->ev.assign((size_t)(2 * steps + 1), nullptr);
+    for (auto &e : m->ev) ck(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+  }
+  m->ev_upd.assign((size_t)(2 * steps), nullptr);
+  m->upd_flops.assign((size_t)steps, 0.0);
+  for (auto &e : m->ev_upd) ck(ctx, hipEventCreate(&e), "event");
+  for (int j = 0; j < 2; ++j) {
+    ck(ctx, hipEventCreate(&m->ev_asm[j]), "event");
+    ck(ctx, hipEventCreate(&m->ev_grad[j]), "event");
+  }
+  sync(ctx);
+  return m.release();
+}
+
+void shard_destroy(ShardModel *m) { delete m; }
+
+void shard_set_data(ShardModel *m, const double *y, const double *X, const double *Z) {
+  ace_ctx *ctx = m->ctx;
+  std::vector<double> yp((size_t)m->npad, 0.0);
+  std::copy(y, y + m->n, yp.begin());
+  for (auto &R : m->ranks) {
+    upload_side(ctx, R->side, m->s, X, Z, m->n, m->npad);
+    ck(ctx, hipMemcpy(R->y.p, yp.data(), yp.size() * sizeof(double), hipMemcpyHostToDevice),
+       "upload y");
+  }
+  sync(ctx);
+}
+
+// One evaluation at theta into A[which]; the host receives (local rank 0's
+// copy of the all-reduced) gradient sums, final sums, scalars and the flag.
+void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool timed,
+                double *gsum, double *sums, double *scal, int *flag) {
+  ace_ctx *ctx = m->ctx;
+  hipStream_t st = ctx->stream;
+  const Shape &s = m->s;
+  const int ncol = s.B * (s.PM + 1);
+  const int64_t naug = m->naug, npad = m->npad, n = m->n;
+  std::vector<double> tab = make_tab(theta, s);
+  for (auto &R : m->ranks) {
+    if (which == 1) {
+      alloc(ctx, R->A[1], R->A[0].bytes, "alloc local A (train stats)");
+      ck(ctx, hipMemsetAsync(R->A[1].p, 0, R->A[1].bytes, st), "memset A");
+    }
+    ck(ctx, hipMemcpyAsync(R->tab.p, tab.data(), tab.size() * sizeof(double),
+                           hipMemcpyHostToDevice, st),
+       "upload tables");
+  }
+  ck(ctx, hipStreamSynchronize(st), "sync tables");  // pageable source
+  // assembly (own tiles) + AUG rows
+  for (size_t j = 0; j < m->ranks.size(); ++j) {
+    RankState &R = *m->ranks[j];
+    const TabView tv = tab_view(R.tab, s);
+    const PairSide ps = R.side.view(n);
+    if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_asm[0], st), "event");
+    ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, npad, s.B, s.ZS, tv, std::exp(theta[0]),
+                            R.A[which].d(), naug, R.kcopy.d(), st, R.tasm.p ? (const Tile *)R.tasm.p : nullptr,
+                            R.nasm, m->G),
+       "assembly");
+    if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_asm[1], st), "event");
+    ck(ctx, launch_aug_init(R.A[which].d(), naug, npad, n, R.y.d(), st, m->G, R.r), "aug init");
+    ck(ctx, hipMemsetAsync(R.flag.p, 0, sizeof(int), st), "memset flag");
+  }
+  run_sweep_sharded(*m, which, timed);
+  // alpha, mu_solution
+  for (auto &R : m->ranks)
+    ck(ctx, launch_aug_extract(R->A[which].d(), naug, npad, m->G, R->r, R->augvec.d(), st),
+       "aug extract");
+  allreduce(*m, 0, 2 * npad + 3, st);
+  for (auto &R : m->ranks)
+    ck(ctx, launch_alpha_from_vec(R->augvec.d(), npad, n, theta[1], use_mu, R->alpha.d(),
+                                  R->scal.d(), st),
+       "alpha");
+  // gradient partial sums and Kfull * alpha partial rows of own tiles
+  for (size_t j = 0; j < m->ranks.size(); ++j) {
+    RankState &R = *m->ranks[j];
+    const TabView tv = tab_view(R.tab, s);
+    const PairSide ps = R.side.view(n);
+    const Tile *tg = (const Tile *)R.tgrad.p;
+    if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_grad[0], st), "event");
+    ck(ctx, launch_grad(s.kind, s.PM, ps, s.B, s.ZS, tv, R.A[which].d(), naug, -1.0, R.alpha.d(),
+                        nullptr, R.gpart.d(), R.trpart.d(), st, tg, R.ngrad, m->G),
+       "grad");
+    if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_grad[1], st), "event");
+    ck(ctx, hipMemsetAsync(R.kapart.p, 0, R.kapart.bytes, st), "memset kapart");
+    ck(ctx, launch_symv_tiles(R.kcopy.d(), naug, n, R.alpha.d(), R.kapart.d(), npad, st, tg,
+                              R.ngrad, m->G),
+       "symv");
+    ck(ctx, hipMemsetAsync(R.red.p, 0, R.red.bytes, st), "memset reduction");
+    if (R.ngrad > 0) {
+      ck(ctx, launch_colsum(R.gpart.d(), R.ngrad, ncol, R.red.d(), st), "colsum");
+      ck(ctx, launch_colsum(R.trpart.d(), R.ngrad, 1, R.red.d() + ncol, st), "colsum");
+    }
+    ck(ctx, launch_rowsum(R.kapart.d(), m->ntr, npad, n, R.red.d() + ncol + 1, st), "rowsum");
+  }
+  allreduce(*m, 1, ncol + 1 + npad, st);
+  for (auto &R : m->ranks)
+    ck(ctx, launch_final_sums(R->y.d(), R->scal.d() + 4, R->alpha.d(), R->red.d() + ncol + 1, n,
+                              R->piv.d(), npad, R->sums.d(), st),
+       "final sums");
+  RankState &R0 = *m->ranks[0];
+  ck(ctx, hipMemcpyAsync(gsum, R0.red.p, (size_t)(ncol + 1) * sizeof(double),
+                         hipMemcpyDeviceToHost, st),
+     "download gsum");
+  ck(ctx, hipMemcpyAsync(sums, R0.sums.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st),
+     "download sums");
+  ck(ctx, hipMemcpyAsync(scal, R0.scal.p, 5 * sizeof(double), hipMemcpyDeviceToHost, st),
+     "download scal");
+  *flag = 0;
+  for (auto &R : m->ranks) {
+    int f = 0;
+    ck(ctx, hipMemcpyAsync(&f, R->flag.p, sizeof(int), hipMemcpyDeviceToHost, st), "download flag");
+    ck(ctx, hipStreamSynchronize(st), "sync");
+    *flag |= f;
+  }
+  sync(ctx);
+}
+
+// Full symmetric inverse (n x n) of the resident A[0] on every rank: own
+// lower columns into a zeroed buffer, all-reduce, mirror.
+void shard_get_inverse(ShardModel *m, double *inv) {
+  ace_ctx *ctx = m->ctx;
+  hipStream_t st = ctx->stream;
+  const int64_t n = m->n, naug = m->naug;
+  DBuf out;
+  std::vector<DBuf> fulls(m->ranks.size());
+  for (size_t j = 0; j < m->ranks.size(); ++j) {
+    RankState &R = *m->ranks[j];
+    alloc(ctx, fulls[j], (size_t)(naug * naug) * sizeof(double), "alloc inverse");
+    ck(ctx, hipMemsetAsync(fulls[j].p, 0, fulls[j].bytes, st), "memset");
+    const int64_t nblk = (naug + NB - 1) / NB;
+    for (int64_t b = R.r; b < nblk; b += m->G) {
+      const int64_t c0 = b * NB, w = std::min<int64_t>(NB, naug - c0);
+      ck(ctx, hipMemcpy2DAsync(fulls[j].d() + c0 * naug, naug * sizeof(double),
+                               R.A[0].d() + lcol(c0, m->G) * naug, naug * sizeof(double),
+                               naug * sizeof(double), (size_t)w, hipMemcpyDeviceToDevice, st),
+         "copy columns");
+    }
+  }
+  if (m->sim) {
+    for (size_t j = 1; j < fulls.size(); ++j)
+      ck(ctx, launch_add(fulls[j].d(), fulls[0].d(), naug * naug, st), "sum");
+  } else {
+    nck(ctx, rccl().AllReduce(fulls[0].p, fulls[0].p, (size_t)(naug * naug), ncclDouble, ncclSum,
+                              m->comm, st),
+        "ncclAllReduce");
+  }
+  alloc(ctx, out, (size_t)(n * n) * sizeof(double), "alloc inverse");
+  ck(ctx, launch_sym_from_lower(fulls[0].d(), naug, n, -1.0, out.d(), n, st), "symmetrize");
+  download(ctx, inv, out.d(), (size_t)(n * n), "download inverse");
+  sync(ctx);
+}
+
+void shard_collect_timing(ShardModel *m, double *t_ms, int64_t *t_launch, double *t_work) {
+  float ms = 0.f;
+  ck(m->ctx, hipEventElapsedTime(&ms, m->ev_asm[0], m->ev_asm[1]), "elapsed");
+  t_ms[1] += ms;
+  t_launch[1] += 1;
+  ck(m->ctx, hipEventElapsedTime(&ms, m->ev_grad[0], m->ev_grad[1]), "elapsed");
+  t_ms[2] += ms;
+  t_launch[2] += 1;
+  for (int j = 0; j + 1 < m->upd_used; j += 2) {
+    ck(m->ctx, hipEventElapsedTime(&ms, m->ev_upd[(size_t)j], m->ev_upd[(size_t)j + 1]),
+       "elapsed");
+    t_ms[0] += ms;
+    t_launch[0] += 1;
+    t_work[0] += m->upd_flops[(size_t)(j / 2)];
+  }
+  // pair kernels: local rank 0's share of the algorithmic flops
+  const RankState &R = *m->ranks[0];
+  const double pairs = (double)(R.ngrad - R.ndiag) * AT * AT + (double)R.ndiag * AT * (AT + 1) / 2;
+  const double B = m->s.B, p = m->s.p;
+  t_work[1] += pairs * B * (3 * p + 3);
+  t_work[2] += pairs * (4 * B * p + 2 * p) + (m->s.kind == ACE_KERNEL_MATERN32 ? pairs * B * p : 0);
+}
+
+int shard_world(const ShardModel *m) { return m->G; }
+int shard_rank(const ShardModel *m) { return m->rank; }

@@ -244,13 +244,17 @@ constexpr int GBKP = 8;            // k per LDS stage
 constexpr int GLB = NB + 16;       // pitch of the W_kk stage  [k][c]
 constexpr int GLA = SUB + 16;      // pitch of the Pn stage    [k][i]
 
+// Sharded model (G > 1): rank r forms W only for the rows it consumes -- the
+// rows of its own column blocks (operand of its update tiles) and, on the
+// owner of block k, every row >= k0 (written back into column block k).
 __global__ __launch_bounds__(512) void k_panel_gemm(double *__restrict__ W,
                                                     const double *__restrict__ Pn, int64_t ldp,
-                                                    int64_t k0) {
+                                                    int64_t k0, int G, int r) {
   __shared__ __attribute__((aligned(16))) double sB[2][GBKP][GLB];
   __shared__ __attribute__((aligned(16))) double sA[2][GBKP][GLA];
   const int64_t i0 = (int64_t)blockIdx.x * SUB;
   if (i0 >= k0 && i0 < k0 + NB) return;  // pivot rows are already final
+  if (G > 1 && !owns_col(i0, G, r) && !(owns_col(k0, G, r) && i0 >= k0)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wi = wv & 3, wc = wv >> 2;
   const int lr = lane & 15, lk = lane >> 4;
@@ -303,15 +307,18 @@ __global__ __launch_bounds__(512) void k_panel_gemm(double *__restrict__ W,
 
 // ---------------------------------------------------------------- update
 // One 128x128 lower tile (I, J) of A per 512-thread workgroup.  Tiles
-// outside block k:  A_IJ += Pn_J-rows x W_I-rows^T over the NB panel
-// columns (Pn = -P), computed as D = Pn W^T + C with the MFMA's
-// D[row=c][col=r] so that the 16 lanes of a fragment walk consecutive rows
-// of the column-major A.  8 waves, each a 64(r) x 32(c) block of 4x2
-// v_mfma_f64_16x16x4_f64 fragments: 32 accumulator doubles per lane, so
-// 4 waves fit per SIMD (61 TF/s vs 46 TF/s for 4 waves of 64x64 -- the
-// latency of the LDS fragment reads is hidden by the other waves,
-// tools/bench_update.hip).  Tiles of block k receive the swept panel W
-// (transposed for the row block).
+// outside block k:  A_IJ += R_I C_J^T over the NB panel columns, computed
+// as D = C R^T + acc with the MFMA's D[row=c][col=r] so that the 16 lanes of
+// a fragment walk consecutive rows of the column-major A.  The product is
+// -P_I D^-1 P_J^T for either operand order: single GPU R = W (swept panel,
+// every row) and C = Pn (= -P); sharded R = Pn (every rank holds the whole
+// gathered panel) and C = W (formed only for the rank's own column rows).
+// 8 waves, each a 64(r) x 32(c) block of 4x2 v_mfma_f64_16x16x4_f64
+// fragments: 32 accumulator doubles per lane, so 4 waves fit per SIMD
+// (61 TF/s vs 46 TF/s for 4 waves of 64x64 -- the latency of the LDS
+// fragment reads is hidden by the other waves, tools/bench_update.hip).
+// Tiles of block k receive the swept panel Wk (transposed for the row
+// block).  Column tile J is stored at local column lcol(J*UT, G).
 #ifndef ACE_BK
 #define ACE_BK 16
 #endif
@@ -321,69 +328,62 @@ constexpr int NCH = NB / BK;
 constexpr int UTHREADS = 512;
 static_assert(BK == 16, "staging maps 512 threads x 4 doubles onto a 128 x 16 chunk");
 
-// LOOK = true : only the "cross" tiles of block kx (tiles with I or J in
-//               block kx) -- the lookahead that the next step's panel needs;
-// LOOK = false: every lower tile except the cross of block kx (kx < 0: all).
-template <bool LOOK>
+// Every lower tile except the "cross" of block kx (tiles with I or J in
+// block kx, updated earlier by k_update_x for the lookahead; kx < 0: none).
+// tiles == nullptr: all lower tiles, 1-D grid in row-major order; otherwise
+// the rank's own tiles from the list.
 __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, int64_t ld,
-                                                        const double *__restrict__ W,
-                                                        const double *__restrict__ Pn,
-                                                        int64_t ldp, int64_t k0, int kx) {
+                                                        const double *__restrict__ Rop,
+                                                        const double *__restrict__ Cop,
+                                                        const double *__restrict__ Wk,
+                                                        int64_t ldp, int64_t k0, int kx,
+                                                        const Tile *__restrict__ tiles, int G) {
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
   constexpr int KT = NB / UT;
   int I, J;
-  if (LOOK) {
-    // grid (nT, 2*KT): y < KT -> row kx*KT+y, J = x <= I ; y >= KT -> column
-    // kx*KT+(y-KT), I = x strictly below block kx
-    const int y = blockIdx.y;
-    if (y < KT) {
-      I = kx * KT + y;
-      J = blockIdx.x;
-      if (J > I) return;
-    } else {
-      J = kx * KT + (y - KT);
-      I = blockIdx.x;
-      if (I < (kx + 1) * KT) return;
-    }
+  if (tiles) {
+    const Tile tt = tiles[blockIdx.x];
+    I = tt.I;
+    J = tt.J;
   } else {
-    // 1-D grid over the lower tiles in row-major order (no dead blocks)
     const int t = blockIdx.x;
     int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
     while ((i + 1) * (i + 2) / 2 <= t) ++i;
     while (i * (i + 1) / 2 > t) --i;
     I = i;
     J = t - i * (i + 1) / 2;
-    if (kx >= 0 && ((I >= kx * KT && I < (kx + 1) * KT) || (J >= kx * KT && J < (kx + 1) * KT)))
-      return;
   }
+  if (kx >= 0 && ((I >= kx * KT && I < (kx + 1) * KT) || (J >= kx * KT && J < (kx + 1) * KT)))
+    return;
   const int kt0 = (int)(k0 / UT), kt1 = kt0 + KT;
   const bool Ik = I >= kt0 && I < kt1, Jk = J >= kt0 && J < kt1;
   const int64_t R0 = (int64_t)I * UT, C0 = (int64_t)J * UT;
+  const int64_t L0 = lcol(C0, G);
   const int tid = threadIdx.x;
 
   if (Ik || Jk) {
     if (Ik && !Jk) {
-      // row block k, columns left of it: A[k0+a, c] = W[c, a]
+      // row block k, columns left of it: A[k0+a, c] = Wk[c, a]
       double *tileT = &sW[0][0][0];  // 64 x 65 scratch
       for (int sa = 0; sa < 2; ++sa)
         for (int sb = 0; sb < 2; ++sb) {
           __syncthreads();
           for (int e = tid; e < 4096; e += UTHREADS) {
             const int c = e & 63, a = e >> 6;
-            tileT[a * 65 + c] = W[(C0 + 64 * sb + c) + (R0 - k0 + 64 * sa + a) * ldp];
+            tileT[a * 65 + c] = Wk[(C0 + 64 * sb + c) + (R0 - k0 + 64 * sa + a) * ldp];
           }
           __syncthreads();
           for (int e = tid; e < 4096; e += UTHREADS) {
             const int a = e & 63, c = e >> 6;
-            A[(R0 + 64 * sa + a) + (C0 + 64 * sb + c) * ld] = tileT[a * 65 + c];
+            A[(R0 + 64 * sa + a) + (L0 + 64 * sb + c) * ld] = tileT[a * 65 + c];
           }
         }
     } else {
-      // column block k (and the diagonal block): A[r, k0+j] = W[r, j]
+      // column block k (and the diagonal block): A[r, k0+j] = Wk[r, j]
       for (int e = tid; e < UT * UT; e += UTHREADS) {
         const int a = e & (UT - 1), c = e >> 7;
-        A[(R0 + a) + (C0 + c) * ld] = W[(R0 + a) + (C0 - k0 + c) * ldp];
+        A[(R0 + a) + (L0 + c) * ld] = Wk[(R0 + a) + (C0 - k0 + c) * ldp];
       }
     }
     return;
@@ -398,14 +398,14 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
 #pragma unroll
     for (int ri = 0; ri < 4; ++ri) {
       const int64_t r = R0 + 64 * wr + 16 * ri + lr;
-      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+      const int64_t c = L0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[ci][ri][j] = A[r + (c + 4 * j) * ld];
     }
-  // staging: each thread moves 4 doubles of W and 4 of Pn per chunk
+  // staging: each thread moves 4 doubles of each operand per chunk
   const int sk = tid >> 5, sm = (tid & 31) * 4;
-  const double *gW = W + (R0 + sm) + (int64_t)sk * ldp;
-  const double *gP = Pn + (C0 + sm) + (int64_t)sk * ldp;
+  const double *gW = Rop + (R0 + sm) + (int64_t)sk * ldp;
+  const double *gP = Cop + (C0 + sm) + (int64_t)sk * ldp;
   double2 rw[2], rp[2];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
 #pragma unroll
     for (int ri = 0; ri < 4; ++ri) {
       const int64_t r = R0 + 64 * wr + 16 * ri + lr;
-      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+      const int64_t c = L0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
       for (int j = 0; j < 4; ++j) A[r + (c + 4 * j) * ld] = acc[ci][ri][j];
     }
@@ -464,13 +464,15 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
 // Lookahead update: only the tiles with I or J in block kx (the next panel).
 // About 2 n/128 tiles -- one workgroup per CU at 128 x 128 -- so it uses
 // 64 x 64 tiles (4 waves of 32 x 32) for 4x the workgroups; same math and
-// write-back rule as k_update.
+// write-back rule as k_update.  Sharded: rank r keeps the tiles whose
+// column block it owns.
 constexpr int XT = 64;
 constexpr int XL = XT + 8;  // LDS pitch
 __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_t ld,
-                                                  const double *__restrict__ W,
-                                                  const double *__restrict__ Pn, int64_t ldp,
-                                                  int64_t k0, int kx) {
+                                                  const double *__restrict__ Rop,
+                                                  const double *__restrict__ Cop,
+                                                  const double *__restrict__ Wk, int64_t ldp,
+                                                  int64_t k0, int kx, int G, int rank) {
   __shared__ __attribute__((aligned(16))) double sW[2][BK][XL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][XL];
   constexpr int KX = NB / XT;  // 64-tiles per block
@@ -485,26 +487,28 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
     I = blockIdx.x;
     if (I < (kx + 1) * KX) return;
   }
+  const int64_t R0 = (int64_t)I * XT, C0 = (int64_t)J * XT;
+  if (!owns_col(C0, G, rank)) return;
+  const int64_t L0 = lcol(C0, G);
   const int kt0 = (int)(k0 / XT), kt1 = kt0 + KX;
   const bool Ik = I >= kt0 && I < kt1, Jk = J >= kt0 && J < kt1;
-  const int64_t R0 = (int64_t)I * XT, C0 = (int64_t)J * XT;
   const int tid = threadIdx.x;
   if (Ik || Jk) {
     if (Ik && !Jk) {
       double *tileT = &sW[0][0][0];  // 64 x 65 scratch (fits in sW)
       for (int e = tid; e < 4096; e += 256) {
         const int c = e & 63, a = e >> 6;
-        tileT[a * 65 + c] = W[(C0 + c) + (R0 - k0 + a) * ldp];
+        tileT[a * 65 + c] = Wk[(C0 + c) + (R0 - k0 + a) * ldp];
       }
       __syncthreads();
       for (int e = tid; e < 4096; e += 256) {
         const int a = e & 63, c = e >> 6;
-        A[(R0 + a) + (C0 + c) * ld] = tileT[a * 65 + c];
+        A[(R0 + a) + (L0 + c) * ld] = tileT[a * 65 + c];
       }
     } else {
       for (int e = tid; e < XT * XT; e += 256) {
         const int a = e & (XT - 1), c = e >> 6;
-        A[(R0 + a) + (C0 + c) * ld] = W[(R0 + a) + (C0 - k0 + c) * ldp];
+        A[(R0 + a) + (L0 + c) * ld] = Wk[(R0 + a) + (C0 - k0 + c) * ldp];
       }
     }
     return;
@@ -518,14 +522,14 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
 #pragma unroll
     for (int ri = 0; ri < 2; ++ri) {
       const int64_t r = R0 + 32 * wr + 16 * ri + lr;
-      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+      const int64_t c = L0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[ci][ri][j] = A[r + (c + 4 * j) * ld];
     }
-  // staging: 256 threads x (4 doubles of W, 4 of Pn) per 64 x 16 chunk
+  // staging: 256 threads x (4 doubles of each operand) per 64 x 16 chunk
   const int sk = tid >> 4, sm = (tid & 15) * 4;
-  const double *gW = W + (R0 + sm) + (int64_t)sk * ldp;
-  const double *gP = Pn + (C0 + sm) + (int64_t)sk * ldp;
+  const double *gW = Rop + (R0 + sm) + (int64_t)sk * ldp;
+  const double *gP = Cop + (C0 + sm) + (int64_t)sk * ldp;
   double2 rw[2], rp[2];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
@@ -575,26 +579,114 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
 #pragma unroll
     for (int ri = 0; ri < 2; ++ri) {
       const int64_t r = R0 + 32 * wr + 16 * ri + lr;
-      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+      const int64_t c = L0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
       for (int j = 0; j < 4; ++j) A[r + (c + 4 * j) * ld] = acc[ci][ri][j];
     }
+}
+
+// ---------------------------------------------------------------- sharded panel
+// Packing for the panel exchange of step k (sharded model).  The owner of
+// block k sends rows [k0, naug) of its column block (contiguous, ld naug-k0)
+// by broadcast; every rank sends the NB x NB pieces A[k-block, j-block] of
+// its own blocks j < k (slot q = j / G) by all-gather.
+__global__ __launch_bounds__(256) void k_pack_lower(const double *__restrict__ A, int64_t ld,
+                                                    int G, int64_t k0, int64_t naug,
+                                                    double *__restrict__ low) {
+  const int64_t i0 = k0 + (int64_t)blockIdx.x * 64;
+  const int j0 = blockIdx.y * 64;
+  const int64_t L = lcol(k0, G);
+  const int64_t h = naug - k0;
+  if (i0 >= k0 + NB || i0 >= k0 + j0 + 64) {  // entirely on / below the diagonal
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+      const int a = e & 63, b = e >> 6;
+      low[(i0 - k0 + a) + (int64_t)(j0 + b) * h] = A[(i0 + a) + (L + j0 + b) * ld];
+    }
+  } else {
+    // pivot block: only its lower triangle is stored, mirror the rest
+    // (both indices lie in block k, so the column map is L + offset)
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+      const int a = e & 63, b = e >> 6;
+      const int ia = (int)(i0 - k0) + a, cb = j0 + b;
+      low[ia + (int64_t)cb * h] =
+          ia >= cb ? A[(k0 + ia) + (L + cb) * ld] : A[(k0 + cb) + (L + ia) * ld];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pack_rows(const double *__restrict__ A, int64_t ld,
+                                                   int64_t k0, double *__restrict__ send) {
+  const int q = blockIdx.z;  // local block q = global block r + q G (< k)
+  const int a0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  double *dst = send + (int64_t)q * NB * NB;
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    const int a = e & 63, c = e >> 6;
+    dst[(a0 + a) + (c0 + c) * NB] = A[(k0 + a0 + a) + ((int64_t)q * NB + c0 + c) * ld];
+  }
+}
+
+// Rebuilds panel k on every rank: Pn = -P for every row, W = P on the pivot
+// rows, S0 = pivot rows of sub-block 0 (k_pivot's input).  Rows >= k0 come
+// from the broadcast block, rows i < k0 (block j = i / NB) from all-gather
+// slot (j % G, j / G), transposed: P[i, c] = A[k0 + c, i].
+__global__ __launch_bounds__(256) void k_unpack_panel(const double *__restrict__ low,
+                                                      const double *__restrict__ recv, int m,
+                                                      int G, int64_t k0, int64_t naug,
+                                                      double *__restrict__ Pn,
+                                                      double *__restrict__ W, int64_t ldp,
+                                                      double *__restrict__ S0) {
+  __shared__ double tile[64][65];
+  const int64_t i0 = (int64_t)blockIdx.x * 64;
+  const int j0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+  if (i0 >= k0) {
+    const int64_t h = naug - k0;
+    for (int e = tid; e < 4096; e += 256) {
+      const int a = e & 63, b = e >> 6;
+      const double v = low[(i0 - k0 + a) + (int64_t)(j0 + b) * h];
+      Pn[(i0 + a) + (int64_t)(j0 + b) * ldp] = -v;
+      if (i0 < k0 + NB) W[(i0 + a) + (int64_t)(j0 + b) * ldp] = v;
+      if (i0 == k0) S0[a + (int64_t)(j0 + b) * SUB] = v;
+    }
+  } else {
+    const int64_t j = i0 / NB;
+    const int rr0 = (int)(i0 % NB);
+    const double *src = recv + ((j % G) * (int64_t)m + j / G) * NB * NB;
+    for (int e = tid; e < 4096; e += 256) {
+      const int b = e & 63, a = e >> 6;  // b: panel column (contiguous in src)
+      tile[a][b] = src[(j0 + b) + (int64_t)(rr0 + a) * NB];
+    }
+    __syncthreads();
+    for (int e = tid; e < 4096; e += 256) {
+      const int a = e & 63, b = e >> 6;
+      Pn[(i0 + a) + (int64_t)(j0 + b) * ldp] = -tile[a][b];
+    }
+  }
+}
+
+// Pivot block sweep (4 x 64-column sub-sweeps, pivots -> piv / flag) and the
+// panel GEMM for the rows rank r consumes.  W's pivot rows and S[0] must
+// hold the panel's pivot rows.
+static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, double *SW,
+                        double *const S[2], double *piv, int *flag, int G, int r,
+                        hipStream_t st) {
+  for (int s = 0; s < NB / SUB; ++s) {
+    hipLaunchKernelGGL(k_pivot, dim3(1), dim3(256), 0, st, S[s & 1], s, SW, piv,
+                       k0 + (int64_t)s * SUB, flag);
+    hipLaunchKernelGGL(k_panel, dim3(NB / SUB), dim3(256), 0, st, W, ld, k0, s, SW, S[s & 1],
+                       S[(s + 1) & 1], k0);
+  }
+  hipLaunchKernelGGL(k_panel_gemm, dim3((unsigned)(ld / SUB)), dim3(512), 0, st, W, Pn, ld, k0,
+                     G, r);
 }
 
 static hipError_t panel_sweep(const SweepBufs &b, int buf, int64_t k0, hipStream_t st) {
   const int64_t naug = b.ld;
   hipLaunchKernelGGL(k_gather, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st, b.A, b.ld,
                      k0, b.P[buf], b.W[buf], b.ld, b.S[0]);
-  // sweep the NB x NB pivot block in place (4 workgroups per sub-step)
-  for (int s = 0; s < NB / SUB; ++s) {
-    hipLaunchKernelGGL(k_pivot, dim3(1), dim3(256), 0, st, b.S[s & 1], s, b.SW, b.piv,
-                       k0 + (int64_t)s * SUB, b.flag);
-    hipLaunchKernelGGL(k_panel, dim3(NB / SUB), dim3(256), 0, st, b.W[buf], b.ld, k0, s, b.SW,
-                       b.S[s & 1], b.S[(s + 1) & 1], k0);
-  }
-  // every other panel row: W_i = Pn_i W_kk
-  hipLaunchKernelGGL(k_panel_gemm, dim3((unsigned)(naug / SUB)), dim3(512), 0, st, b.W[buf],
-                     b.P[buf], b.ld, k0);
+  // sweep the NB x NB pivot block in place, then every other panel row:
+  // W_i = Pn_i W_kk
+  panel_chain(b.P[buf], b.W[buf], b.ld, k0, b.SW, b.S, b.piv, b.flag, 1, 0, st);
   return hipGetLastError();
 }
 
@@ -646,7 +738,7 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
     }
     if (more) {
       hipLaunchKernelGGL(k_update_x, dim3((unsigned)(naug / XT), 2 * (NB / XT)), dim3(256), 0, st,
-                         b.A, b.ld, b.W[buf], b.P[buf], b.ld, k0, k + 1);
+                         b.A, b.ld, b.W[buf], b.P[buf], b.W[buf], b.ld, k0, k + 1, 1, 0);
       if (two) {
         e = hipEventRecord(sy->ev[2 * k + 1], st);  // cross of block k+1 updated
         if (e != hipSuccess) return e;
@@ -662,8 +754,9 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
     }
     const bool timed = tm && tm->ev && used + 2 <= tm->nev;
     if (timed) (void)hipEventRecord(tm->ev[used], st);
-    hipLaunchKernelGGL(k_update<false>, dim3(nT * (nT + 1) / 2), dim3(UTHREADS), 0, st, b.A, b.ld,
-                       b.W[buf], b.P[buf], b.ld, k0, more ? k + 1 : -1);
+    hipLaunchKernelGGL(k_update, dim3(nT * (nT + 1) / 2), dim3(UTHREADS), 0, st, b.A, b.ld,
+                       b.W[buf], b.P[buf], b.W[buf], b.ld, k0, more ? k + 1 : -1,
+                       (const Tile *)nullptr, 1);
     if (timed) {
       (void)hipEventRecord(tm->ev[used + 1], st);
       if (tm->flops) tm->flops[used / 2] =
@@ -675,6 +768,45 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
   }
   if (tm && tm->used) *tm->used = used;
   return hipSuccess;
+}
+
+// ---- sharded step pieces (driven by ace_shard.cpp) --------------------------
+int shard_row_slots(int k, int G) { return (k + G - 1) / G; }
+
+hipError_t shard_pack(const ShardSweep &b, int k, hipStream_t st) {
+  const int64_t k0 = (int64_t)k * NB, naug = b.ld;
+  if (k % b.G == b.r)
+    hipLaunchKernelGGL(k_pack_lower, dim3((unsigned)((naug - k0) / 64), NB / 64), dim3(256), 0,
+                       st, b.A, b.ld, b.G, k0, naug, b.low);
+  const int own = k > b.r ? (k - b.r + b.G - 1) / b.G : 0;  // own blocks j < k
+  if (own > 0)
+    hipLaunchKernelGGL(k_pack_rows, dim3(NB / 64, NB / 64, (unsigned)own), dim3(256), 0, st, b.A,
+                       b.ld, k0, b.send);
+  return hipGetLastError();
+}
+
+hipError_t shard_unpack_chain(const ShardSweep &b, int k, int buf, hipStream_t st) {
+  const int64_t k0 = (int64_t)k * NB, naug = b.ld;
+  hipLaunchKernelGGL(k_unpack_panel, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st,
+                     b.low, b.recv, shard_row_slots(k, b.G), b.G, k0, naug, b.P[buf], b.W[buf],
+                     b.ld, b.S[0]);
+  panel_chain(b.P[buf], b.W[buf], b.ld, k0, b.SW, b.S, b.piv, b.flag, b.G, b.r, st);
+  return hipGetLastError();
+}
+
+hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t st) {
+  const int64_t naug = b.ld;
+  hipLaunchKernelGGL(k_update_x, dim3((unsigned)(naug / XT), 2 * (NB / XT)), dim3(256), 0, st,
+                     b.A, b.ld, b.P[buf], b.W[buf], b.W[buf], b.ld, (int64_t)k * NB, k + 1, b.G,
+                     b.r);
+  return hipGetLastError();
+}
+
+hipError_t shard_update_main(const ShardSweep &b, int k, int buf, int kx, hipStream_t st) {
+  if (b.ntiles > 0)
+    hipLaunchKernelGGL(k_update, dim3((unsigned)b.ntiles), dim3(UTHREADS), 0, st, b.A, b.ld,
+                       b.P[buf], b.W[buf], b.W[buf], b.ld, (int64_t)k * NB, kx, b.tiles, b.G);
+  return hipGetLastError();
 }
 
 }  // namespace ace

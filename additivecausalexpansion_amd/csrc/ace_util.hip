@@ -27,20 +27,89 @@ __device__ __forceinline__ double block_sum256(double v, double *sh) {
 // ---------------------------------------------------------------- AUG rows
 // rows npad .. npad+AUG-1 of A: row 0 = y (j < n), row 1 = 1 (j < n), 0 else
 __global__ void k_aug_init(double *__restrict__ A, int64_t ld, int64_t npad, int64_t n,
-                           const double *__restrict__ y) {
-  const int64_t j = blockIdx.x;  // column
+                           const double *__restrict__ y, int G, int rank) {
+  const int64_t j = blockIdx.x;  // global column
+  if (!owns_col(j, G, rank)) return;
   const int t = threadIdx.x;     // AUG rows
   double v = 0.0;
   if (j < n) {
     if (t == 0) v = y[j];
     else if (t == 1) v = 1.0;
   }
-  A[(npad + t) + j * ld] = v;
+  A[(npad + t) + lcol(j, G) * ld] = v;
 }
 
 hipError_t launch_aug_init(double *A, int64_t ld, int64_t npad, int64_t n, const double *y,
-                           hipStream_t st) {
-  hipLaunchKernelGGL(k_aug_init, dim3((unsigned)ld), dim3(AUG), 0, st, A, ld, npad, n, y);
+                           hipStream_t st, int G, int rank) {
+  hipLaunchKernelGGL(k_aug_init, dim3((unsigned)ld), dim3(AUG), 0, st, A, ld, npad, n, y, G,
+                     rank);
+  return hipGetLastError();
+}
+
+// Sharded model: the swept AUG rows of the rank's own columns into
+// vec = [u (npad) | v (npad) | yKy, yK1, 1K1], zero elsewhere, so that a
+// sum over ranks (all-reduce) yields the whole vectors on every rank.
+__global__ void k_aug_extract(const double *__restrict__ A, int64_t ld, int64_t npad, int G,
+                              int rank, double *__restrict__ vec) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < npad) {
+    const bool own = owns_col(j, G, rank);
+    const int64_t l = lcol(j, G);
+    vec[j] = own ? A[npad + l * ld] : 0.0;
+    vec[npad + j] = own ? A[(npad + 1) + l * ld] : 0.0;
+  }
+  if (j == 0) {
+    const bool own = owns_col(npad, G, rank);
+    const int64_t l = lcol(npad, G);
+    vec[2 * npad + 0] = own ? -A[npad + l * ld] : 0.0;
+    vec[2 * npad + 1] = own ? -A[(npad + 1) + l * ld] : 0.0;
+    vec[2 * npad + 2] = own ? -A[(npad + 1) + (l + 1) * ld] : 0.0;
+  }
+}
+
+hipError_t launch_aug_extract(const double *A, int64_t ld, int64_t npad, int G, int rank,
+                              double *vec, hipStream_t st) {
+  hipLaunchKernelGGL(k_aug_extract, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, st, A,
+                     ld, npad, G, rank, vec);
+  return hipGetLastError();
+}
+
+// alpha / scal from the all-reduced aug vector (same formulas as
+// k_alpha_from_aug).
+__global__ void k_alpha_from_vec(const double *__restrict__ vec, int64_t npad, int64_t n,
+                                 double theta1, int use_mu, double *__restrict__ alpha,
+                                 double *__restrict__ scal) {
+  const double yKy = vec[2 * npad], yK1 = vec[2 * npad + 1], oK1 = vec[2 * npad + 2];
+  const double mu = 0.5 * yK1 / oK1;  // Q4 (src/utilities_cpp.cpp:9)
+  const double mu_eff = use_mu ? mu : theta1;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) alpha[j] = vec[j] - mu_eff * vec[npad + j];
+  if (j == 0) {
+    scal[0] = yKy;
+    scal[1] = yK1;
+    scal[2] = oK1;
+    scal[3] = mu;
+    scal[4] = mu_eff;
+  }
+}
+
+hipError_t launch_alpha_from_vec(const double *vec, int64_t npad, int64_t n, double theta1,
+                                 int use_mu, double *alpha, double *scal, hipStream_t st) {
+  hipLaunchKernelGGL(k_alpha_from_vec, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, vec,
+                     npad, n, theta1, use_mu, alpha, scal);
+  return hipGetLastError();
+}
+
+// y += x (in-process all-reduce of the simulated rank group)
+__global__ void k_axpy1(const double *__restrict__ x, double *__restrict__ y, int64_t count) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < count) y[j] += x[j];
+}
+
+hipError_t launch_add(const double *x, double *y, int64_t count, hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_axpy1, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, x, y,
+                     count);
   return hipGetLastError();
 }
 

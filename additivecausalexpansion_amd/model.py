@@ -15,19 +15,33 @@ import ctypes
 import numpy as np
 
 from . import native
-from ._lib import KIND, AceError, check, default_context, fmat, lib, ptr
+from ._lib import KIND, UNIQUE_ID_BYTES, AceError, check, default_context, fmat, lib, ptr
 
 
 class DeviceModel:
     """ace_model handle: one fit's resident data and the last inverse."""
 
-    def __init__(self, kind, n, p, B, ctx=None):
+    def __init__(self, kind, n, p, B, ctx=None, world=1, rank=0, unique_id=None,
+                 sharded=False):
+        """sharded=False: one GPU (ace_model_create).  sharded=True: rank
+        `rank` of a `world`-rank block-column-sharded model
+        (ace_model_create_sharded): unique_id = the 128 bytes rank 0 got from
+        comm_unique_id() (RCCL, one process per GPU), or None to simulate all
+        ranks in this process (validation mode)."""
         self.ctx = ctx or default_context()
         self.kind, self.n, self.p, self.B = kind, n, p, B
         self.P = 2 + B * (p + 1)
+        self.world, self.rank = (world, rank) if sharded else (1, 0)
         h = ctypes.c_void_p()
-        check(lib().ace_model_create(self.ctx.handle, KIND[kind], n, p, B, ctypes.byref(h)),
-              self.ctx.handle)
+        if sharded:
+            if unique_id is not None and len(unique_id) != UNIQUE_ID_BYTES:
+                raise ValueError("unique_id must be 128 bytes")
+            check(lib().ace_model_create_sharded(self.ctx.handle, KIND[kind], n, p, B, int(world),
+                                                 int(rank), unique_id, ctypes.byref(h)),
+                  self.ctx.handle)
+        else:
+            check(lib().ace_model_create(self.ctx.handle, KIND[kind], n, p, B, ctypes.byref(h)),
+                  self.ctx.handle)
         self.handle = h
 
     def set_data(self, y, X, Z, std_y):
@@ -80,6 +94,14 @@ class DeviceModel:
             self.close()
         except Exception:
             pass
+
+
+def comm_unique_id():
+    """ace_comm_unique_id: the RCCL bootstrap id (rank 0 calls it and sends
+    the bytes to every rank out of band)."""
+    buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    check(lib().ace_comm_unique_id(buf), None)
+    return buf.raw
 
 
 class _KernelClass:

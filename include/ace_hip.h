@@ -196,6 +196,35 @@ int ace_model_profile(ace_model *m, int enable);
 int ace_model_kernel_time(ace_model *m, int which, double *ms,
                           int64_t *launches, double *work);
 
+/* ------------------------------- multi-GPU: block-column-sharded model
+ *
+ * For n beyond what one evaluation should spend on one GPU (SURVEY.md §8e,
+ * configs C3/C4).  The reference has no multi-process path (one R process,
+ * BLAS threads only); this is the scale-out of the same para_update.
+ * A is distributed by NB = 256-wide column blocks, block-cyclic over the
+ * `world` ranks (block j on rank j % world), one process per GPU.  Each
+ * sweep step broadcasts the pivot block's column panel from its owner and
+ * all-gathers the panel's row pieces (RCCL over xGMI); assembly, update,
+ * gradient and Kfull*alpha work only on the rank's own columns; one
+ * all-reduce per evaluation combines alpha, the gradient partial sums and
+ * Kfull*alpha.  Every rank returns identical grad / stats.
+ *
+ * Bootstrap: rank 0 calls ace_comm_unique_id() and sends the 128 bytes to
+ * every rank out of band (MPI, torch.distributed, a file); each rank then
+ * calls ace_model_create_sharded() with the same id (blocks until all
+ * `world` ranks have joined).  With id == NULL all `world` ranks are
+ * simulated inside this process on ctx's device and the exchanges are
+ * device copies: the validation mode the single-GPU tests use.
+ * The returned model takes every ace_model_* call above; calls are
+ * collective (every rank makes the same sequence of calls). */
+#define ACE_UNIQUE_ID_BYTES 128
+int ace_comm_unique_id(unsigned char *id);
+int ace_model_create_sharded(ace_ctx *ctx, int kind, int64_t n, int p, int B,
+                             int world, int rank, const unsigned char *id,
+                             ace_model **out);
+/* world / rank of a model (1 / 0 for ace_model_create models) */
+int ace_model_shard_info(const ace_model *m, int *world, int *rank);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,142 @@
+"""GPU parity tests of the block-column-sharded model through
+the C ABI (ace_model_create_sharded).
+
+On one GPU the G ranks are simulated inside the process (unique_id=None):
+every rank has its own local column blocks, panel buffers and tile lists,
+and the broadcast / all-gather / all-reduce are device copies with the
+RCCL semantics, so the packing, ownership maps and redundant pivot chains
+are the ones the multi-process run uses.  A world-size-1 RCCL communicator
+runs the real RCCL code path (dlopen, ncclCommInitRank, grouped broadcast +
+all-gather, all-reduce) on the single card.
+
+Tolerances as in test_gpu.py: gradients / stats 1e-6 relative (north star),
+inverse 1e-9 of its scale."""
+import numpy as np
+import pytest
+from test_gpu import close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def A():
+    import additivecausalexpansion_amd as pkg
+    pkg.default_context()
+    return pkg
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import ace_oracle
+    return ace_oracle
+
+
+def _oracle_eval(O, kernel, y, X, Z, th, sy, B, it):
+    sym, _, grad = O.KERNELS[kernel]
+    t = th.copy()
+    Kl = sym(X, Z, t)
+    inv = O.invkernel_cpp(Kl["full"], t[0])
+    if it == 1:
+        t[1] = O.mu_solution_cpp(y, inv["inv"])
+    st = np.zeros(2)
+    g = grad(y, X, Z, Kl["full"], Kl["elements"], inv["inv"], inv["eigenval"], t, st, B, sy)
+    return t, g, st, inv
+
+
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+@pytest.mark.parametrize("world,n,p,B", [(2, 300, 2, 5), (3, 700, 3, 4), (4, 1000, 20, 10),
+                                          (8, 1100, 5, 3), (5, 130, 1, 2)])
+def test_sharded_sim_matches_oracle(A, O, kernel, world, n, p, B):
+    """world simulated ranks; n not a multiple of 256, ranks owning no pivot
+    block (world 8 / 5 at small n), both kernels, iter 1 (mu first) and 2."""
+    from additivecausalexpansion_amd.synthetic import make_problem
+    y, X, Z, th, sy = make_problem(n, p, B, seed=11)
+    m = A.DeviceModel(kernel, n, p, B, world=world, rank=0, sharded=True)
+    m.set_data(y, X, Z, sy)
+    for it in (1, 2):
+        t_dev = th.copy()
+        g, st, mu_post = m.para_update(it, t_dev)
+        t_ref, g_ref, st_ref, inv = _oracle_eval(O, kernel, y, X, Z, th, sy, B, it)
+        # mu = 0.5 yK1 / 1K1 (Q4) cancels; y is standardised, so 1e-9 absolute
+        assert t_dev[1] == pytest.approx(t_ref[1], rel=1e-6, abs=1e-9)
+        close(g, g_ref)
+        close(st, st_ref)
+        assert mu_post == pytest.approx(O.mu_solution_cpp(y, inv["inv"]), rel=1e-6, abs=1e-9)
+        if it == 1:
+            close(m.inverse(), inv["inv"], 1e-9, 1e-9)
+        th = th + 0.01
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_sharded_sim_matches_single_gpu(A, world):
+    """Sharded and single-GPU models agree to rounding at a size with 8 pivot
+    blocks (several lookahead steps, every rank owning several blocks)."""
+    from additivecausalexpansion_amd.synthetic import make_problem
+    n, p, B = 2000, 6, 5
+    y, X, Z, th, sy = make_problem(n, p, B, seed=5)
+    single = A.DeviceModel("Matern32", n, p, B)
+    single.set_data(y, X, Z, sy)
+    sh = A.DeviceModel("Matern32", n, p, B, world=world, sharded=True)
+    sh.set_data(y, X, Z, sy)
+    g1, s1, m1 = single.para_update(2, th.copy())
+    g2, s2, m2 = sh.para_update(2, th.copy())
+    close(g2, g1, 1e-9, 1e-11)
+    close(s2, s1, 1e-10, 0)
+    assert m2 == pytest.approx(m1, rel=1e-9)
+    close(sh.inverse(), single.inverse(), 1e-9, 1e-10)  # operand order differs: rounding
+
+
+def test_sharded_train_stats_keeps_inverse(A, O):
+    from additivecausalexpansion_amd.synthetic import make_problem
+    n, p, B = 600, 3, 4
+    y, X, Z, th, sy = make_problem(n, p, B, seed=3)
+    m = A.DeviceModel("SE", n, p, B, world=3, sharded=True)
+    m.set_data(y, X, Z, sy)
+    m.para_update(2, th.copy())
+    inv1 = m.inverse()
+    th2 = th + 0.05
+    st = m.train_stats(th2)
+    K = O.kernmat_SE_symmetric_cpp(X, Z, th2)["full"]
+    inv = O.invkernel_cpp(K, th2[0])
+    close(st, O.stats_cpp(y, K, inv["inv"], inv["eigenval"], th2[1], sy))
+    assert np.array_equal(m.inverse(), inv1)  # Q6
+
+
+def test_sharded_rccl_world1_matches_oracle(A, O):
+    """A real RCCL communicator (world size 1): the multi-process code path --
+    RCCL loaded by dlopen, grouped broadcast + all-gather per step,
+    all-reduces -- on one card."""
+    from additivecausalexpansion_amd.synthetic import make_problem
+    uid = A.comm_unique_id()
+    assert len(uid) == 128
+    n, p, B = 900, 4, 4
+    y, X, Z, th, sy = make_problem(n, p, B, seed=9)
+    m = A.DeviceModel("Matern32", n, p, B, world=1, rank=0, unique_id=uid, sharded=True)
+    m.set_data(y, X, Z, sy)
+    g, st, _ = m.para_update(1, th.copy())
+    _, g_ref, st_ref, inv = _oracle_eval(O, "Matern32", y, X, Z, th, sy, B, 1)
+    close(g, g_ref)
+    close(st, st_ref)
+    close(m.inverse(), inv["inv"], 1e-9, 1e-9)
+
+
+def test_sharded_large_residual(A):
+    """n = 6000 over 4 simulated ranks: ||A A^-1 - I|| and the log-det through
+    the stats, vs the single-GPU model (size-independent properties)."""
+    from additivecausalexpansion_amd.synthetic import make_problem
+    n, p, B = 6000, 8, 6
+    y, X, Z, th, sy = make_problem(n, p, B, seed=21)
+    sh = A.DeviceModel("SE", n, p, B, world=4, sharded=True)
+    sh.set_data(y, X, Z, sy)
+    single = A.DeviceModel("SE", n, p, B)
+    single.set_data(y, X, Z, sy)
+    g2, s2, _ = sh.para_update(2, th.copy())
+    g1, s1, _ = single.para_update(2, th.copy())
+    close(g2, g1, 1e-8, 1e-10)
+    close(s2, s1, 1e-9, 0)
+    inv = sh.inverse()
+    K = A.kernmat_SE_symmetric_cpp(X, Z, th)["full"]
+    K[np.diag_indices(n)] += np.exp(th[0])
+    R = K @ inv
+    R[np.diag_indices(n)] -= 1.0
+    assert np.abs(R).max() < 1e-7
