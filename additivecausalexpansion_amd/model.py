@@ -186,6 +186,14 @@ class _KernelClass:
             self._data_id = key
         return self._model
 
+    def use_model(self, model, y, X, Z):
+        """Attach an already-created DeviceModel (e.g. a sharded one) holding
+        y, X, Z; para_update then runs on it."""
+        model.set_data(y, X, Z, self.stdy)
+        self._model = model
+        self._data_id = (id(y), id(X), id(Z))
+        return model
+
     def para_update(self, iter, y, X, Z, Optim, printevery=100, verbose=True):  # noqa: A002
         """R/kernel_SE_R6.R:40-62 (R/kernel_Matern32_R6.R:142-163)."""
         model = self._ensure_model(y, X, Z)

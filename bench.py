@@ -10,11 +10,23 @@ gradient and both statistics; the host then takes the Nadam step with
 norm clipping and the mu overwrite, exactly like the R6 class.  Inputs are
 resident in HBM before the timed region.
 
-Multi-GPU (torchrun, one process per GPU): round 1 runs independent replicas
-(DESIGN.md §5): every rank fits its own C2 problem on its own GPU, so per-GPU
-work is fixed ("weak") and value = all ranks' evals / max-over-ranks time.
+Multi-GPU (torchrun, one process per GPU):
+  * headline `value`: independent C2 replicas, one per GPU (per-GPU work
+    fixed, "weak"): value = all ranks' evals / max-over-ranks time.  One C2
+    evaluation fits a GPU, so replicas are the highest-throughput way to
+    spend N GPUs on the n=16384 metric.
+  * `sharded` leg (N > 1, after the replicas): ONE evaluation spread over
+    all N GPUs -- A block-column-sharded, RCCL panel broadcast + all-gather
+    per sweep step -- on the BASELINE config for that GPU
+    count (C3 n=32768 at 4, C4 n=65536 at 8, C2-shaped n = 16384 N^(1/3)
+    otherwise), with the weak-scaling efficiency of SURVEY §8d,
+    E(N) = [n_N^3 / t_N / N] / [16384^3 / t_1], t_1 = this run's C2 step.
+    A watchdog bounds it; the headline line is printed regardless.
+  * `--mode sharded`: the sharded leg alone (also at N = 1, where it runs the
+    RCCL code path with one rank).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
+                       [--mode auto|replicas|sharded] [--shard-config C4]
 """
 from __future__ import annotations
 
@@ -23,6 +35,7 @@ import json
 import os
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -33,14 +46,17 @@ METRIC = "log-marg-lik+grad evals/sec at n=16384,d=20; Cholesky GF/s vs MFMA pea
 # MI355X_MICROARCH.md lists no fp64 row, so the spec value is used).
 FP64_MFMA_PEAK_TFLOPS = 78.6
 HBM_PEAK_GBS = 8000.0
+N1 = 16384  # C2
 
 
 def _dist_init():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world == 1:
+    if world == 1 and "RANK" not in os.environ:
         return None, rank, world, local
+    # torch first: its HIP runtime / RCCL are then the process-wide ones and
+    # libace_hip.so binds to them by soname
     import torch
     import torch.distributed as dist
     backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -68,7 +84,7 @@ def _allreduce_max(dist, x):
     return float(t.item())
 
 
-def pmc_traffic(kernel="k_update<false>"):
+def pmc_traffic(kernel="k_update"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/rNN_pmc_traffic.json, written by tools/pmc_traffic.py from two
     separate rocprofv3 --pmc passes of this bench).  None if absent."""
@@ -78,7 +94,9 @@ def pmc_traffic(kernel="k_update<false>"):
         return None, None
     try:
         d = json.load(open(files[-1]))
-        return d["kernels"][kernel]["traffic"], os.path.relpath(files[-1], ROOT)
+        ks = d["kernels"]
+        name = next((k for k in ks if k == kernel or k.startswith(kernel + "<")), None)
+        return (ks[name]["traffic"] if name else None), os.path.relpath(files[-1], ROOT)
     except (KeyError, ValueError, OSError):
         return None, None
 
@@ -98,48 +116,128 @@ def cpu_baseline(cfg, timeout=240):
                 "sample": f"failed: {type(e).__name__}: {e}"[:300]}
 
 
+def shard_config(world, name=None):
+    """(label, n, p, B, kernel) of the sharded leg for `world` GPUs."""
+    from additivecausalexpansion_amd.synthetic import CONFIGS
+    if name:
+        return (name,) + tuple(CONFIGS[name])
+    if world == 8:
+        return ("C4",) + tuple(CONFIGS["C4"])
+    if world == 4:
+        return ("C3",) + tuple(CONFIGS["C3"])
+    if world == 1:
+        return ("C2",) + tuple(CONFIGS["C2"])
+    n = int(round(N1 * world ** (1.0 / 3.0) / 256.0)) * 256
+    return (f"C2-shape n={n}", n, 20, 10, "Matern32")
+
+
+def make_step(kernel, p, B, theta, std_y, ctx, y, X, Z, model=None):
+    import additivecausalexpansion_amd as ace
+    Kc = ace.KernelClass_Matern32_R6 if kernel == "Matern32" else ace.KernelClass_SE_R6
+    k = Kc(p, B, theta, std_y, ctx=ctx)
+    opt = ace.set_optimizer("Nadam", k, 0.01, 0.0, 0.9, 0.999, True, 1.0)
+    if model is None:
+        model = k._ensure_model(y, X, Z)  # uploads X, Z, y once (resident in HBM)
+    else:
+        k.use_model(model, y, X, Z)
+    state = {"it": 0}
+
+    def step():
+        state["it"] += 1
+        return k.para_update(state["it"], y, X, Z, opt, verbose=False)
+    return step, model
+
+
+def timed_steps(dist, step, steps, warmup, model):
+    for _ in range(warmup):
+        step()
+    model.profile(True)
+    _barrier_sync(dist)
+    t0 = time.perf_counter()
+    stats = None
+    for _ in range(steps):
+        stats = step()
+    _barrier_sync(dist)
+    dt = time.perf_counter() - t0
+    return _allreduce_max(dist, dt), stats
+
+
+def run_sharded(dist, rank, world, ctx, steps, warmup, name=None):
+    """One evaluation over all ranks (block-column-sharded model, RCCL)."""
+    import additivecausalexpansion_amd as ace
+    from additivecausalexpansion_amd.synthetic import make_problem
+    label, n, p, B, kernel = shard_config(world, name)
+    uid = ace.comm_unique_id() if rank == 0 else None
+    if dist is not None:
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    y, X, Z, theta, std_y = make_problem(n, p, B, seed=2000)  # same data on every rank
+    model = ace.DeviceModel(kernel, n, p, B, ctx=ctx, world=world, rank=rank, unique_id=uid,
+                            sharded=True)
+    step, model = make_step(kernel, p, B, theta, std_y, ctx, y, X, Z, model=model)
+    dt, stats = timed_steps(dist, step, steps, warmup, model)
+    upd_ms, upd_n, upd_work = model.kernel_time(0)
+    model.profile(False)
+    ms = dt / steps * 1e3
+    out = {
+        "config": label, "n": n, "p": p, "B": B, "kernel": kernel, "n_gpus": world,
+        "parallelism": f"block-column shard x{world} (NB=256 cyclic), RCCL bcast+allgather/step",
+        "steps": steps, "warmup": warmup, "ms_per_step": ms, "evals_per_s": 1e3 / ms,
+        "dense_tflops_total": n ** 3 / (ms * 1e-3) / 1e12,
+        "dense_tflops_per_gpu": n ** 3 / (ms * 1e-3) / 1e12 / world,
+        "rank0_update_kernel_tflops": (upd_work / (upd_ms * 1e-3) / 1e12) if upd_ms else None,
+        "last_stats": [float(stats[0]), float(stats[1])] if stats is not None else None,
+    }
+    model.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2")
+    ap.add_argument("--mode", default="auto", choices=["auto", "replicas", "sharded"])
+    ap.add_argument("--shard-config", default=None)
+    ap.add_argument("--shard-steps", type=int, default=2)
+    ap.add_argument("--shard-timeout", type=float, default=240.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
 
     dist, rank, world, local = _dist_init()
-    import numpy as np
-
     import additivecausalexpansion_amd as ace
     from additivecausalexpansion_amd.synthetic import CONFIGS, make_problem
+    ctx = ace.Context(local)
+
+    if a.mode == "sharded":
+        sh = run_sharded(dist, rank, world, ctx, a.steps, a.warmup, a.shard_config)
+        if rank == 0:
+            line = {"metric": METRIC, "value": sh["evals_per_s"], "unit": "evals/s",
+                    "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                    "ms_per_step": sh["ms_per_step"], "higher_is_better": True,
+                    "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                    "data": "synthetic (seeded SURVEY.md §8d generator)",
+                    "config": {"workload": f"{sh['config']} sharded para_update",
+                               **{k: sh[k] for k in ("n", "p", "B", "kernel", "parallelism")}},
+                    "sharded": sh}
+            print(json.dumps(line), flush=True)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     n, p, B, kernel = CONFIGS[a.config]
     y, X, Z, theta, std_y = make_problem(n, p, B, seed=1000 + rank)
-    ctx = ace.Context(local)
-    Kc = ace.KernelClass_Matern32_R6 if kernel == "Matern32" else ace.KernelClass_SE_R6
-    k = Kc(p, B, theta, std_y, ctx=ctx)
-    opt = ace.set_optimizer("Nadam", k, 0.01, 0.0, 0.9, 0.999, True, 1.0)
-    model = k._ensure_model(y, X, Z)  # uploads X, Z, y once (resident in HBM)
-
-    it = 0
-    for _ in range(a.warmup):
-        it += 1
-        k.para_update(it, y, X, Z, opt, verbose=False)
-
-    model.profile(True)
-    _barrier_sync(dist)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        it += 1
-        stats = k.para_update(it, y, X, Z, opt, verbose=False)
-    _barrier_sync(dist)
-    dt = time.perf_counter() - t0
-    dt_max = _allreduce_max(dist, dt)
+    step, model = make_step(kernel, p, B, theta, std_y, ctx, y, X, Z)
+    dt_max, stats = timed_steps(dist, step, a.steps, a.warmup, model)
     upd_ms, upd_n, upd_work = model.kernel_time(0)
     asm_ms, _, asm_work = model.kernel_time(1)
     grad_ms, _, grad_work = model.kernel_time(2)
     model.profile(False)
 
+    line = None
     if rank == 0:
         traffic, traffic_src = pmc_traffic()
         evals = a.steps * world
@@ -190,7 +288,35 @@ def main():
         }
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(a.config)
+
+    failed = False
+    if world > 1 and a.mode == "auto":
+        model.close()
+
+        def watchdog():  # a hung collective must not cost the headline line
+            if line is not None:
+                line["sharded"] = {"error": f"timed out after {a.shard_timeout:.0f} s"}
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+        timer = threading.Timer(a.shard_timeout, watchdog)
+        timer.daemon = True
+        timer.start()
+        try:
+            sh = run_sharded(dist, rank, world, ctx, a.shard_steps, 1)
+            t1 = dt_max / a.steps
+            sh["weak_scaling_efficiency"] = (sh["n"] ** 3 / (sh["ms_per_step"] * 1e-3) / world) / (
+                n ** 3 / t1) if a.config == "C2" else None
+        except Exception as e:  # reported, never fatal for the headline
+            sh = {"error": f"{type(e).__name__}: {e}"[:300]}
+            failed = True
+        timer.cancel()
+        if line is not None:
+            line["sharded"] = sh
+    if line is not None:
         print(json.dumps(line), flush=True)
+    if failed:  # peers may be stuck in a collective: no barrier
+        sys.stdout.flush()
+        os._exit(0)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
