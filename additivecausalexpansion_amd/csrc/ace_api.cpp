@@ -494,6 +494,7 @@ struct ace_model {
   SweepWork sw2;  // train_stats scratch (keeps sw's inverse, Q6)
   bool prof = false;
   hipEvent_t ev_asm[2] = {nullptr, nullptr}, ev_grad[2] = {nullptr, nullptr};
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // Kfull*alpha on the side stream
   std::vector<hipEvent_t> ev_upd;
   std::vector<double> upd_flops;
   int upd_used = 0;
@@ -531,17 +532,24 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   ck(ctx, launch_alpha_from_aug(w.A.d(), w.naug, w.npad, m->n, theta[1], use_mu, m->alpha.d(),
                                 m->scal.d(), st),
      "alpha");
+  // Kfull * alpha (HBM-bound read of the Kfull copy) runs on the side stream
+  // under the VALU-bound gradient kernel
+  hipStream_t side = ctx->side;
+  ck(ctx, hipEventRecord(m->ev_fork, st), "event");
+  ck(ctx, hipStreamWaitEvent(side, m->ev_fork, 0), "event wait");
+  ck(ctx, launch_symv_tiles(m->kcopy.d(), w.naug, m->n, m->alpha.d(), m->kapart.d(), w.npad, side),
+     "symv");
+  ck(ctx, launch_rowsum(m->kapart.d(), m->ntr, w.npad, m->n, m->ka.d(), side), "rowsum");
+  ck(ctx, hipEventRecord(m->ev_join, side), "event");
   if (timed) ck(ctx, hipEventRecord(m->ev_grad[0], st), "event");
   ck(ctx, launch_grad(s.kind, s.PM, ps, s.B, s.ZS, tv, w.A.d(), w.naug, -1.0, m->alpha.d(),
                       nullptr, m->gpart.d(), m->trpart.d(), st),
      "grad");
   if (timed) ck(ctx, hipEventRecord(m->ev_grad[1], st), "event");
-  ck(ctx, launch_symv_tiles(m->kcopy.d(), w.naug, m->n, m->alpha.d(), m->kapart.d(), w.npad, st),
-     "symv");
   const int ncol = s.B * (s.PM + 1);
   ck(ctx, launch_colsum(m->gpart.d(), m->ntiles, ncol, m->gsum.d(), st), "colsum");
   ck(ctx, launch_colsum(m->trpart.d(), m->ntiles, 1, m->gsum.d() + ncol, st), "colsum");
-  ck(ctx, launch_rowsum(m->kapart.d(), m->ntr, w.npad, m->n, m->ka.d(), st), "rowsum");
+  ck(ctx, hipStreamWaitEvent(st, m->ev_join, 0), "event wait");
   ck(ctx, launch_final_sums(m->y.d(), m->scal.d() + 4, m->alpha.d(), m->ka.d(), m->n, w.piv.d(),
                             w.npad, m->sums.d(), st),
      "final sums");
@@ -610,6 +618,8 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
       ck(ctx, hipEventCreate(&m->ev_asm[j]), "event");
       ck(ctx, hipEventCreate(&m->ev_grad[j]), "event");
     }
+    ck(ctx, hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming), "event");
+    ck(ctx, hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming), "event");
     sync(ctx);
   } catch (const Fail &f) {
     ace_model_destroy(m);
@@ -629,6 +639,8 @@ void ace_model_destroy(ace_model *m) {
     if (m->ev_asm[j]) (void)hipEventDestroy(m->ev_asm[j]);
     if (m->ev_grad[j]) (void)hipEventDestroy(m->ev_grad[j]);
   }
+  if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
+  if (m->ev_join) (void)hipEventDestroy(m->ev_join);
   delete m;
 }
 

@@ -29,6 +29,8 @@ namespace ace {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------- gather
+// P = -A[:, k] for every row; W = A[:, k] only on the pivot rows (k_panel
+// sweeps them; k_panel_gemm forms every other row of W from P).
 __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, int64_t ld,
                                                 int64_t k0, double *__restrict__ P,
                                                 double *__restrict__ W, int64_t ldp,
@@ -40,12 +42,13 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
   const int tid = threadIdx.x;
   const bool all_lower = i0 >= col0 + 63;
   const bool all_upper = i0 + 63 < col0;
+  const bool piv = i0 >= k0 && i0 < k0 + NB;  // pivot rows: W needed
   if (all_lower) {
     for (int e = tid; e < 4096; e += 256) {
       const int a = e & 63, b = e >> 6;
       const double v = A[(i0 + a) + (col0 + b) * ld];
       P[(i0 + a) + (int64_t)(j0 + b) * ldp] = -v;
-      W[(i0 + a) + (int64_t)(j0 + b) * ldp] = v;
+      if (piv) W[(i0 + a) + (int64_t)(j0 + b) * ldp] = v;
     }
   } else if (all_upper) {
     for (int e = tid; e < 4096; e += 256) {
@@ -57,7 +60,7 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
       const int a = e & 63, b = e >> 6;
       const double v = tile[a][b];
       P[(i0 + a) + (int64_t)(j0 + b) * ldp] = -v;
-      W[(i0 + a) + (int64_t)(j0 + b) * ldp] = v;
+      if (piv) W[(i0 + a) + (int64_t)(j0 + b) * ldp] = v;
     }
   } else {
     for (int e = tid; e < 4096; e += 256) {
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
       const int64_t i = i0 + a, c = col0 + b;
       const double v = (i >= c) ? A[i + c * ld] : A[c + i * ld];
       P[i + (int64_t)(j0 + b) * ldp] = -v;
-      W[i + (int64_t)(j0 + b) * ldp] = v;
+      if (piv) W[i + (int64_t)(j0 + b) * ldp] = v;
     }
   }
   if (i0 == k0) {  // pivot rows of sub-block 0: snapshot for k_pivot / k_panel
