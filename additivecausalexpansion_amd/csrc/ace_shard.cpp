@@ -284,9 +284,11 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
     const bool more = k + 1 < steps;
     wait(st, 2 * k);  // panel k ready
     if (more) {
-      for (auto &b : v) ck(ctx, shard_update_cross(b, k, buf, st), "shard cross update");
+      // side stream, under the bulk update k: cross of block k+1 (after the
+      // bulk update k-1), then pack / exchange / sweep of panel k+1
       rec(2 * k + 1, st);
       wait(side, 2 * k + 1);
+      for (auto &b : v) ck(ctx, shard_update_cross(b, k, buf, side), "shard cross update");
       prepare(k + 1, buf ^ 1);
       rec(2 * (k + 1), side);
     }

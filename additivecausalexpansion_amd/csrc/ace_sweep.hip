@@ -707,9 +707,11 @@ int64_t update_gemm_tiles(int64_t naug, int64_t k0, int kx, bool look) {
   return cnt;
 }
 
-// Step k: panel sweep k (side stream, overlapped with the previous update),
-// then on the main stream the cross tiles of block k+1 (so panel k+1 can
-// start) and the remaining tiles.  P/W are double-buffered by step parity.
+// Step k: the main stream runs only the bulk update of step k (every tile
+// outside the cross of block k+1).  The high-priority side stream, once the
+// bulk update of step k-1 is done, updates the cross of block k+1 with panel
+// k and then gathers and sweeps panel k+1 -- all of it under the main
+// stream's update k.  P/W are double-buffered by step parity.
 hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
                      const SweepTiming *tm) {
   const int64_t naug = b.ld;
@@ -740,14 +742,14 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
       if (e != hipSuccess) return e;
     }
     if (more) {
-      hipLaunchKernelGGL(k_update_x, dim3((unsigned)(naug / XT), 2 * (NB / XT)), dim3(256), 0, st,
-                         b.A, b.ld, b.W[buf], b.P[buf], b.W[buf], b.ld, k0, k + 1, 1, 0);
       if (two) {
-        e = hipEventRecord(sy->ev[2 * k + 1], st);  // cross of block k+1 updated
+        e = hipEventRecord(sy->ev[2 * k + 1], st);  // bulk update k-1 done
         if (e != hipSuccess) return e;
         e = hipStreamWaitEvent(side, sy->ev[2 * k + 1], 0);
         if (e != hipSuccess) return e;
       }
+      hipLaunchKernelGGL(k_update_x, dim3((unsigned)(naug / XT), 2 * (NB / XT)), dim3(256), 0,
+                         side, b.A, b.ld, b.W[buf], b.P[buf], b.W[buf], b.ld, k0, k + 1, 1, 0);
       e = panel_sweep(b, buf ^ 1, k0 + NB, side);
       if (e != hipSuccess) return e;
       if (two) {
