@@ -7,7 +7,7 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SOURCES = ["csrc/ace_pairs.hip", "csrc/ace_sweep.hip", "csrc/ace_util.hip",
+SOURCES = ["csrc/ace_pairs.hip", "csrc/ace_pairs_mm.hip", "csrc/ace_sweep.hip", "csrc/ace_util.hip",
            "csrc/ace_api.cpp", "csrc/ace_host.cpp", "csrc/ace_shard.cpp"]
 HEADERS = ["csrc/ace_internal.h", "csrc/ace_common.h", "../include/ace_hip.h"]
 OUT = os.path.join(HERE, "libace_hip.so")

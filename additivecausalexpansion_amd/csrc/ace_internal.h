@@ -65,6 +65,17 @@ hipError_t launch_assembly(int mode, int kind, int PM, PairSide rows,
                            double *cube, hipStream_t st, const Tile *tiles = nullptr,
                            int64_t ntiles = 0, int G = 1);
 
+// MFMA-expansion variant of mode 0 (ace_pairs_mm.hip)
+hipError_t launch_assembly_mm(int kind, int PM, PairSide S, int64_t npad, int B, int ZS,
+                              TabView tab, double sig, double *out, int64_t ld,
+                              double *kcopy, hipStream_t st, const Tile *tiles,
+                              int64_t ntiles, int G);
+bool pairs_use_mm(int PM);
+hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
+                          const double *A, int64_t ld, double sA, const double *alpha,
+                          double *gpart, double *trpart, hipStream_t st, const Tile *tiles,
+                          int64_t ntiles, int G);
+
 // ---- gradient --------------------------------------------------------------
 // T = sA * A[r,c] - alpha_r alpha_c over the lower 64x64 tiles of [0,n)
 // (grad_ntiles(n) of them).

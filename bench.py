@@ -178,6 +178,8 @@ def run_sharded(dist, rank, world, ctx, steps, warmup, name=None):
     step, model = make_step(kernel, p, B, theta, std_y, ctx, y, X, Z, model=model)
     dt, stats = timed_steps(dist, step, steps, warmup, model)
     upd_ms, upd_n, upd_work = model.kernel_time(0)
+    asm_ms = model.kernel_time(1)[0]
+    grad_ms = model.kernel_time(2)[0]
     model.profile(False)
     ms = dt / steps * 1e3
     out = {
@@ -187,6 +189,8 @@ def run_sharded(dist, rank, world, ctx, steps, warmup, name=None):
         "dense_tflops_total": n ** 3 / (ms * 1e-3) / 1e12,
         "dense_tflops_per_gpu": n ** 3 / (ms * 1e-3) / 1e12 / world,
         "rank0_update_kernel_tflops": (upd_work / (upd_ms * 1e-3) / 1e12) if upd_ms else None,
+        "rank0_phase_ms_per_step": {"update_kernel": upd_ms / steps, "assembly_kernel":
+                                    asm_ms / steps, "gradient_kernel": grad_ms / steps},
         "last_stats": [float(stats[0]), float(stats[1])] if stats is not None else None,
     }
     model.close()
