@@ -179,10 +179,13 @@ def test_pred_golden(A, kernel):
 
 # ------------------------------------------------------------------ fused model
 @pytest.mark.parametrize("kernel", ["SE", "Matern32"])
-@pytest.mark.parametrize("n,p,B", [(300, 2, 5), (513, 3, 4), (1000, 20, 10), (130, 1, 2)])
+@pytest.mark.parametrize("n,p,B", [(300, 2, 5), (513, 3, 4), (1000, 20, 10), (130, 1, 2),
+                                   (600, 32, 5), (700, 40, 6), (300, 64, 3)])
 def test_model_para_update_matches_oracle(A, O, kernel, n, p, B):
     """One device-resident para_update (kernel + sweep + fused gradient) vs the
-    oracle's kernmat_sym -> invkernel -> grad chain, at iter 1 (mu first) and 2."""
+    oracle's kernmat_sym -> invkernel -> grad chain, at iter 1 (mu first) and 2.
+    p >= 25 runs the MFMA-expansion pair kernels (feature buckets 32/48/64),
+    p <= 24 the all-VALU ones."""
     from additivecausalexpansion_amd.synthetic import make_problem
     y, X, Z, th, sy = make_problem(n, p, B, seed=7)
     m = A.DeviceModel(kernel, n, p, B)
