@@ -685,26 +685,27 @@ static hipError_t asm_pm(int mode, int kind, PairSide R, PairSide C, int64_t npa
   return hipGetLastError();
 }
 
-// Fused-model pair kernels: the all-VALU kernels above for feature buckets
-// PM <= 24, the MFMA-expansion kernels (ace_pairs_mm.hip) from PM = 32 up,
-// where the VALU kernels run out of registers (C2 p=20: VALU 3.9 / 9.1 ms vs
-// MFMA 4.4 / 12.2 ms for assembly / gradient; C4 p=50: VALU 369 / 1538 ms vs
-// MFMA 160 / 509 ms; profiles/r01_pairs_ab.txt).  ACE_PAIRS=valu|mm forces
-// one family (diagnostic A/B switch).
-bool pairs_use_mm(int PM) {
+// Fused-model pair kernels: the MFMA-expansion kernels (ace_pairs_mm.hip)
+// for the assembly at every bucket and for the gradient from PM = 32 up; the
+// all-VALU k_grad2 for the gradient at PM <= 24, where it is still faster
+// (profiles/r01_pairs_ab.txt: C2 p=20 gradient VALU 9.1 ms vs MFMA 9.5 ms,
+// assembly MFMA 3.87 ms vs VALU 3.96 ms; C4 p=50 gradient MFMA 372 ms vs VALU
+// 1534 ms, assembly 161 vs 368 ms).  ACE_PAIRS=valu|mm forces one family
+// (diagnostic A/B switch).  `grad` selects the gradient rule.
+bool pairs_use_mm(int PM, bool grad) {
   static int v = -1;
   if (v < 0) {
     const char *e = getenv("ACE_PAIRS");
     v = !e ? 2 : (e[0] == 'm' ? 1 : (e[0] == 'v' ? 0 : 2));
   }
-  return v == 2 ? PM >= 32 : v == 1;
+  return v == 2 ? (!grad || PM >= 32) : v == 1;
 }
 
 hipError_t launch_assembly(int mode, int kind, int PM, PairSide R, PairSide C, int64_t npad,
                            int B, int ZS, TabView tab, double sig, double *out, int64_t ld,
                            double *cube, hipStream_t st, const Tile *tiles, int64_t ntiles,
                            int G) {
-  if (mode == 0 && pairs_use_mm(PM))
+  if (mode == 0 && pairs_use_mm(PM, false))
     return launch_assembly_mm(kind, PM, R, npad, B, ZS, tab, sig, out, ld, cube, st, tiles,
                               ntiles, G);
   switch (PM) {
@@ -748,7 +749,7 @@ hipError_t launch_grad(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                        const double *A, int64_t ld, double sA, const double *alpha,
                        const double *cube, double *gpart, double *trpart, hipStream_t st,
                        const Tile *tiles, int64_t ntiles, int G) {
-  if (!cube && pairs_use_mm(PM))
+  if (!cube && pairs_use_mm(PM, true))
     return launch_grad_mm(kind, PM, S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st, tiles,
                           ntiles, G);
   switch (PM) {

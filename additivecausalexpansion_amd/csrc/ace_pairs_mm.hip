@@ -22,6 +22,9 @@
 
 namespace ace {
 
+// Register caps (__launch_bounds__ second argument = waves per SIMD):
+// gradient 2 (LDS 2 x 33 KB at p = 64 allows 2 workgroups per CU anyway),
+// assembly 3 up to PM = 32 and 2 above (3 would spill at PM = 64).
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 #define SQRT3 1.7320508075688772
@@ -69,7 +72,7 @@ __device__ __forceinline__ void tile_of(const Tile *tiles, int64_t t, int64_t &I
 // k_assembly<PM, KIND, 0>.
 // ---------------------------------------------------------------------------
 template <int PM, int KIND>
-__global__ __launch_bounds__(256) void k_asm_mm(PairSide S, int B, int ZS, TabView tab,
+__global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, int B, int ZS, TabView tab,
                                                 double sig, double *__restrict__ out, int64_t ld,
                                                 double *__restrict__ kcopy,
                                                 const Tile *__restrict__ tiles, int G) {
@@ -178,41 +181,70 @@ __global__ __launch_bounds__(256) void k_asm_mm(PairSide S, int B, int ZS, TabVi
 
 // ---------------------------------------------------------------------------
 // Fused gradient traces (same outputs as k_grad2): per slice b (descending),
-//   GEMM1  G = X_J (w_b X_I)^T          -> r2, K_b, U = T K_b [/ (1 + sqrt(3 r~2_b))]
-//   GEMM2  V = U [X_J | X_J^2 | 1]      -> for every feature i
-//          sum_rc U d_i^2 = sum_r (x_ri^2 R_r - 2 x_ri V_ri) + sum_r V_r,p+i,
-//          R_r = V_r,2p = sum_c U_rc.
-// U never leaves the registers: the GEMM1 result fragment (row r = 16w+lr,
-// column c = 16cb+lk+4v) is exactly GEMM2's A fragment for k-step 4cb+v.
+//   GEMM1  G = X_J (w_b X_I)^T        -> r2, K_b, U = T K_b [/ (1 + sqrt(3 r~2_b))]
+//   GEMM2  V = U [X_J | 1]            -> for every feature i
+//          sum_rc U d_i^2 = sum_r (x_ri^2 R_r - 2 x_ri V_ri) + sum_c x_ci^2 C_c
+//          with R_r = V_r,p (row sums) and C_c (column sums, through LDS).
+// U never leaves the registers for the GEMMs: the GEMM1 result fragment
+// (row r = 16w+lr, column c = 16cb+lk+4v) is exactly GEMM2's A fragment for
+// k-step 4cb+v.  The row operand x_r is read from global memory (L1/L2) in
+// the k-loop, so no register holds a p-long vector.
 // Matern32: r~2_b uses the gradient-indexed weights, which equal slice b+1's
 // kernel weights (Q1), so the factor 1 + sqrt3 t of slice b+1 is cached per
 // pair; the last slice gets its own GEMM with wg[B-1].
 // ---------------------------------------------------------------------------
 template <int PM>
-__device__ __forceinline__ void gemm1_mm(const double *sXJ, const double (&xq)[PM / 4],
+__device__ __forceinline__ void gemm1_mm(const double *sXJ, const double *__restrict__ xrow,
                                          const double *sw, int lr, int lk, d4 (&acc)[4]) {
   constexpr int XP = PM + 1;
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) acc[cb] = d4{0.0, 0.0, 0.0, 0.0};
-  // one k-step of A fragments in flight (explicit prefetch; the scheduling
-  // barrier keeps the compiler from hoisting every LDS read of the loop)
+  // one k-step of operands in flight (explicit prefetch; the scheduling
+  // barrier keeps the compiler from hoisting every load of the loop)
   double an[4];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) an[cb] = sXJ[(16 * cb + lr) * XP + lk];
+  double xn = xrow[lk];
 #pragma unroll
   for (int kk = 0; kk < PM / 4; ++kk) {
     double ac[4];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) ac[cb] = an[cb];
-    const double bop = xq[kk] * sw[4 * kk + lk];
+    const double bop = xn * sw[4 * kk + lk];
     if (kk + 1 < PM / 4) {
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) an[cb] = sXJ[(16 * cb + lr) * XP + 4 * (kk + 1) + lk];
+      xn = xrow[4 * (kk + 1) + lk];
     }
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
       acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[cb], bop, acc[cb], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// s_b of the 64 columns (threads 0..63, from LDS) and of the 64 rows
+// (threads 64..127, from global X) into sSc / sSr.
+template <int PM>
+__device__ __forceinline__ void slice_norms(const double *sXJ, const double *__restrict__ X,
+                                            int64_t R0, const double *sw, int tid, double *sSc,
+                                            double *sSr) {
+  constexpr int XP = PM + 1;
+  if (tid < 64) {
+    double s = 0.0;
+    for (int i = 0; i < PM; ++i) {
+      const double x = sXJ[tid * XP + i];
+      s = fma(x * x, sw[i], s);
+    }
+    sSc[tid] = s;
+  } else if (tid < 128) {
+    const double *xr = X + (R0 + tid - 64) * PM;
+    double s = 0.0;
+    for (int i = 0; i < PM; ++i) {
+      const double x = xr[i];
+      s = fma(x * x, sw[i], s);
+    }
+    sSr[tid - 64] = s;
   }
 }
 
@@ -225,20 +257,20 @@ __device__ __forceinline__ double rcp_nr_mm(double f) {
 }
 
 template <int PM, int KIND>
-__global__ __launch_bounds__(256) void k_grad_mm(PairSide S, int B, int ZS, TabView tab,
+__global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, TabView tab,
                                                  const double *__restrict__ A, int64_t ld,
                                                  double sA, const double *__restrict__ alpha,
                                                  double *__restrict__ gpart,
                                                  double *__restrict__ trpart, int64_t ntiles,
                                                  const Tile *__restrict__ tiles, int G) {
   constexpr int XP = PM + 1;
-  constexpr int KQ = PM / 4;
   constexpr int NV = PM + 1;
-  constexpr int NN = 2 * PM + 1;            // [x | x^2 | 1]
-  constexpr int NB2 = (NN + 15) / 16;        // GEMM2 column blocks
-  constexpr int NBR = (2 * PM) / 16, LRR = (2 * PM) % 16;  // where R_r lands
+  constexpr int NB2 = (PM + 1 + 15) / 16;    // GEMM2 column blocks: [x | 1]
+  constexpr int NBR = PM / 16, LRR = PM % 16;  // where R_r lands
+  constexpr int UP = 65;                       // sU pitch
   __shared__ double sXJ[64 * XP];
-  __shared__ double sSc[64], sSr[64], sZc[64], sLZc[64];
+  __shared__ double sU[64 * UP];
+  __shared__ double sSc[64], sSr[64], sZc[64], sLZc[64], sC[4][64];
   __shared__ double sW[PM];
   __shared__ double sRed[4][NB2 * 16 + 1];
   const int64_t t = blockIdx.x;
@@ -250,13 +282,11 @@ __global__ __launch_bounds__(256) void k_grad_mm(PairSide S, int B, int ZS, TabV
   const int64_t R0 = I * AT, C0 = J * AT, n = S.n;
   const int64_t r = R0 + 16 * w + lr;
   const bool rvalid = r < n;
+  const double *xrow = S.X + r * PM;
   for (int e = tid; e < 64 * PM; e += 256) {
     const int c = e / PM, i = e - c * PM;
     sXJ[c * XP + i] = S.X[(C0 + c) * PM + i];
   }
-  double xq[KQ];
-#pragma unroll
-  for (int kk = 0; kk < KQ; ++kk) xq[kk] = S.X[r * PM + 4 * kk + lk];
   // T = w_rc (sA A[r,c] - alpha_r alpha_c), w = 2 off the diagonal (lower pairs)
   const double ar = rvalid ? alpha[r] : 0.0;
   double tv[4][4];
@@ -278,26 +308,14 @@ __global__ __launch_bounds__(256) void k_grad_mm(PairSide S, int B, int ZS, TabV
   d4 acc[4];
   for (int b = B - 1; b >= 0; --b) {
     const bool last = (b == B - 1);
-    // Matern, last slice: r~2 with its own (gradient-indexed) weights
-    if (KIND == 1 && last) {
+    if (KIND == 1 && last) {  // Matern, last slice: r~2 with its own weights
       __syncthreads();
       if (tid < PM) sW[tid] = tab.wg[b * PM + tid];
       __syncthreads();
-      if (tid < 64) {
-        double s = 0.0;
-        for (int i = 0; i < PM; ++i) {
-          const double x = sXJ[tid * XP + i];
-          s = fma(x * x, sW[i], s);
-        }
-        sSc[tid] = s;
-      }
-      double sr = 0.0;
-#pragma unroll
-      for (int kk = 0; kk < KQ; ++kk) sr = fma(xq[kk] * xq[kk], sW[4 * kk + lk], sr);
-      sr += __shfl_xor(sr, 16, 64);
-      sr += __shfl_xor(sr, 32, 64);
-      gemm1_mm<PM>(sXJ, xq, sW, lr, lk, acc);
+      slice_norms<PM>(sXJ, S.X, R0, sW, tid, sSc, sSr);
+      gemm1_mm<PM>(sXJ, xrow, sW, lr, lk, acc);
       __syncthreads();
+      const double sr = sSr[16 * w + lr];
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
@@ -308,28 +326,17 @@ __global__ __launch_bounds__(256) void k_grad_mm(PairSide S, int B, int ZS, TabV
           fc[cb][v] = 1.0 + sqrt(3.0 * rt2);
         }
     }
-    __syncthreads();  // previous users of sW / sSc / sZc / sRed are done
+    __syncthreads();  // previous users of sW / sSc / sSr / sZc / sU / sRed are done
     if (tid < PM) sW[tid] = tab.wk[b * PM + tid];
     if (b > 0 && tid >= 64 && tid < 128) {
       sZc[tid - 64] = S.Z[(C0 + tid - 64) * ZS + b - 1];
       if (KIND == 0) sLZc[tid - 64] = S.LZ[(C0 + tid - 64) * ZS + b - 1];
     }
     __syncthreads();
-    if (tid < 64) {
-      double s = 0.0;
-      for (int i = 0; i < PM; ++i) {
-        const double x = sXJ[tid * XP + i];
-        s = fma(x * x, sW[i], s);
-      }
-      sSc[tid] = s;
-    }
-    double sr = 0.0;
-#pragma unroll
-    for (int kk = 0; kk < KQ; ++kk) sr = fma(xq[kk] * xq[kk], sW[4 * kk + lk], sr);
-    sr += __shfl_xor(sr, 16, 64);
-    sr += __shfl_xor(sr, 32, 64);
-    gemm1_mm<PM>(sXJ, xq, sW, lr, lk, acc);
-    __syncthreads();  // sSc, sZc ready
+    slice_norms<PM>(sXJ, S.X, R0, sW, tid, sSc, sSr);
+    gemm1_mm<PM>(sXJ, xrow, sW, lr, lk, acc);
+    __syncthreads();  // sSc, sSr, sZc ready
+    const double sr = sSr[16 * w + lr];
     const double lam = tab.lam[b];
     double zr = 0.0, lzr = 0.0;
     if (b > 0) {
@@ -352,10 +359,9 @@ __global__ __launch_bounds__(256) void k_grad_mm(PairSide S, int B, int ZS, TabV
         }
         const bool rlo = r < c;
         const double zlo = rlo ? zr : zc, zhi = rlo ? zc : zr;
-        const double lzlo = rlo ? lzr : lzc, lzhi = rlo ? lzc : lzr;
         double kb, f = 1.0;
         if (KIND == 0) {
-          kb = kval_mm<0>(b, r2, lam, zlo, zhi, lzlo, lzhi);
+          kb = kval_mm<0>(b, r2, lam, zlo, zhi, rlo ? lzr : lzc, rlo ? lzc : lzr);
         } else {
           const double tt = sqrt(r2);
           f = 1.0 + SQRT3 * tt;
@@ -364,12 +370,15 @@ __global__ __launch_bounds__(256) void k_grad_mm(PairSide S, int B, int ZS, TabV
         }
         const double tk = tv[cb][v] * kb;
         gl += tk;
+        double u;
         if (KIND == 0) {
-          acc[cb][v] = tk;  // U
+          u = tk;
         } else {
-          acc[cb][v] = tk * rcp_nr_mm(fc[cb][v]);
+          u = tk * rcp_nr_mm(fc[cb][v]);
           fc[cb][v] = f;
         }
+        acc[cb][v] = u;
+        sU[(16 * w + lr) * UP + cl] = u;
         __builtin_amdgcn_sched_barrier(0);
       }
     // GEMM2 over the column blocks, the block holding R_r first
@@ -377,18 +386,16 @@ __global__ __launch_bounds__(256) void k_grad_mm(PairSide S, int B, int ZS, TabV
     for (int q = 0; q < NB2; ++q) {
       const int nb = (q == 0) ? NBR : (q <= NBR ? q - 1 : q);
       const int nn = 16 * nb + lr;
-      const int fi = nn < PM ? nn : (nn < 2 * PM ? nn - PM : -1);
-      const bool sq = nn >= PM;
+      const double bconst = (nn == PM) ? 1.0 : 0.0;
+      const int fo = nn < PM ? nn : 0;
       d4 a2 = d4{0.0, 0.0, 0.0, 0.0};
-      const int fo = fi >= 0 ? fi : 0;
-      const double bconst = (nn == 2 * PM) ? 1.0 : 0.0;
       double xn = sXJ[lk * XP + fo];
 #pragma unroll
       for (int kk = 0; kk < 16; ++kk) {
         const double x = xn;
         if (kk + 1 < 16) xn = sXJ[(4 * (kk + 1) + lk) * XP + fo];
-        const double bv = fi >= 0 ? (sq ? x * x : x) : bconst;
-        a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[kk >> 2][kk & 3], bv, a2, 0, 0, 0);
+        a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[kk >> 2][kk & 3], nn < PM ? x : bconst,
+                                                  a2, 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
       // a2[v'] = V[r' = R0 + 16 w + lk + 4 v'][nn]
@@ -403,8 +410,6 @@ __global__ __launch_bounds__(256) void k_grad_mm(PairSide S, int B, int ZS, TabV
           const double x = S.X[(R0 + 16 * w + lk + 4 * v) * PM + nn];
           part += fma(x * x, Rv[v], -2.0 * x * a2[v]);
         }
-      } else if (nn < 2 * PM) {
-        part = (a2[0] + a2[1]) + (a2[2] + a2[3]);
       }
       part += __shfl_xor(part, 16, 64);
       part += __shfl_xor(part, 32, 64);
@@ -417,12 +422,25 @@ __global__ __launch_bounds__(256) void k_grad_mm(PairSide S, int B, int ZS, TabV
     gl += __shfl_xor(gl, 16, 64);
     gl += __shfl_xor(gl, 32, 64);
     if (lane == 0) sRed[w][NB2 * 16] = gl;
+    __syncthreads();  // sU, sRed complete
+    {  // column sums of U: thread (quarter q, column c) over 16 rows
+      const int c = tid & 63, qq = tid >> 6;
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += sU[(16 * qq + k) * UP + c];
+      sC[qq][c] = s;
+    }
     __syncthreads();
     if (tid < PM) {
       double g = 0.0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) g += sRed[q][tid] + sRed[q][PM + tid];
-      gpart[((int64_t)b * NV + tid) * ntiles + t] = g;
+      for (int q = 0; q < 4; ++q) g += sRed[q][tid];
+      double gc = 0.0;
+      for (int c = 0; c < 64; ++c) {
+        const double x = sXJ[c * XP + tid];
+        gc = fma(x * x, (sC[0][c] + sC[1][c]) + (sC[2][c] + sC[3][c]), gc);
+      }
+      gpart[((int64_t)b * NV + tid) * ntiles + t] = g + gc;
     } else if (tid == PM) {
       const double g = (sRed[0][NB2 * 16] + sRed[1][NB2 * 16]) + (sRed[2][NB2 * 16] + sRed[3][NB2 * 16]);
       gpart[((int64_t)b * NV + PM) * ntiles + t] = g;
