@@ -14,7 +14,10 @@
 #include <cstdlib>
 #include <vector>
 
-constexpr int NB = 256, UT = 128, AUG = 128, BK = 16, LDL = 144, NCH = NB / BK;
+#ifndef KDEPTH
+#define KDEPTH 256
+#endif
+constexpr int NB = KDEPTH, UT = 128, AUG = 128, BK = 16, LDL = 144, NCH = NB / BK;
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 template <int V>
