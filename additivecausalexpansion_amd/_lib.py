@@ -66,6 +66,11 @@ SIGNATURES = {
     "ace_model_kernel_time": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(_I64),
                                              ctypes.POINTER(ctypes.c_double)]),
+    "ace_model_train": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                       ctypes.c_double, ctypes.c_int, ctypes.c_double, _D, _D,
+                                       ctypes.POINTER(ctypes.c_int),
+                                       ctypes.POINTER(ctypes.c_int)]),
     "ace_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "ace_model_create_sharded": (ctypes.c_int, [_vp, ctypes.c_int, _I64, ctypes.c_int,
                                                 ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -76,7 +81,8 @@ SIGNATURES = {
 UNIQUE_ID_BYTES = 128
 
 STATUS = {0: "ACE_OK", 1: "ACE_ERR_ARG", 2: "ACE_ERR_HIP", 3: "ACE_ERR_OOM",
-          4: "ACE_ERR_UNSUPPORTED"}
+          4: "ACE_ERR_UNSUPPORTED", 5: "ACE_ERR_NONFINITE"}
+OPTIMIZER = {"GD": 0, "NAG": 0, "Adam": 1, "Nadam": 2}
 
 
 class AceError(RuntimeError):

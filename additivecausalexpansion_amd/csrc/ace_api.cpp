@@ -819,4 +819,55 @@ int ace_model_shard_info(const ace_model *m, int *world, int *rank) {
   return ACE_OK;
 }
 
+int ace_model_train(ace_model *m, int optimizer, double learn_rate, double momentum, double beta1,
+                    double beta2, int norm_clip, double clip_at, int maxiter, double tol,
+                    double *theta, double *stats, int *iters, int *converged) {
+  if (!m) return ACE_ERR_ARG;
+  ace_ctx *ctx = m->ctx;
+  if (!theta || !stats || maxiter < 1 ||
+      (optimizer != ACE_OPT_NESTEROV && optimizer != ACE_OPT_ADAM && optimizer != ACE_OPT_NADAM)) {
+    ctx->err = "ace_model_train: bad argument";
+    return ACE_ERR_ARG;
+  }
+  const int P = 2 + m->s.B * (m->s.p + 1);
+  std::vector<double> g((size_t)P), mom1((size_t)P, 0.0), mom2((size_t)P, 0.0);
+  for (int64_t j = 0; j < 2 * (int64_t)(maxiter + 2); ++j) stats[j] = 0.0;
+  int it = 0;
+  for (it = 1; it <= maxiter; ++it) {
+    double st[2], mu = 0.0;
+    const int rc = ace_model_para_update(m, it, theta, g.data(), st, &mu);
+    if (rc != ACE_OK) return rc;
+    stats[2 * it] = st[0];
+    stats[2 * it + 1] = st[1];
+    ace_norm_clip(norm_clip, P, g.data(), clip_at);  // Optim$update (R/optimizer_classes.R)
+    int ok = 0;
+    if (optimizer == ACE_OPT_NADAM)
+      ok = ace_nadam(P, it, learn_rate, beta1, beta2, 1e-8, mom1.data(), mom2.data(), g.data(), theta);
+    else if (optimizer == ACE_OPT_ADAM)
+      ok = ace_adam(P, it, learn_rate, beta1, beta2, 1e-8, mom1.data(), mom2.data(), g.data(), theta);
+    else
+      ok = ace_nesterov(P, learn_rate, momentum, mom1.data(), g.data(), theta);
+    if (!ok) {
+      ctx->err = "Some gradients are not finite, NaN, or NA. Often this is due to too large "
+                 "learning rates.";
+      if (iters) *iters = it;
+      if (converged) *converged = 0;
+      return ACE_ERR_NONFINITE;
+    }
+    theta[1] = mu;  // private$mean_solution(y) with this iteration's inverse
+    const double change = std::fabs(stats[2 * it + 1] - stats[2 * (it - 1) + 1]);
+    if (change < tol && it > 3) break;
+  }
+  if (it > maxiter) it = maxiter;
+  double fin[2];
+  const int rc = ace_model_train_stats(m, theta, fin);
+  if (rc != ACE_OK) return rc;
+  stats[2 * (it + 1)] = fin[0];
+  stats[2 * (it + 1) + 1] = fin[1];
+  if (iters) *iters = it;
+  if (converged) *converged = it < maxiter ? 1 : 0;
+  return ACE_OK;
+}
+
 }  // extern "C"
+

@@ -62,6 +62,24 @@ class DeviceModel:
               self.ctx.handle)
         return g, st, mu.value
 
+    def train(self, theta, optimizer="Nadam", learning_rate=0.01, momentum=0.0, beta1=0.9,
+              beta2=0.999, norm_clip=True, clip_at=1.0, maxiter=1000, tol=1e-4):
+        """ace_model_train: the whole ace.train loop natively (R/main_ace.R:213-235).
+        theta (float64, P) is updated in place; returns (stats 2 x (maxiter+2),
+        iterations, converged)."""
+        from ._lib import OPTIMIZER
+        if optimizer == "GD":
+            momentum = 0.0
+        stats = np.zeros((2, maxiter + 2), order="F")
+        it = ctypes.c_int()
+        conv = ctypes.c_int()
+        check(lib().ace_model_train(self.handle, OPTIMIZER[optimizer], float(learning_rate),
+                                    float(momentum), float(beta1), float(beta2),
+                                    1 if norm_clip else 0, float(clip_at), int(maxiter),
+                                    float(tol), ptr(theta), ptr(stats), ctypes.byref(it),
+                                    ctypes.byref(conv)), self.ctx.handle)
+        return stats, it.value, bool(conv.value)
+
     def train_stats(self, theta):
         th = np.ascontiguousarray(theta, dtype=np.float64)
         st = np.empty(2)

@@ -131,8 +131,10 @@ class AceFit(dict):
 def ace_train(y, X, Z, pi=None, kernel="SE", basis="linear", n_knots=1, optimizer="Nadam",
               maxiter=1000, tol=1e-4, learning_rate=0.01, beta1=0.9, beta2=0.999, momentum=0.0,
               norm_clip=None, clip_at=1.0, init_sigma=None, init_length_scale=20.0,
-              plot_stats=False, verbose=True, ctx=None):
-    """R/main_ace.R:132-254 (ace.train)."""
+              plot_stats=False, verbose=True, ctx=None, native_loop=False):
+    """R/main_ace.R:132-254 (ace.train).  native_loop=True runs the optimisation
+    loop inside the library (ace_model_train: no per-iteration round trip
+    through Python; same arithmetic, so the same trajectory)."""
     if norm_clip is None:
         norm_clip = optimizer in ("Adam", "Nadam")  # R/main_ace.R:143 (Q5)
     yv = np.array(np.ravel(y), dtype=np.float64)
@@ -172,6 +174,27 @@ def ace_train(y, X, Z, pi=None, kernel="SE", basis="linear", n_knots=1, optimize
     myKernel = Kc(px, myBasis.dim(), theta0, moments[0, 1], verbose, ctx=ctx)
     myOptimizer = set_optimizer(optimizer, myKernel, learning_rate, momentum, beta1, beta2,
                                 norm_clip, clip_at)
+    if native_loop:
+        model = myKernel._ensure_model(yv, Xi, myBasis.B)
+        theta = np.ascontiguousarray(myKernel.parameters, dtype=np.float64)
+        stats, it, convergence = model.train(theta, optimizer, learning_rate, momentum, beta1,
+                                             beta2, norm_clip, clip_at, maxiter, tol)
+        myKernel.parameters = theta
+        myKernel._mark_kernel(Xi, myBasis.B)
+        myKernel._inv = None
+        myKernel._inv_from_model = True
+        if verbose:
+            print("Final training log Evidence: ", stats[1, it + 1])
+        stats = stats[:, 2:it + 2]
+        return AceFit(Kernel=myKernel, Basis=myBasis,
+                      OptimSettings={"optim": optimizer, "lr": learning_rate, "momentum": momentum,
+                                     "beta1": beta1, "beta2": beta2},
+                      moments=moments,
+                      train_data={"y": yv, "X": Xi, "Z": Zi, "Zbinary": isbinary},
+                      train_stats={"RIC_bias_corrected": pi is not None,
+                                   "init.length_scale": init_length_scale,
+                                   "convergence": convergence, "final_evidence": stats[1, -1],
+                                   "stats": stats})
     stats = np.zeros((2, maxiter + 2))
     it = 0
     for it in range(1, maxiter + 1):

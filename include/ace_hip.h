@@ -44,7 +44,8 @@ enum ace_status {
   ACE_ERR_ARG = 1,         /* invalid argument / shape                          */
   ACE_ERR_HIP = 2,         /* HIP runtime failure (no device, launch failure)   */
   ACE_ERR_OOM = 3,         /* device allocation failed                          */
-  ACE_ERR_UNSUPPORTED = 4  /* shape outside the compiled range (p > 64, B > 32) */
+  ACE_ERR_UNSUPPORTED = 4, /* shape outside the compiled range (p > 64, B > 32) */
+  ACE_ERR_NONFINITE = 5    /* non-finite gradient in ace_model_train (R's stop()) */
 };
 
 typedef struct ace_ctx ace_ctx;
@@ -195,6 +196,29 @@ int ace_model_get_inverse(ace_model *m, double *inv);
 int ace_model_profile(ace_model *m, int enable);
 int ace_model_kernel_time(ace_model *m, int which, double *ms,
                           int64_t *launches, double *work);
+
+/* The whole ace.train optimisation loop (R/main_ace.R:213-235) in native
+ * code, with no per-iteration round trip through the host language:
+ *   for iter = 1..maxiter:
+ *     para_update (R/kernel_SE_R6.R:40-62): kernel, inverse, gradient, stats,
+ *       theta[1] <- mu_solution at iter 1;
+ *     norm clip (Q5, src/utilities_cpp.cpp:121-129), optimizer step (Q8,
+ *       src/optimizer_cpp.cpp:8-63), theta[1] <- mu_solution (Q4);
+ *     stop when |Delta log evidence| < tol and iter > 3;
+ *   then get_train_stats at the final theta (R/kernel_SE_R6.R:63-74).
+ * optimizer: ACE_OPT_NESTEROV (also "GD" with momentum 0), ACE_OPT_ADAM,
+ * ACE_OPT_NADAM; eps = 1e-8 as in R/optimizer_classes.R.  theta (P) in/out.
+ * stats: 2 x (maxiter + 2) column-major, zero-filled like the R matrix;
+ * column j (1..iter) holds [RMSE, log evidence] of iteration j and column
+ * iter + 1 the final train stats.  *iters = iterations run, *converged =
+ * (iter < maxiter).  A non-finite gradient returns ACE_ERR_NONFINITE (the
+ * optimizer classes' stop(), R/optimizer_classes.R:26-29) with theta and
+ * stats as of that iteration.  Works on sharded models (collective). */
+enum ace_optimizer { ACE_OPT_NESTEROV = 0, ACE_OPT_ADAM = 1, ACE_OPT_NADAM = 2 };
+int ace_model_train(ace_model *m, int optimizer, double learn_rate,
+                    double momentum, double beta1, double beta2, int norm_clip,
+                    double clip_at, int maxiter, double tol, double *theta,
+                    double *stats, int *iters, int *converged);
 
 /* ------------------------------- multi-GPU: block-column-sharded model
  *

@@ -296,6 +296,39 @@ def test_ace_train_and_predict_end_to_end(A):
     assert set(out) >= {"ate", "att", "atu"}
 
 
+@pytest.mark.parametrize("optimizer,kernel", [("Nadam", "SE"), ("Adam", "Matern32"),
+                                              ("NAG", "SE")])
+def test_native_training_loop_matches_python_loop(A, optimizer, kernel):
+    """ace_model_train (the R loop of R/main_ace.R:213-235 inside the library)
+    and the Python mirror of the same loop call the same native para_update
+    and optimizer routines, so their trajectories agree bit for bit, including
+    the stopping iteration and the final train stats."""
+    from additivecausalexpansion_amd.synthetic import readme_data
+    y, X, Z = readme_data(seed=9, n=250)
+    kw = dict(kernel=kernel, basis="cubic", n_knots=2, optimizer=optimizer, maxiter=40,
+              tol=1e-3, learning_rate=0.02, momentum=0.5, norm_clip=True, verbose=False)
+    f_py = A.ace_train(y, X, Z, **kw)
+    f_nat = A.ace_train(y, X, Z, native_loop=True, **kw)
+    assert np.array_equal(f_nat["train_stats"]["stats"], f_py["train_stats"]["stats"])
+    assert f_nat["train_stats"]["convergence"] == f_py["train_stats"]["convergence"]
+    assert np.array_equal(f_nat["Kernel"].parameters, f_py["Kernel"].parameters)
+    p_nat, p_py = A.predict_ace(f_nat), A.predict_ace(f_py)
+    assert np.array_equal(p_nat["map"], p_py["map"])
+
+
+def test_native_training_loop_nonfinite_stops(A):
+    """A learning rate that blows the hyperparameters up ends in the
+    optimizer's stop() (R/optimizer_classes.R:26-29) -> ACE_ERR_NONFINITE."""
+    from additivecausalexpansion_amd.synthetic import make_problem
+    y, X, Z, th, sy = make_problem(200, 2, 3, seed=2)
+    m = A.DeviceModel("SE", 200, 2, 3)
+    m.set_data(y, X, Z, sy)
+    th = th.copy()
+    th[0] = 800.0  # e^800 overflows: non-finite stats and gradient
+    with pytest.raises(A.AceError, match="NONFINITE"):
+        m.train(th, "Nadam", maxiter=5)
+
+
 # ------------------------------------------------------------------ full-size properties
 def test_sweep_large_residual_and_logdet(A):
     """n = 4096 (C1 size): ||A A^-1 - I|| small and logdet vs LAPACK slogdet."""
