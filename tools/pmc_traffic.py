@@ -20,12 +20,13 @@ import sys
 from collections import defaultdict
 
 KERNELS = {
-    "k_update<false>": "k_update<false>",
-    "k_update<true>": "k_update<true>",
-    "k_gather": "ace::k_gather",
-    "k_grad": "ace::k_grad",
-    "k_assembly": "ace::k_assembly",
-    "k_symv_tiles": "ace::k_symv_tiles",
+    "k_update": "ace::k_update(",
+    "k_update_x": "ace::k_update_x(",
+    "k_gather": "ace::k_gather(",
+    "k_panel_gemm": "ace::k_panel_gemm(",
+    "k_grad2": "ace::k_grad2<",
+    "k_asm_mm": "ace::k_asm_mm<",
+    "k_symv_tiles": "ace::k_symv_tiles(",
 }
 
 
