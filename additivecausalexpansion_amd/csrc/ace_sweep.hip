@@ -28,6 +28,18 @@ namespace ace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+// The lookahead chain kernels (k_pivot, k_panel: one to four workgroups of
+// latency-bound work) share CUs with the MFMA-heavy update tiles of the main
+// stream.  Raising their waves' issue priority lets them win the SIMD
+// arbitration instead of getting a 1/5 share of the issue slots.
+#ifndef ACE_CHAIN_PRIO
+#define ACE_CHAIN_PRIO 3
+#endif
+#define CHAIN_PRIO() \
+  do {               \
+    if (ACE_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(ACE_CHAIN_PRIO); \
+  } while (0)
+
 // ---------------------------------------------------------------- gather
 // P = -A[:, k] for every row; W = A[:, k] only on the pivot rows (k_panel
 // sweeps them; k_panel_gemm forms every other row of W from P).
@@ -92,6 +104,7 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
 __global__ __launch_bounds__(256) void k_pivot(const double *__restrict__ S, int s,
                                                double *__restrict__ SW, double *__restrict__ piv,
                                                int64_t p0, int *__restrict__ flag) {
+  CHAIN_PRIO();
   __shared__ __attribute__((aligned(16))) double colb[2][SUB];
   __shared__ __attribute__((aligned(16))) double rowb[2][SUB];
   __shared__ double pv[SUB];
@@ -161,6 +174,7 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ W, int64_t l
                                                int s, const double *__restrict__ SW,
                                                const double *__restrict__ S,
                                                double *__restrict__ Snext, int64_t row0) {
+  CHAIN_PRIO();
   __shared__ double sSW[SUB][PLD];  // sSW[b][a] = SW(a, b)
   __shared__ double sSt[SUB][SLD];  // sSt[c][t] = S(t, 64 cc + c)
   const int64_t i0 = row0 + (int64_t)blockIdx.x * SUB;
