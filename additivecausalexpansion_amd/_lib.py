@@ -29,6 +29,7 @@ SIGNATURES = {
     "ace_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
     "ace_destroy": (None, [_vp]),
     "ace_last_error": (ctypes.c_char_p, [_vp]),
+    "ace_set_interrupt_poll": (ctypes.c_int, [_vp, ctypes.c_void_p, ctypes.c_void_p]),
     "ace_kernmat_cross": (ctypes.c_int, [_vp, ctypes.c_int, _I64, _I64, ctypes.c_int, ctypes.c_int,
                                          _D, _D, _D, _D, _D, _D, _D]),
     "ace_kernmat_sym": (ctypes.c_int, [_vp, ctypes.c_int, _I64, ctypes.c_int, ctypes.c_int,
@@ -81,7 +82,8 @@ SIGNATURES = {
 UNIQUE_ID_BYTES = 128
 
 STATUS = {0: "ACE_OK", 1: "ACE_ERR_ARG", 2: "ACE_ERR_HIP", 3: "ACE_ERR_OOM",
-          4: "ACE_ERR_UNSUPPORTED", 5: "ACE_ERR_NONFINITE"}
+          4: "ACE_ERR_UNSUPPORTED", 5: "ACE_ERR_NONFINITE", 6: "ACE_ERR_INTERRUPTED"}
+POLL_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
 OPTIMIZER = {"GD": 0, "NAG": 0, "Adam": 1, "Nadam": 2}
 
 
@@ -136,6 +138,13 @@ class Context:
         h = _vp()
         check(lib().ace_create(device, ctypes.byref(h)), None)
         self.handle = h
+
+    def set_interrupt_poll(self, fn):
+        """fn() -> bool, polled between training iterations (ace_set_interrupt_poll);
+        None removes it."""
+        self._poll = None if fn is None else POLL_FN(lambda _u: 1 if fn() else 0)
+        ptr_ = ctypes.cast(self._poll, ctypes.c_void_p) if self._poll is not None else None
+        check(lib().ace_set_interrupt_poll(self.handle, ptr_, None), self.handle)
 
     def close(self):
         if getattr(self, "handle", None):

@@ -69,6 +69,13 @@ void ace_destroy(ace_ctx *ctx) {
   delete ctx;
 }
 
+int ace_set_interrupt_poll(ace_ctx *ctx, int (*poll)(void *user), void *user) {
+  if (!ctx) return ACE_ERR_ARG;
+  ctx->poll = poll;
+  ctx->poll_user = user;
+  return ACE_OK;
+}
+
 const char *ace_last_error(const ace_ctx *ctx) {
   if (!ctx) return g_create_err.c_str();
   return ctx->err.c_str();
@@ -673,6 +680,10 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, d
                           double *mu_post) {
   if (!m) return ACE_ERR_ARG;
   ace_ctx *ctx = m->ctx;
+  if (ctx->poll && ctx->poll(ctx->poll_user)) {
+    ctx->err = "interrupted";
+    return ACE_ERR_INTERRUPTED;
+  }
   ACE_TRY
   ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
   arg(ctx, m->has_data, "ace_model_set_data() not called");
@@ -836,7 +847,11 @@ int ace_model_train(ace_model *m, int optimizer, double learn_rate, double momen
   for (it = 1; it <= maxiter; ++it) {
     double st[2], mu = 0.0;
     const int rc = ace_model_para_update(m, it, theta, g.data(), st, &mu);
-    if (rc != ACE_OK) return rc;
+    if (rc != ACE_OK) {  // interrupted (or failed) before iteration `it`
+      if (iters) *iters = it - 1;
+      if (converged) *converged = 0;
+      return rc;
+    }
     stats[2 * it] = st[0];
     stats[2 * it + 1] = st[1];
     ace_norm_clip(norm_clip, P, g.data(), clip_at);  // Optim$update (R/optimizer_classes.R)

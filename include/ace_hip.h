@@ -45,7 +45,8 @@ enum ace_status {
   ACE_ERR_HIP = 2,         /* HIP runtime failure (no device, launch failure)   */
   ACE_ERR_OOM = 3,         /* device allocation failed                          */
   ACE_ERR_UNSUPPORTED = 4, /* shape outside the compiled range (p > 64, B > 32) */
-  ACE_ERR_NONFINITE = 5    /* non-finite gradient in ace_model_train (R's stop()) */
+  ACE_ERR_NONFINITE = 5,   /* non-finite gradient in ace_model_train (R's stop()) */
+  ACE_ERR_INTERRUPTED = 6  /* the interrupt poll asked to stop                  */
 };
 
 typedef struct ace_ctx ace_ctx;
@@ -59,6 +60,12 @@ void ace_destroy(ace_ctx *ctx);
 /* Message of the last failure on this context ("" if none).  NULL ctx gives
  * the message of the last failed ace_create in this process. */
 const char *ace_last_error(const ace_ctx *ctx);
+/* Optional interrupt poll (the reference calls Rcpp::checkUserInterrupt() in
+ * its row loops, src/kernel_SE_cpp.cpp): poll(user) is called between
+ * iterations of ace_model_train and before every ace_model_para_update; a
+ * non-zero return stops the call with ACE_ERR_INTERRUPTED (the R shim maps
+ * it to R's interrupt).  poll == NULL removes it. */
+int ace_set_interrupt_poll(ace_ctx *ctx, int (*poll)(void *user), void *user);
 
 /* ------------------------------------------------ Rcpp-export equivalents */
 

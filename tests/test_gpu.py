@@ -329,6 +329,24 @@ def test_native_training_loop_nonfinite_stops(A):
         m.train(th, "Nadam", maxiter=5)
 
 
+def test_interrupt_poll_stops_training(A):
+    """ace_set_interrupt_poll: the poll runs before every para_update; a true
+    return stops ace_model_train with ACE_ERR_INTERRUPTED (R's interrupt,
+    Rcpp::checkUserInterrupt in the reference's loops)."""
+    from additivecausalexpansion_amd.synthetic import make_problem
+    y, X, Z, th, sy = make_problem(200, 2, 3, seed=4)
+    ctx = A.Context(0)
+    calls = []
+    ctx.set_interrupt_poll(lambda: calls.append(1) or len(calls) > 3)
+    m = A.DeviceModel("SE", 200, 2, 3, ctx=ctx)
+    m.set_data(y, X, Z, sy)
+    with pytest.raises(A.AceError, match="INTERRUPTED"):
+        m.train(th.copy(), "Nadam", maxiter=50)
+    assert len(calls) == 4  # three iterations ran, the fourth poll stopped the loop
+    ctx.set_interrupt_poll(None)
+    m.para_update(1, th.copy())  # no poll any more
+
+
 # ------------------------------------------------------------------ full-size properties
 def test_sweep_large_residual_and_logdet(A):
     """n = 4096 (C1 size): ||A A^-1 - I|| small and logdet vs LAPACK slogdet."""
