@@ -24,15 +24,22 @@ using namespace Rcpp;
 
 namespace {
 
+// Rcpp::checkUserInterrupt() equivalent: R_CheckUserInterrupt longjmps, so
+// it runs under R_ToplevelExec and a FALSE return means "interrupt pending".
+void check_interrupt(void *) { R_CheckUserInterrupt(); }
+int r_poll(void *) { return R_ToplevelExec(check_interrupt, nullptr) == FALSE; }
+
 ace_ctx *ctx() {
   static ace_ctx *c = nullptr;
   if (!c) {
     if (ace_create(0, &c) != ACE_OK) Rcpp::stop(std::string("ace: ") + ace_last_error(nullptr));
+    ace_set_interrupt_poll(c, r_poll, nullptr);
   }
   return c;
 }
 
 void ok(int status) {
+  if (status == ACE_ERR_INTERRUPTED) throw Rcpp::internal::InterruptedException();
   if (status != ACE_OK) Rcpp::stop(std::string("ace: ") + ace_last_error(ctx()));
 }
 
@@ -249,4 +256,18 @@ List ace_model_step(SEXP model, int iter, NumericVector parameters) {
   double mu = 0;
   ok(ace_model_para_update(m.get(), iter, parameters.begin(), g.begin(), st.begin(), &mu));
   return List::create(_["gradients"] = g, _["stats"] = st, _["mu"] = mu);
+}
+
+// The whole ace.train loop (R/main_ace.R:213-235) natively; optimizer
+// 0 = Nesterov, 1 = Adam, 2 = Nadam.  parameters is updated in place.
+// [[Rcpp::export]]
+List ace_model_fit(SEXP model, int optimizer, double learn_rate, double momentum, double beta1,
+                   double beta2, bool norm_clip, double clip_at, int maxiter, double tol,
+                   NumericVector parameters) {
+  XPtr<ace_model, PreserveStorage, ace_model_destroy, true> m(model);
+  NumericVector st(2);
+  int iters = 0, converged = 0;
+  ok(ace_model_train(m.get(), optimizer, learn_rate, momentum, beta1, beta2, norm_clip ? 1 : 0,
+                     clip_at, maxiter, tol, parameters.begin(), st.begin(), &iters, &converged));
+  return List::create(_["stats"] = st, _["iterations"] = iters, _["converged"] = converged != 0);
 }
