@@ -71,6 +71,7 @@ hipError_t launch_assembly_mm(int kind, int PM, PairSide S, int64_t npad, int B,
                               double *kcopy, hipStream_t st, const Tile *tiles,
                               int64_t ntiles, int G);
 bool pairs_use_mm(int PM, bool grad);
+bool mm_lds_ok(int PM, int B, int kind, bool grad);
 hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                           const double *A, int64_t ld, double sA, const double *alpha,
                           double *gpart, double *trpart, hipStream_t st, const Tile *tiles,

@@ -687,25 +687,27 @@ static hipError_t asm_pm(int mode, int kind, PairSide R, PairSide C, int64_t npa
 
 // Fused-model pair kernels: the MFMA-expansion kernels (ace_pairs_mm.hip)
 // for the assembly at every bucket and for the gradient from PM = 32 up; the
-// all-VALU k_grad2 for the gradient at PM <= 24, where it is still faster
-// (profiles/r01_pairs_ab.txt: C2 p=20 gradient VALU 9.1 ms vs MFMA 9.5 ms,
-// assembly MFMA 3.87 ms vs VALU 3.96 ms; C4 p=50 gradient MFMA 372 ms vs VALU
-// 1534 ms, assembly 161 vs 368 ms).  ACE_PAIRS=valu|mm forces one family
-// (diagnostic A/B switch).  `grad` selects the gradient rule.
+// MFMA-expansion kernels (ace_pairs_mm.hip) for fused-model assembly and the
+// cube-less gradient at every PM; the all-VALU kernels remain for the ABI
+// modes (cube outputs) and when the per-tile staging does not fit in LDS
+// (profiles/r01_pairs_ab.txt: C2 p=20 gradient MFMA 7.45 ms vs VALU 9.1 ms,
+// assembly 3.4 vs 3.96 ms; C4 p=50 gradient 372 vs 1534 ms).  ACE_PAIRS=valu
+// forces the VALU family (diagnostic A/B switch).
 bool pairs_use_mm(int PM, bool grad) {
   static int v = -1;
   if (v < 0) {
     const char *e = getenv("ACE_PAIRS");
     v = !e ? 2 : (e[0] == 'm' ? 1 : (e[0] == 'v' ? 0 : 2));
   }
-  return v == 2 ? (!grad || PM >= 32) : v == 1;
+  (void)grad;
+  return v != 0;
 }
 
 hipError_t launch_assembly(int mode, int kind, int PM, PairSide R, PairSide C, int64_t npad,
                            int B, int ZS, TabView tab, double sig, double *out, int64_t ld,
                            double *cube, hipStream_t st, const Tile *tiles, int64_t ntiles,
                            int G) {
-  if (mode == 0 && pairs_use_mm(PM, false))
+  if (mode == 0 && pairs_use_mm(PM, false) && mm_lds_ok(PM, B, kind, false))
     return launch_assembly_mm(kind, PM, R, npad, B, ZS, tab, sig, out, ld, cube, st, tiles,
                               ntiles, G);
   switch (PM) {
@@ -749,7 +751,7 @@ hipError_t launch_grad(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                        const double *A, int64_t ld, double sA, const double *alpha,
                        const double *cube, double *gpart, double *trpart, hipStream_t st,
                        const Tile *tiles, int64_t ntiles, int G) {
-  if (!cube && pairs_use_mm(PM, true))
+  if (!cube && pairs_use_mm(PM, true) && mm_lds_ok(PM, B, kind, true))
     return launch_grad_mm(kind, PM, S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st, tiles,
                           ntiles, G);
   switch (PM) {

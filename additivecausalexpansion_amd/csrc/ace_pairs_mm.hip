@@ -27,10 +27,65 @@ namespace ace {
 // assembly 3 up to PM = 32 and 2 above (3 would spill at PM = 64).
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+// Pairs per scheduling group in the elementwise loops (a sched_barrier after
+// every ACE_MM_PG pairs bounds live ranges; 0 = no barriers).
+#ifndef ACE_MM_PG
+#define ACE_MM_PG 2
+#endif
+// Most GEMM2 column blocks accumulated per pass of its k-loop.
+#ifndef ACE_MM_QG
+#define ACE_MM_QG 4
+#endif
+#define MM_PAIR_FENCE(cb, v) \
+  if (ACE_MM_PG > 0 && ((4 * (cb) + (v) + 1) % (ACE_MM_PG > 0 ? ACE_MM_PG : 1)) == 0) \
+    __builtin_amdgcn_sched_barrier(0)
+
 #define SQRT3 1.7320508075688772
 
 __device__ __forceinline__ double sgn_mm(double x) {
   return (double)((0.0 < x) - (x < 0.0));
+}
+
+// exp(x) without the library's special-case handling: every argument here is
+// lam - r2 (+ log|z| terms) or lam - sqrt3 t, finite and bounded above by the
+// amplitude parameter.  Cody-Waite reduction x = k ln2 + r, |r| <= ln2/2, and
+// the degree-12 Taylor polynomial (truncation < 2e-16 relative), then
+// ldexp; arguments below -745 give 0 like exp().
+__device__ __forceinline__ double exp_pk(double x) {
+  x = fmax(x, -745.2);
+  const double kf = __builtin_rint(x * 1.4426950408889634);
+  double r = fma(-kf, 6.93147180369123816490e-01, x);
+  r = fma(-kf, 1.90821492927058770002e-10, r);
+  double q = 2.08767569878680989792e-09;   // 1/12!
+  q = fma(q, r, 2.50521083854417187751e-08);  // 1/11!
+  q = fma(q, r, 2.75573192239858906526e-07);  // 1/10!
+  q = fma(q, r, 2.75573192239858906526e-06);  // 1/9!
+  q = fma(q, r, 2.48015873015873015873e-05);  // 1/8!
+  q = fma(q, r, 1.98412698412698412698e-04);  // 1/7!
+  q = fma(q, r, 1.38888888888888888889e-03);  // 1/6!
+  q = fma(q, r, 8.33333333333333333333e-03);  // 1/5!
+  q = fma(q, r, 4.16666666666666666667e-02);  // 1/4!
+  q = fma(q, r, 1.66666666666666666667e-01);  // 1/3!
+  q = fma(q, r, 0.5);
+  q = fma(q, r, 1.0);
+  q = fma(q, r, 1.0);
+  return __builtin_amdgcn_ldexp(q, (int)kf);
+}
+
+// sqrt(x), x >= 0 and normal or 0 (r2 values): hardware rsq + the
+// Goldschmidt refinement of the library sequence, without its denormal
+// rescaling.  x = 0 gives 0 (the estimate is taken at max(x, 1e-300)).
+__device__ __forceinline__ double sqrt_pk(double x) {
+  const double y = __builtin_amdgcn_rsq(fmax(x, 1e-300));
+  double s = x * y;
+  double h = 0.5 * y;
+  const double e = fma(-h, s, 0.5);
+  s = fma(s, e, s);
+  h = fma(h, e, h);
+  double d = fma(-s, s, x);
+  s = fma(d, h, s);
+  d = fma(-s, s, x);
+  return fma(d, h, s);
 }
 
 // Reference expressions of one slice value (same as ace_pairs.hip kval):
@@ -39,12 +94,12 @@ template <int KIND>
 __device__ __forceinline__ double kval_mm(int b, double r2, double lam, double zlo, double zhi,
                                           double lzlo, double lzhi) {
   if (KIND == 0) {
-    if (b == 0) return exp(lam - r2);
+    if (b == 0) return exp_pk(lam - r2);
     if (zlo == 0.0 || zhi == 0.0) return 0.0;
-    return (sgn_mm(zlo) * sgn_mm(zhi)) * exp(((lam - r2) + lzlo) + lzhi);
+    return (sgn_mm(zlo) * sgn_mm(zhi)) * exp_pk(((lam - r2) + lzlo) + lzhi);
   } else {
-    const double t = sqrt(r2);
-    const double e = (1.0 + SQRT3 * t) * exp(lam - SQRT3 * t);
+    const double t = sqrt_pk(r2);
+    const double e = (1.0 + SQRT3 * t) * exp_pk(lam - SQRT3 * t);
     if (b == 0) return e;
     if (zlo == 0.0) return 0.0;
     return (e * zlo) * zhi;
@@ -67,6 +122,176 @@ __device__ __forceinline__ void tile_of(const Tile *tiles, int64_t t, int64_t &I
 }
 
 // ---------------------------------------------------------------------------
+// Per-tile staging shared by both kernels (dynamic LDS, doubles):
+//   XJ  [64][XP]      column-side covariates (gradient, PM % 16 != 0: [x | x^2])
+//   XI  [64][PM+1]    row-side covariates (gradient, PM <= 32: GEMM2 epilogue)
+//   Z   [B-1][64]     column-side basis values (slices 1..B-1)
+//   LZ  [B-1][64]     log|z| (SE only)
+//   Nc  [NS][64]      column norms s_b(x_c) = sum_i w_bi x_ci^2
+//   Nr  [NS][64]      row norms s_b(x_r)
+//   W   [NS][PM]      slice weights
+//   Red               gradient partials of the four waves
+// NS = B slice norms with the kernel weights (+ 1 with the gradient weights
+// of slice B-1 for the Matern gradient).  Staged once per tile, so the slice
+// loops read only LDS and registers, apart from the row values z_r, whose
+// load is issued ahead of each slice's GEMM1.
+// ---------------------------------------------------------------------------
+struct MmLayout {
+  int xj, xi, z, lz, nc, nr, w, red, red_slices, total;
+};
+
+// Width of the staged covariate table: the gradient of a PM that is not a
+// multiple of 16 stages [x | x^2] (GEMM2's B operand, whose 16-wide column
+// blocks then mix the two halves); otherwise x only.
+__host__ __device__ constexpr int mm_table_width(int PM, bool grad) {
+  return (grad && PM % 16 != 0) ? 2 * PM : PM;
+}
+
+// Gradient partials: one buffer per slice (no barrier inside the slice
+// loop) when that fits in 16 KB, else two buffers and a barrier per slice.
+__host__ __device__ inline MmLayout mm_layout(int PM, int B, int KIND, bool grad) {
+  MmLayout o;
+  const int NS = (grad && KIND == 1) ? B + 1 : B;
+  int off = 0;
+  o.xj = off;
+  off += 64 * (mm_table_width(PM, grad) + 1);
+  o.xi = off;
+  if (grad && PM <= 32) off += 64 * (PM + 1);
+  o.z = off;
+  off += (B - 1) * 64;
+  o.lz = off;
+  if (KIND == 0) off += (B - 1) * 64;
+  o.nc = off;
+  off += NS * 64;
+  o.nr = off;
+  off += NS * 64;
+  o.w = off;
+  off += NS * PM;
+  o.red = off;
+  o.red_slices = 0;
+  if (grad) {
+    const int per = 4 * (2 * PM + 1);
+    o.red_slices = (B * per * 8 <= 16 * 1024) ? B : 2;
+    off += o.red_slices * per + 4;
+  }
+  o.total = off;
+  return o;
+}
+
+struct MmLds {
+  double *XJ, *XI, *Z, *LZ, *Nc, *Nr, *W, *Red;
+  int red_slices;
+};
+
+template <int PM, int KIND, int XP, bool GRAD>
+__device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS,
+                                          const double *__restrict__ wk,
+                                          const double *__restrict__ wlast, int64_t R0,
+                                          int64_t C0, int tid) {
+  const MmLayout o = mm_layout(PM, B, KIND, GRAD);
+  const int NS = (GRAD && KIND == 1) ? B + 1 : B;
+  constexpr bool XI = GRAD && PM <= 32;
+  MmLds L;
+  L.XJ = lds + o.xj;
+  L.XI = lds + o.xi;
+  L.Z = lds + o.z;
+  L.LZ = lds + o.lz;
+  L.Nc = lds + o.nc;
+  L.Nr = lds + o.nr;
+  L.W = lds + o.w;
+  L.Red = lds + o.red;
+  L.red_slices = o.red_slices;
+  for (int e = tid; e < 64 * PM; e += 256) {
+    const int c = e / PM, i = e - c * PM;
+    const double x = S.X[(C0 + c) * PM + i];
+    L.XJ[c * XP + i] = x;
+    if (XP > PM + 1) L.XJ[c * XP + PM + i] = x * x;
+    if (XI) L.XI[c * (PM + 1) + i] = S.X[(R0 + c) * PM + i];
+  }
+  for (int e = tid; e < (B - 1) * 64; e += 256) {
+    const int bb = e >> 6, c = e & 63;
+    L.Z[e] = S.Z[(C0 + c) * ZS + bb];
+    if (KIND == 0) L.LZ[e] = S.LZ[(C0 + c) * ZS + bb];
+  }
+  for (int e = tid; e < NS * PM; e += 256) L.W[e] = (e < B * PM) ? wk[e] : wlast[e - B * PM];
+  __syncthreads();
+  // norms: task = (side, slice, point), same accumulation order as the
+  // per-slice loops they replace (i ascending, fma(x^2, w, s))
+  for (int e = tid; e < 2 * NS * 64; e += 256) {
+    const int side = e / (NS * 64), rem = e - side * NS * 64;
+    const int sl = rem >> 6, pt = rem & 63;
+    const double *w = L.W + sl * PM;
+    double s = 0.0;
+    if (side == 0) {
+#pragma unroll 4
+      for (int i = 0; i < PM; ++i) {
+        const double x = L.XJ[pt * XP + i];
+        s = fma(x * x, w[i], s);
+      }
+      L.Nc[rem] = s;
+    } else {
+      const double *xr = XI ? L.XI + pt * (PM + 1) : S.X + (R0 + pt) * PM;
+#pragma unroll 4
+      for (int i = 0; i < PM; ++i) {
+        const double x = xr[i];
+        s = fma(x * x, w[i], s);
+      }
+      L.Nr[rem] = s;
+    }
+  }
+  __syncthreads();
+  return L;
+}
+
+// Row operand of GEMM1 for one lane: x_r[4 kk + lk], kept in registers up to
+// PM = 32 and read from L1/L2 above.
+template <int PM, bool FROM_PTR = false>
+struct RowX {
+  static constexpr bool REG = PM <= 32 && !FROM_PTR;
+  double q[REG ? PM / 4 : 1];
+  const double *g;
+  __device__ __forceinline__ void load(const double *xrow, int lk) {
+    g = xrow;
+    if (REG) {
+#pragma unroll
+      for (int kk = 0; kk < PM / 4; ++kk) q[kk] = xrow[4 * kk + lk];
+    }
+  }
+  __device__ __forceinline__ double at(int kk, int lk) const {
+    return REG ? q[kk] : g[4 * kk + lk];
+  }
+};
+
+// GEMM1: acc[cb][v] = sum_i w_i x_ci x_ri for the lane's 16 pairs
+// (row r = 16 w + lr, column c = 16 cb + lk + 4 v); w in LDS.
+template <int XP, int PM, bool FP>
+__device__ __forceinline__ void gemm1_mm(const double *sXJ, const RowX<PM, FP> &xr, const double *w,
+                                         int lr, int lk, d4 (&acc)[4]) {
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) acc[cb] = d4{0.0, 0.0, 0.0, 0.0};
+  double an[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) an[cb] = sXJ[(16 * cb + lr) * XP + lk];
+  double bn = xr.at(0, lk) * w[lk];
+#pragma unroll
+  for (int kk = 0; kk < PM / 4; ++kk) {
+    double ac[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) ac[cb] = an[cb];
+    const double bop = bn;
+    if (kk + 1 < PM / 4) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) an[cb] = sXJ[(16 * cb + lr) * XP + 4 * (kk + 1) + lk];
+      bn = xr.at(kk + 1, lk) * w[4 * (kk + 1) + lk];
+    }
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+      acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[cb], bop, acc[cb], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Fused assembly (mode 0): lower 64-tiles of A (sigma on the diagonal,
 // identity on padding) and of the Kfull copy; same outputs as
 // k_assembly<PM, KIND, 0>.
@@ -76,12 +301,7 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
                                                 double sig, double *__restrict__ out, int64_t ld,
                                                 double *__restrict__ kcopy,
                                                 const Tile *__restrict__ tiles, int G) {
-  constexpr int XP = PM + 1;  // odd LDS pitch
-  constexpr int KQ = PM / 4;
-  __shared__ double sXJ[64 * XP];
-  __shared__ double sSc[64];
-  __shared__ double sZc[64], sLZc[64];
-  __shared__ double sW[PM];
+  extern __shared__ __attribute__((aligned(16))) double lds[];
   int64_t I, J;
   tile_of(tiles, blockIdx.x, I, J);
   if (G > 1) {
@@ -92,77 +312,45 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
   const int64_t R0 = I * AT, C0 = J * AT, n = S.n;
-  const int64_t r = R0 + 16 * w + lr;
-  for (int e = tid; e < 64 * PM; e += 256) {
-    const int c = e / PM, i = e - c * PM;
-    sXJ[c * XP + i] = S.X[(C0 + c) * PM + i];
-  }
-  double xq[KQ];
-#pragma unroll
-  for (int kk = 0; kk < KQ; ++kk) xq[kk] = S.X[r * PM + 4 * kk + lk];
+  const int rl = 16 * w + lr;
+  const int64_t r = R0 + rl;
+  constexpr int XP = PM + 1;
+  const MmLds L = mm_stage<PM, KIND, XP, false>(lds, S, B, ZS, tab.wk, tab.wk, R0, C0, tid);
+  RowX<PM> xr;
+  xr.load(S.X + r * PM, lk);
   double kf[4][4];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
     for (int v = 0; v < 4; ++v) kf[cb][v] = 0.0;
-
   for (int b = 0; b < B; ++b) {
-    __syncthreads();  // previous slice done with sW / sSc (and sXJ staged)
-    if (tid < PM) sW[tid] = tab.wk[b * PM + tid];
-    if (b > 0 && tid >= 64 && tid < 128) {
-      sZc[tid - 64] = S.Z[(C0 + tid - 64) * ZS + b - 1];
-      if (KIND == 0) sLZc[tid - 64] = S.LZ[(C0 + tid - 64) * ZS + b - 1];
-    }
-    __syncthreads();
-    if (tid < 64) {
-      double s = 0.0;
-#pragma unroll 4
-      for (int i = 0; i < PM; ++i) {
-        const double x = sXJ[tid * XP + i];
-        s = fma(x * x, sW[i], s);
-      }
-      sSc[tid] = s;
-    }
-    double sr = 0.0;
-#pragma unroll
-    for (int kk = 0; kk < KQ; ++kk) sr = fma(xq[kk] * xq[kk], sW[4 * kk + lk], sr);
-    sr += __shfl_xor(sr, 16, 64);
-    sr += __shfl_xor(sr, 32, 64);
-    d4 acc[4];
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) acc[cb] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int kk = 0; kk < KQ; ++kk) {
-      const double bop = xq[kk] * sW[4 * kk + lk];
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-        acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(sXJ[(16 * cb + lr) * XP + 4 * kk + lk], bop,
-                                                       acc[cb], 0, 0, 0);
-    }
-    __syncthreads();  // sSc ready
-    const double lam = tab.lam[b];
-    double zr = 0.0, lzr = 0.0;
+    double zr = 0.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
     if (b > 0) {
       zr = S.Z[r * ZS + b - 1];
       if (KIND == 0) lzr = S.LZ[r * ZS + b - 1];
     }
+    d4 acc[4];
+    gemm1_mm<XP>(L.XJ, xr, L.W + b * PM, lr, lk, acc);
+    const double sr = L.Nr[b * 64 + rl];
+    const double *nc = L.Nc + b * 64;
+    const double lam = tab.lam[b];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int cl = 16 * cb + lk + 4 * v;
         const int64_t c = C0 + cl;
-        double r2 = fmax(fma(-2.0, acc[cb][v], sr + sSc[cl]), 0.0);
+        double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), 0.0);
         if (c == r) r2 = 0.0;
         double zc = 0.0, lzc = 0.0;
         if (b > 0) {
-          zc = sZc[cl];
-          if (KIND == 0) lzc = sLZc[cl];
+          zc = L.Z[(b - 1) * 64 + cl];
+          if (KIND == 0) lzc = L.LZ[(b - 1) * 64 + cl];
         }
         const double kb = (r < c) ? kval_mm<KIND>(b, r2, lam, zr, zc, lzr, lzc)
                                   : kval_mm<KIND>(b, r2, lam, zc, zr, lzc, lzr);
         kf[cb][v] += kb;
-        __builtin_amdgcn_sched_barrier(0);  // one pair at a time: bounded live ranges
+        MM_PAIR_FENCE(cb, v);
       }
   }
 #pragma unroll
@@ -181,73 +369,18 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
 
 // ---------------------------------------------------------------------------
 // Fused gradient traces (same outputs as k_grad2): per slice b (descending),
-//   GEMM1  G = X_J (w_b X_I)^T        -> r2, K_b, U = T K_b [/ (1 + sqrt(3 r~2_b))]
-//   GEMM2  V = U [X_J | 1]            -> for every feature i
-//          sum_rc U d_i^2 = sum_r (x_ri^2 R_r - 2 x_ri V_ri) + sum_c x_ci^2 C_c
-//          with R_r = V_r,p (row sums) and C_c (column sums, through LDS).
-// U never leaves the registers for the GEMMs: the GEMM1 result fragment
-// (row r = 16w+lr, column c = 16cb+lk+4v) is exactly GEMM2's A fragment for
-// k-step 4cb+v.  The row operand x_r is read from global memory (L1/L2) in
-// the k-loop, so no register holds a p-long vector.
+//   GEMM1  G = X_J (w_b X_I)^T          -> r2, K_b, U = T K_b [/ (1 + sqrt(3 r~2_b))]
+//   GEMM2  V = U [X_J | X_J^2]          -> for every feature i
+//          sum_rc U d_i^2 = sum_r (x_ri^2 R_r - 2 x_ri V_ri + V2_ri)
+//          with R_r the row sums of U (in registers + 2 shuffles).
+// U never leaves the registers: the GEMM1 result fragment (row r = 16w+lr,
+// column c = 16cb+lk+4v) is exactly GEMM2's A fragment for k-step 4cb+v.
+// The four waves' per-slice partials meet in LDS; with one buffer per slice
+// the slice loop has no workgroup barrier at all.
 // Matern32: r~2_b uses the gradient-indexed weights, which equal slice b+1's
 // kernel weights (Q1), so the factor 1 + sqrt3 t of slice b+1 is cached per
 // pair; the last slice gets its own GEMM with wg[B-1].
 // ---------------------------------------------------------------------------
-template <int PM>
-__device__ __forceinline__ void gemm1_mm(const double *sXJ, const double *__restrict__ xrow,
-                                         const double *sw, int lr, int lk, d4 (&acc)[4]) {
-  constexpr int XP = PM + 1;
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb) acc[cb] = d4{0.0, 0.0, 0.0, 0.0};
-  // one k-step of operands in flight (explicit prefetch; the scheduling
-  // barrier keeps the compiler from hoisting every load of the loop)
-  double an[4];
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb) an[cb] = sXJ[(16 * cb + lr) * XP + lk];
-  double xn = xrow[lk];
-#pragma unroll
-  for (int kk = 0; kk < PM / 4; ++kk) {
-    double ac[4];
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) ac[cb] = an[cb];
-    const double bop = xn * sw[4 * kk + lk];
-    if (kk + 1 < PM / 4) {
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) an[cb] = sXJ[(16 * cb + lr) * XP + 4 * (kk + 1) + lk];
-      xn = xrow[4 * (kk + 1) + lk];
-    }
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
-      acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[cb], bop, acc[cb], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-// s_b of the 64 columns (threads 0..63, from LDS) and of the 64 rows
-// (threads 64..127, from global X) into sSc / sSr.
-template <int PM>
-__device__ __forceinline__ void slice_norms(const double *sXJ, const double *__restrict__ X,
-                                            int64_t R0, const double *sw, int tid, double *sSc,
-                                            double *sSr) {
-  constexpr int XP = PM + 1;
-  if (tid < 64) {
-    double s = 0.0;
-    for (int i = 0; i < PM; ++i) {
-      const double x = sXJ[tid * XP + i];
-      s = fma(x * x, sw[i], s);
-    }
-    sSc[tid] = s;
-  } else if (tid < 128) {
-    const double *xr = X + (R0 + tid - 64) * PM;
-    double s = 0.0;
-    for (int i = 0; i < PM; ++i) {
-      const double x = xr[i];
-      s = fma(x * x, sw[i], s);
-    }
-    sSr[tid - 64] = s;
-  }
-}
-
 __device__ __forceinline__ double rcp_nr_mm(double f) {
   double q = __builtin_amdgcn_rcp(f);
   double e = fma(-f, q, 1.0);
@@ -263,16 +396,15 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
                                                  double *__restrict__ gpart,
                                                  double *__restrict__ trpart, int64_t ntiles,
                                                  const Tile *__restrict__ tiles, int G) {
-  constexpr int XP = PM + 1;
+  constexpr int XP = mm_table_width(PM, true) + 1;
+  constexpr bool B2 = XP > PM + 1;           // x^2 staged beside x
+  constexpr bool XIL = PM <= 32;             // row covariates staged in LDS
   constexpr int NV = PM + 1;
-  constexpr int NB2 = (PM + 1 + 15) / 16;    // GEMM2 column blocks: [x | 1]
-  constexpr int NBR = PM / 16, LRR = PM % 16;  // where R_r lands
-  constexpr int UP = 65;                       // sU pitch
-  __shared__ double sXJ[64 * XP];
-  __shared__ double sU[64 * UP];
-  __shared__ double sSc[64], sSr[64], sZc[64], sLZc[64], sC[4][64];
-  __shared__ double sW[PM];
-  __shared__ double sRed[4][NB2 * 16 + 1];
+  constexpr int NC2 = 2 * PM;                // GEMM2 columns [x | x^2]
+  constexpr int NQ = (NC2 + 15) / 16;        // 16-wide column blocks
+  constexpr int QG = NQ >= 6 ? 2 : (NQ < ACE_MM_QG ? NQ : ACE_MM_QG);  // blocks per k-loop pass
+  constexpr int RS = NC2 + 1;                // partial row: [x part | x^2 part | T K]
+  extern __shared__ __attribute__((aligned(16))) double lds[];
   const int64_t t = blockIdx.x;
   int64_t I, J;
   tile_of(tiles, t, I, J);
@@ -280,82 +412,73 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
   const int64_t R0 = I * AT, C0 = J * AT, n = S.n;
-  const int64_t r = R0 + 16 * w + lr;
+  const int rl = 16 * w + lr;
+  const int64_t r = R0 + rl;
   const bool rvalid = r < n;
-  const double *xrow = S.X + r * PM;
-  for (int e = tid; e < 64 * PM; e += 256) {
-    const int c = e / PM, i = e - c * PM;
-    sXJ[c * XP + i] = S.X[(C0 + c) * PM + i];
-  }
+  const double *wlast = (KIND == 1) ? tab.wg + (B - 1) * PM : tab.wk;
+  const MmLds L = mm_stage<PM, KIND, XP, true>(lds, S, B, ZS, tab.wk, wlast, R0, C0, tid);
   // T = w_rc (sA A[r,c] - alpha_r alpha_c), w = 2 off the diagonal (lower pairs)
   const double ar = rvalid ? alpha[r] : 0.0;
   double tv[4][4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int64_t c = C0 + 16 * cb + lk + 4 * v;
+      tv[cb][v] = (rvalid && c < n && !(I == J && c > r)) ? sA * A[r + c * ld] - ar * alpha[c] : 0.0;
+    }
   double tr = 0.0;
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int64_t c = C0 + 16 * cb + lk + 4 * v;
-      double x = 0.0;
-      if (rvalid && c < n && !(I == J && c > r)) {
-        x = sA * A[r + c * ld] - ar * alpha[c];
-        if (c == r) tr += x;
-        else x *= 2.0;
-      }
-      tv[cb][v] = x;
+      if (c == r) tr += tv[cb][v];
+      else tv[cb][v] *= 2.0;
     }
+  RowX<PM, XIL> xr;  // x_r from the staged rows when they are in LDS
+  xr.load(XIL ? L.XI + rl * (PM + 1) : S.X + r * PM, lk);
   double fc[4][4];  // Matern: 1 + sqrt3 t of slice b+1
   d4 acc[4];
+  if (KIND == 1) {  // Matern, last slice: r~2 with its own weights
+    gemm1_mm<XP>(L.XJ, xr, L.W + B * PM, lr, lk, acc);
+    const double sr = L.Nr[B * 64 + rl];
+    const double *nc = L.Nc + B * 64;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int cl = 16 * cb + lk + 4 * v;
+        double rt2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), 0.0);
+        if (C0 + cl == r) rt2 = 0.0;
+        fc[cb][v] = 1.0 + sqrt_pk(3.0 * rt2);
+      }
+  }
+  const bool per_slice = L.red_slices == B;
   for (int b = B - 1; b >= 0; --b) {
-    const bool last = (b == B - 1);
-    if (KIND == 1 && last) {  // Matern, last slice: r~2 with its own weights
-      __syncthreads();
-      if (tid < PM) sW[tid] = tab.wg[b * PM + tid];
-      __syncthreads();
-      slice_norms<PM>(sXJ, S.X, R0, sW, tid, sSc, sSr);
-      gemm1_mm<PM>(sXJ, xrow, sW, lr, lk, acc);
-      __syncthreads();
-      const double sr = sSr[16 * w + lr];
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int cl = 16 * cb + lk + 4 * v;
-          double rt2 = fmax(fma(-2.0, acc[cb][v], sr + sSc[cl]), 0.0);
-          if (C0 + cl == r) rt2 = 0.0;
-          fc[cb][v] = 1.0 + sqrt(3.0 * rt2);
-        }
-    }
-    __syncthreads();  // previous users of sW / sSc / sSr / sZc / sU / sRed are done
-    if (tid < PM) sW[tid] = tab.wk[b * PM + tid];
-    if (b > 0 && tid >= 64 && tid < 128) {
-      sZc[tid - 64] = S.Z[(C0 + tid - 64) * ZS + b - 1];
-      if (KIND == 0) sLZc[tid - 64] = S.LZ[(C0 + tid - 64) * ZS + b - 1];
-    }
-    __syncthreads();
-    slice_norms<PM>(sXJ, S.X, R0, sW, tid, sSc, sSr);
-    gemm1_mm<PM>(sXJ, xrow, sW, lr, lk, acc);
-    __syncthreads();  // sSc, sSr, sZc ready
-    const double sr = sSr[16 * w + lr];
-    const double lam = tab.lam[b];
-    double zr = 0.0, lzr = 0.0;
+    double *red = L.Red + (per_slice ? b : (b & 1)) * 4 * RS;
+    double zr = 0.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
     if (b > 0) {
       zr = S.Z[r * ZS + b - 1];
       if (KIND == 0) lzr = S.LZ[r * ZS + b - 1];
     }
-    double gl = 0.0;
+    gemm1_mm<XP>(L.XJ, xr, L.W + b * PM, lr, lk, acc);
+    const double sr = L.Nr[b * 64 + rl];
+    const double *nc = L.Nc + b * 64;
+    const double lam = tab.lam[b];
+    double gl = 0.0, rs = 0.0;
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int cl = 16 * cb + lk + 4 * v;
         const int64_t c = C0 + cl;
-        double r2 = fmax(fma(-2.0, acc[cb][v], sr + sSc[cl]), 0.0);
+        double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), 0.0);
         if (c == r) r2 = 0.0;
         double zc = 0.0, lzc = 0.0;
         if (b > 0) {
-          zc = sZc[cl];
-          if (KIND == 0) lzc = sLZc[cl];
+          zc = L.Z[(b - 1) * 64 + cl];
+          if (KIND == 0) lzc = L.LZ[(b - 1) * 64 + cl];
         }
         const bool rlo = r < c;
         const double zlo = rlo ? zr : zc, zhi = rlo ? zc : zr;
@@ -363,9 +486,9 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
         if (KIND == 0) {
           kb = kval_mm<0>(b, r2, lam, zlo, zhi, rlo ? lzr : lzc, rlo ? lzc : lzr);
         } else {
-          const double tt = sqrt(r2);
+          const double tt = sqrt_pk(r2);
           f = 1.0 + SQRT3 * tt;
-          const double e = f * exp(lam - SQRT3 * tt);
+          const double e = f * exp_pk(lam - SQRT3 * tt);
           kb = (b == 0) ? e : (zlo == 0.0 ? 0.0 : (e * zlo) * zhi);
         }
         const double tk = tv[cb][v] * kb;
@@ -378,42 +501,66 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
           fc[cb][v] = f;
         }
         acc[cb][v] = u;
-        sU[(16 * w + lr) * UP + cl] = u;
-        __builtin_amdgcn_sched_barrier(0);
+        rs += u;
+        MM_PAIR_FENCE(cb, v);
       }
-    // GEMM2 over the column blocks, the block holding R_r first
-    double Rv[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int q = 0; q < NB2; ++q) {
-      const int nb = (q == 0) ? NBR : (q <= NBR ? q - 1 : q);
-      const int nn = 16 * nb + lr;
-      const double bconst = (nn == PM) ? 1.0 : 0.0;
-      const int fo = nn < PM ? nn : 0;
-      d4 a2 = d4{0.0, 0.0, 0.0, 0.0};
-      double xn = sXJ[lk * XP + fo];
+    // R_r: row sums of U over the tile (lanes of one lr hold the 4 quarters)
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    double Rv[4];
 #pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const double x = xn;
-        if (kk + 1 < 16) xn = sXJ[(4 * (kk + 1) + lk) * XP + fo];
-        a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[kk >> 2][kk & 3], nn < PM ? x : bconst,
-                                                  a2, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // a2[v'] = V[r' = R0 + 16 w + lk + 4 v'][nn]
-      if (q == 0) {
+    for (int v = 0; v < 4; ++v) Rv[v] = __shfl(rs, lk + 4 * v, 64);  // row 16w + lk + 4v
+    // GEMM2 over [x | x^2], QG column blocks per pass of the k-loop
 #pragma unroll
-        for (int v = 0; v < 4; ++v) Rv[v] = __shfl(a2[v], lk * 16 + LRR, 64);
-      }
-      double part = 0.0;
-      if (nn < PM) {
+    for (int q0 = 0; q0 < NQ; q0 += QG) {
+      d4 a2[QG];
+      int fo[QG];
+      bool sq[QG];
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const double x = S.X[(R0 + 16 * w + lk + 4 * v) * PM + nn];
-          part += fma(x * x, Rv[v], -2.0 * x * a2[v]);
+      for (int j = 0; j < QG; ++j) {
+        a2[j] = d4{0.0, 0.0, 0.0, 0.0};
+        const int nn = 16 * (q0 + j) + lr;
+        if (B2) {  // [x | x^2] staged: column nn of the table
+          sq[j] = false;
+          fo[j] = nn < NC2 ? nn : 0;
+        } else {   // PM % 16 == 0: whole blocks are x or x^2
+          sq[j] = q0 + j >= PM / 16;
+          fo[j] = sq[j] ? (nn < NC2 ? nn - PM : 0) : nn;
         }
       }
-      part += __shfl_xor(part, 16, 64);
-      part += __shfl_xor(part, 32, 64);
-      if (lk == 0) sRed[w][nn] = part;
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const double *xc = L.XJ + (4 * kk + lk) * XP;
+#pragma unroll
+        for (int j = 0; j < QG; ++j) {
+          if (q0 + j < NQ) {
+            const double x = xc[fo[j]];
+            a2[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[kk >> 2][kk & 3], sq[j] ? x * x : x,
+                                                         a2[j], 0, 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // a2[j][v] = V[row 16 w + lk + 4 v][column 16 (q0 + j) + lr]
+#pragma unroll
+      for (int j = 0; j < QG; ++j) {
+        if (q0 + j >= NQ) continue;
+        const int nn = 16 * (q0 + j) + lr;
+        double part = 0.0;
+        if (nn < PM) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int rr = 16 * w + lk + 4 * v;
+            const double x = XIL ? L.XI[rr * (PM + 1) + nn] : S.X[(R0 + rr) * PM + nn];
+            part += fma(x * x, Rv[v], -2.0 * x * a2[j][v]);
+          }
+        } else {
+          part = (a2[j][0] + a2[j][1]) + (a2[j][2] + a2[j][3]);
+        }
+        part += __shfl_xor(part, 16, 64);
+        part += __shfl_xor(part, 32, 64);
+        if (lk == 0 && nn < NC2) red[w * RS + nn] = part;
+      }
     }
     gl += __shfl_xor(gl, 1, 64);
     gl += __shfl_xor(gl, 2, 64);
@@ -421,29 +568,18 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
     gl += __shfl_xor(gl, 8, 64);
     gl += __shfl_xor(gl, 16, 64);
     gl += __shfl_xor(gl, 32, 64);
-    if (lane == 0) sRed[w][NB2 * 16] = gl;
-    __syncthreads();  // sU, sRed complete
-    {  // column sums of U: thread (quarter q, column c) over 16 rows
-      const int c = tid & 63, qq = tid >> 6;
-      double s = 0.0;
+    if (lane == 0) red[w * RS + NC2] = gl;
+    if (!per_slice) {
+      __syncthreads();  // the four waves' partials of slice b are in red
+      if (tid < PM) {
+        double g = 0.0;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) s += sU[(16 * qq + k) * UP + c];
-      sC[qq][c] = s;
-    }
-    __syncthreads();
-    if (tid < PM) {
-      double g = 0.0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) g += sRed[q][tid];
-      double gc = 0.0;
-      for (int c = 0; c < 64; ++c) {
-        const double x = sXJ[c * XP + tid];
-        gc = fma(x * x, (sC[0][c] + sC[1][c]) + (sC[2][c] + sC[3][c]), gc);
+        for (int q = 0; q < 4; ++q) g += red[q * RS + tid] + red[q * RS + PM + tid];
+        gpart[((int64_t)b * NV + tid) * ntiles + t] = g;
+      } else if (tid == PM) {
+        const double g = (red[NC2] + red[RS + NC2]) + (red[2 * RS + NC2] + red[3 * RS + NC2]);
+        gpart[((int64_t)b * NV + PM) * ntiles + t] = g;
       }
-      gpart[((int64_t)b * NV + tid) * ntiles + t] = g + gc;
-    } else if (tid == PM) {
-      const double g = (sRed[0][NB2 * 16] + sRed[1][NB2 * 16]) + (sRed[2][NB2 * 16] + sRed[3][NB2 * 16]);
-      gpart[((int64_t)b * NV + PM) * ntiles + t] = g;
     }
   }
   // trace of T
@@ -453,10 +589,25 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
   tr += __shfl_xor(tr, 8, 64);
   tr += __shfl_xor(tr, 16, 64);
   tr += __shfl_xor(tr, 32, 64);
+  double *str = L.Red + L.red_slices * 4 * RS;
+  if (lane == 0) str[w] = tr;
   __syncthreads();
-  if (lane == 0) sSr[w] = tr;
-  __syncthreads();
-  if (tid == 0) trpart[t] = (sSr[0] + sSr[1]) + (sSr[2] + sSr[3]);
+  if (per_slice) {  // all slices' partials at once
+    for (int e = tid; e < B * NV; e += 256) {
+      const int bb = e / NV, i = e - bb * NV;
+      const double *red = L.Red + bb * 4 * RS;
+      double g;
+      if (i < PM) {
+        g = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g += red[q * RS + i] + red[q * RS + PM + i];
+      } else {
+        g = (red[NC2] + red[RS + NC2]) + (red[2 * RS + NC2] + red[3 * RS + NC2]);
+      }
+      gpart[((int64_t)bb * NV + i) * ntiles + t] = g;
+    }
+  }
+  if (tid == 0) trpart[t] = (str[0] + str[1]) + (str[2] + str[3]);
 }
 
 template <int PM>
@@ -467,13 +618,26 @@ static hipError_t grad_mm_pm(int kind, PairSide S, int B, int ZS, TabView tab, c
   const int64_t nt = (S.n + AT - 1) / AT;
   const int64_t nblk = tiles ? ntiles : nt * (nt + 1) / 2;
   if (nblk == 0) return hipSuccess;
+  const size_t lds = (size_t)mm_layout(PM, B, kind == 0 ? 0 : 1, true).total * sizeof(double);
+  if (lds > 65536) {
+    const void *f = kind == 0 ? (const void *)k_grad_mm<PM, 0> : (const void *)k_grad_mm<PM, 1>;
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   if (kind == 0)
-    hipLaunchKernelGGL((k_grad_mm<PM, 0>), dim3((unsigned)nblk), dim3(256), 0, st, S, B, ZS, tab,
-                       A, ld, sA, alpha, gpart, trpart, nblk, tiles, G);
+    hipLaunchKernelGGL((k_grad_mm<PM, 0>), dim3((unsigned)nblk), dim3(256), lds, st, S, B, ZS,
+                       tab, A, ld, sA, alpha, gpart, trpart, nblk, tiles, G);
   else
-    hipLaunchKernelGGL((k_grad_mm<PM, 1>), dim3((unsigned)nblk), dim3(256), 0, st, S, B, ZS, tab,
-                       A, ld, sA, alpha, gpart, trpart, nblk, tiles, G);
+    hipLaunchKernelGGL((k_grad_mm<PM, 1>), dim3((unsigned)nblk), dim3(256), lds, st, S, B, ZS,
+                       tab, A, ld, sA, alpha, gpart, trpart, nblk, tiles, G);
   return hipGetLastError();
+}
+
+// Whether the per-tile staging of the MFMA kernels fits the LDS budget
+// (two workgroups per CU); above it the VALU kernels take over.
+bool mm_lds_ok(int PM, int B, int kind, bool grad) {
+  return (int64_t)mm_layout(PM, B, kind == 0 ? 0 : 1, grad).total * (int64_t)sizeof(double) <=
+         80 * 1024;
 }
 
 hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
@@ -498,12 +662,18 @@ static hipError_t asm_mm_pm(int kind, PairSide S, int64_t npad, int B, int ZS, T
   const int64_t nt = npad / AT;
   const int64_t nblk = tiles ? ntiles : nt * (nt + 1) / 2;
   if (nblk == 0) return hipSuccess;
+  const size_t lds = (size_t)mm_layout(PM, B, kind == 0 ? 0 : 1, false).total * sizeof(double);
+  if (lds > 65536) {
+    const void *f = kind == 0 ? (const void *)k_asm_mm<PM, 0> : (const void *)k_asm_mm<PM, 1>;
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   if (kind == 0)
-    hipLaunchKernelGGL((k_asm_mm<PM, 0>), dim3((unsigned)nblk), dim3(256), 0, st, S, B, ZS, tab,
-                       sig, out, ld, kcopy, tiles, G);
+    hipLaunchKernelGGL((k_asm_mm<PM, 0>), dim3((unsigned)nblk), dim3(256), lds, st, S, B, ZS,
+                       tab, sig, out, ld, kcopy, tiles, G);
   else
-    hipLaunchKernelGGL((k_asm_mm<PM, 1>), dim3((unsigned)nblk), dim3(256), 0, st, S, B, ZS, tab,
-                       sig, out, ld, kcopy, tiles, G);
+    hipLaunchKernelGGL((k_asm_mm<PM, 1>), dim3((unsigned)nblk), dim3(256), lds, st, S, B, ZS,
+                       tab, sig, out, ld, kcopy, tiles, G);
   return hipGetLastError();
 }
 
