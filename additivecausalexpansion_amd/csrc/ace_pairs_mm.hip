@@ -32,6 +32,10 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 #ifndef ACE_MM_PG
 #define ACE_MM_PG 2
 #endif
+// Waves per SIMD the 512-thread gradient kernel is compiled for (register cap).
+#ifndef ACE_MM_GRAD_WPE
+#define ACE_MM_GRAD_WPE 4
+#endif
 // Most GEMM2 column blocks accumulated per pass of its k-loop.
 #ifndef ACE_MM_QG
 #define ACE_MM_QG 4
@@ -48,28 +52,58 @@ __device__ __forceinline__ double sgn_mm(double x) {
 
 // exp(x) without the library's special-case handling: every argument here is
 // lam - r2 (+ log|z| terms) or lam - sqrt3 t, finite and bounded above by the
-// amplitude parameter.  Cody-Waite reduction x = k ln2 + r, |r| <= ln2/2, and
-// the degree-12 Taylor polynomial (truncation < 2e-16 relative), then
-// ldexp; arguments below -745 give 0 like exp().
-__device__ __forceinline__ double exp_pk(double x) {
+// amplitude parameter.  x = (32 m + j) ln2/32 + r, |r| <= ln2/64:
+// exp(x) = 2^m * 2^(j/32) * p(r), p the degree-6 Taylor polynomial
+// (truncation < 4e-18), 2^(j/32) from a 32-entry LDS table (correctly
+// rounded by the host's pow).  Arguments below -745 give 0 like exp().
+__device__ const double kExp2Tab[32] = {
+    1,
+    1.0218971486541166,
+    1.0442737824274138,
+    1.0671404006768237,
+    1.0905077326652577,
+    1.1143867425958924,
+    1.1387886347566916,
+    1.1637248587775775,
+    1.189207115002721,
+    1.215247359980469,
+    1.241857812073484,
+    1.2690509571917332,
+    1.2968395546510096,
+    1.3252366431597413,
+    1.3542555469368927,
+    1.383909881963832,
+    1.4142135623730951,
+    1.4451808069770467,
+    1.4768261459394993,
+    1.5091644275934228,
+    1.5422108254079407,
+    1.5759808451078865,
+    1.6104903319492543,
+    1.6457554781539649,
+    1.681792830507429,
+    1.7186192981224779,
+    1.7562521603732995,
+    1.7947090750031072,
+    1.8340080864093424,
+    1.8741676341103,
+    1.9152065613971474,
+    1.9571441241754002};
+
+__device__ __forceinline__ double exp_tb(double x, const double *tab) {
   x = fmax(x, -745.2);
-  const double kf = __builtin_rint(x * 1.4426950408889634);
-  double r = fma(-kf, 6.93147180369123816490e-01, x);
-  r = fma(-kf, 1.90821492927058770002e-10, r);
-  double q = 2.08767569878680989792e-09;   // 1/12!
-  q = fma(q, r, 2.50521083854417187751e-08);  // 1/11!
-  q = fma(q, r, 2.75573192239858906526e-07);  // 1/10!
-  q = fma(q, r, 2.75573192239858906526e-06);  // 1/9!
-  q = fma(q, r, 2.48015873015873015873e-05);  // 1/8!
-  q = fma(q, r, 1.98412698412698412698e-04);  // 1/7!
-  q = fma(q, r, 1.38888888888888888889e-03);  // 1/6!
-  q = fma(q, r, 8.33333333333333333333e-03);  // 1/5!
-  q = fma(q, r, 4.16666666666666666667e-02);  // 1/4!
-  q = fma(q, r, 1.66666666666666666667e-01);  // 1/3!
+  const double kf = __builtin_rint(x * 46.16624130844683);  // 32 / ln2
+  double r = fma(-kf, 0.02166084938653512, x);               // (ln2 / 32) hi
+  r = fma(-kf, 5.9631716539705866e-12, r);                   // (ln2 / 32) lo
+  const int ki = (int)kf;
+  double q = 1.0 / 720.0;
+  q = fma(q, r, 1.0 / 120.0);
+  q = fma(q, r, 1.0 / 24.0);
+  q = fma(q, r, 1.0 / 6.0);
   q = fma(q, r, 0.5);
   q = fma(q, r, 1.0);
   q = fma(q, r, 1.0);
-  return __builtin_amdgcn_ldexp(q, (int)kf);
+  return __builtin_amdgcn_ldexp(q * tab[ki & 31], ki >> 5);
 }
 
 // sqrt(x), x >= 0 and normal or 0 (r2 values): hardware rsq + the
@@ -92,14 +126,14 @@ __device__ __forceinline__ double sqrt_pk(double x) {
 //  SE  (src/kernel_SE_cpp.cpp:96, 119), Matern32 (src/kernel_Matern_cpp.cpp:217-227).
 template <int KIND>
 __device__ __forceinline__ double kval_mm(int b, double r2, double lam, double zlo, double zhi,
-                                          double lzlo, double lzhi) {
+                                          double lzlo, double lzhi, const double *etab) {
   if (KIND == 0) {
-    if (b == 0) return exp_pk(lam - r2);
+    if (b == 0) return exp_tb(lam - r2, etab);
     if (zlo == 0.0 || zhi == 0.0) return 0.0;
-    return (sgn_mm(zlo) * sgn_mm(zhi)) * exp_pk(((lam - r2) + lzlo) + lzhi);
+    return (sgn_mm(zlo) * sgn_mm(zhi)) * exp_tb(((lam - r2) + lzlo) + lzhi, etab);
   } else {
     const double t = sqrt_pk(r2);
-    const double e = (1.0 + SQRT3 * t) * exp_pk(lam - SQRT3 * t);
+    const double e = (1.0 + SQRT3 * t) * exp_tb(lam - SQRT3 * t, etab);
     if (b == 0) return e;
     if (zlo == 0.0) return 0.0;
     return (e * zlo) * zhi;
@@ -137,7 +171,7 @@ __device__ __forceinline__ void tile_of(const Tile *tiles, int64_t t, int64_t &I
 // load is issued ahead of each slice's GEMM1.
 // ---------------------------------------------------------------------------
 struct MmLayout {
-  int xj, xi, z, lz, nc, nr, w, red, red_slices, total;
+  int etab, xj, xi, z, lz, nc, nr, w, red, red_slices, total;
 };
 
 // Width of the staged covariate table: the gradient of a PM that is not a
@@ -149,10 +183,12 @@ __host__ __device__ constexpr int mm_table_width(int PM, bool grad) {
 
 // Gradient partials: one buffer per slice (no barrier inside the slice
 // loop) when that fits in 16 KB, else two buffers and a barrier per slice.
-__host__ __device__ inline MmLayout mm_layout(int PM, int B, int KIND, bool grad) {
+__host__ __device__ inline MmLayout mm_layout(int PM, int B, int KIND, bool grad, int nwave = 4) {
   MmLayout o;
   const int NS = (grad && KIND == 1) ? B + 1 : B;
   int off = 0;
+  o.etab = off;
+  off += 32;
   o.xj = off;
   off += 64 * (mm_table_width(PM, grad) + 1);
   o.xi = off;
@@ -170,28 +206,29 @@ __host__ __device__ inline MmLayout mm_layout(int PM, int B, int KIND, bool grad
   o.red = off;
   o.red_slices = 0;
   if (grad) {
-    const int per = 4 * (2 * PM + 1);
+    const int per = nwave * (2 * PM + 1);
     o.red_slices = (B * per * 8 <= 16 * 1024) ? B : 2;
-    off += o.red_slices * per + 4;
+    off += o.red_slices * per + nwave;
   }
   o.total = off;
   return o;
 }
 
 struct MmLds {
-  double *XJ, *XI, *Z, *LZ, *Nc, *Nr, *W, *Red;
+  double *E, *XJ, *XI, *Z, *LZ, *Nc, *Nr, *W, *Red;
   int red_slices;
 };
 
-template <int PM, int KIND, int XP, bool GRAD>
+template <int PM, int KIND, int XP, bool GRAD, int NT = 256>
 __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS,
                                           const double *__restrict__ wk,
                                           const double *__restrict__ wlast, int64_t R0,
                                           int64_t C0, int tid) {
-  const MmLayout o = mm_layout(PM, B, KIND, GRAD);
+  const MmLayout o = mm_layout(PM, B, KIND, GRAD, NT / 64);
   const int NS = (GRAD && KIND == 1) ? B + 1 : B;
   constexpr bool XI = GRAD && PM <= 32;
   MmLds L;
+  L.E = lds + o.etab;
   L.XJ = lds + o.xj;
   L.XI = lds + o.xi;
   L.Z = lds + o.z;
@@ -201,23 +238,24 @@ __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS
   L.W = lds + o.w;
   L.Red = lds + o.red;
   L.red_slices = o.red_slices;
-  for (int e = tid; e < 64 * PM; e += 256) {
+  for (int e = tid; e < 64 * PM; e += NT) {
     const int c = e / PM, i = e - c * PM;
     const double x = S.X[(C0 + c) * PM + i];
     L.XJ[c * XP + i] = x;
     if (XP > PM + 1) L.XJ[c * XP + PM + i] = x * x;
     if (XI) L.XI[c * (PM + 1) + i] = S.X[(R0 + c) * PM + i];
   }
-  for (int e = tid; e < (B - 1) * 64; e += 256) {
+  for (int e = tid; e < (B - 1) * 64; e += NT) {
     const int bb = e >> 6, c = e & 63;
     L.Z[e] = S.Z[(C0 + c) * ZS + bb];
     if (KIND == 0) L.LZ[e] = S.LZ[(C0 + c) * ZS + bb];
   }
-  for (int e = tid; e < NS * PM; e += 256) L.W[e] = (e < B * PM) ? wk[e] : wlast[e - B * PM];
+  if (tid < 32) L.E[tid] = kExp2Tab[tid];
+  for (int e = tid; e < NS * PM; e += NT) L.W[e] = (e < B * PM) ? wk[e] : wlast[e - B * PM];
   __syncthreads();
   // norms: task = (side, slice, point), same accumulation order as the
   // per-slice loops they replace (i ascending, fma(x^2, w, s))
-  for (int e = tid; e < 2 * NS * 64; e += 256) {
+  for (int e = tid; e < 2 * NS * 64; e += NT) {
     const int side = e / (NS * 64), rem = e - side * NS * 64;
     const int sl = rem >> 6, pt = rem & 63;
     const double *w = L.W + sl * PM;
@@ -262,30 +300,31 @@ struct RowX {
   }
 };
 
-// GEMM1: acc[cb][v] = sum_i w_i x_ci x_ri for the lane's 16 pairs
-// (row r = 16 w + lr, column c = 16 cb + lk + 4 v); w in LDS.
-template <int XP, int PM, bool FP>
+// GEMM1: acc[cb][v] = sum_i w_i x_ci x_ri for the lane's 4 CB pairs
+// (row r = 16 w + lr, column c = cbase + 16 cb + lk + 4 v); w in LDS.
+template <int XP, int CB = 4, int PM, bool FP>
 __device__ __forceinline__ void gemm1_mm(const double *sXJ, const RowX<PM, FP> &xr, const double *w,
-                                         int lr, int lk, d4 (&acc)[4]) {
+                                         int lr, int lk, d4 (&acc)[CB], int cbase = 0) {
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb) acc[cb] = d4{0.0, 0.0, 0.0, 0.0};
-  double an[4];
+  for (int cb = 0; cb < CB; ++cb) acc[cb] = d4{0.0, 0.0, 0.0, 0.0};
+  const double *xj = sXJ + (cbase + lr) * XP + lk;
+  double an[CB];
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb) an[cb] = sXJ[(16 * cb + lr) * XP + lk];
+  for (int cb = 0; cb < CB; ++cb) an[cb] = xj[16 * cb * XP];
   double bn = xr.at(0, lk) * w[lk];
 #pragma unroll
   for (int kk = 0; kk < PM / 4; ++kk) {
-    double ac[4];
+    double ac[CB];
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) ac[cb] = an[cb];
+    for (int cb = 0; cb < CB; ++cb) ac[cb] = an[cb];
     const double bop = bn;
     if (kk + 1 < PM / 4) {
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) an[cb] = sXJ[(16 * cb + lr) * XP + 4 * (kk + 1) + lk];
+      for (int cb = 0; cb < CB; ++cb) an[cb] = xj[16 * cb * XP + 4 * (kk + 1)];
       bn = xr.at(kk + 1, lk) * w[4 * (kk + 1) + lk];
     }
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
+    for (int cb = 0; cb < CB; ++cb)
       acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[cb], bop, acc[cb], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -347,8 +386,8 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
           zc = L.Z[(b - 1) * 64 + cl];
           if (KIND == 0) lzc = L.LZ[(b - 1) * 64 + cl];
         }
-        const double kb = (r < c) ? kval_mm<KIND>(b, r2, lam, zr, zc, lzr, lzc)
-                                  : kval_mm<KIND>(b, r2, lam, zc, zr, lzc, lzr);
+        const double kb = (r < c) ? kval_mm<KIND>(b, r2, lam, zr, zc, lzr, lzc, L.E)
+                                  : kval_mm<KIND>(b, r2, lam, zc, zr, lzc, lzr, L.E);
         kf[cb][v] += kb;
         MM_PAIR_FENCE(cb, v);
       }
@@ -389,21 +428,34 @@ __device__ __forceinline__ double rcp_nr_mm(double f) {
   return fma(q, e, q);
 }
 
-template <int PM, int KIND>
-__global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, TabView tab,
-                                                 const double *__restrict__ A, int64_t ld,
-                                                 double sA, const double *__restrict__ alpha,
-                                                 double *__restrict__ gpart,
-                                                 double *__restrict__ trpart, int64_t ntiles,
-                                                 const Tile *__restrict__ tiles, int G) {
+// CB = column blocks (16 wide) per wave.  CB = 4: 256 threads, every wave
+// holds 16 rows x 64 columns (16 pairs per lane, 2 workgroups per CU).
+// CB = 2: 512 threads, wave w holds rows 16 (w & 3).., columns 32 (w >> 2)..
+// (8 pairs per lane): half the per-lane state, so twice the waves per SIMD
+// hide the fp64 latencies.
+template <int PM, int KIND, int CB>
+__global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2)) void k_grad_mm(PairSide S, int B, int ZS,
+                                                                  TabView tab,
+                                                                  const double *__restrict__ A,
+                                                                  int64_t ld, double sA,
+                                                                  const double *__restrict__ alpha,
+                                                                  double *__restrict__ gpart,
+                                                                  double *__restrict__ trpart,
+                                                                  int64_t ntiles,
+                                                                  const Tile *__restrict__ tiles,
+                                                                  int G) {
+  constexpr int NT = 64 * 4 * (4 / CB);      // threads
+  constexpr int NWV = NT / 64;               // waves
   constexpr int XP = mm_table_width(PM, true) + 1;
   constexpr bool B2 = XP > PM + 1;           // x^2 staged beside x
   constexpr bool XIL = PM <= 32;             // row covariates staged in LDS
   constexpr int NV = PM + 1;
   constexpr int NC2 = 2 * PM;                // GEMM2 columns [x | x^2]
   constexpr int NQ = (NC2 + 15) / 16;        // 16-wide column blocks
-  constexpr int QG = NQ >= 6 ? 2 : (NQ < ACE_MM_QG ? NQ : ACE_MM_QG);  // blocks per k-loop pass
+  // GEMM2 column blocks per pass of its k-loop (one at CB = 2: register cap)
+  constexpr int QG = CB == 2 ? 1 : (NQ >= 6 ? 2 : (NQ < ACE_MM_QG ? NQ : ACE_MM_QG));
   constexpr int RS = NC2 + 1;                // partial row: [x part | x^2 part | T K]
+  constexpr int NKK = 4 * CB;                // GEMM2 k-steps (the wave's columns / 4)
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int64_t t = blockIdx.x;
   int64_t I, J;
@@ -411,84 +463,86 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
   if (G > 1) A += (lcol(J * AT, G) - J * AT) * ld;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
+  const int wr = w & 3;                      // row block of the wave
+  const int cbase = 16 * CB * (w >> 2);      // first column of the wave
   const int64_t R0 = I * AT, C0 = J * AT, n = S.n;
-  const int rl = 16 * w + lr;
+  const int rl = 16 * wr + lr;
   const int64_t r = R0 + rl;
   const bool rvalid = r < n;
   const double *wlast = (KIND == 1) ? tab.wg + (B - 1) * PM : tab.wk;
-  const MmLds L = mm_stage<PM, KIND, XP, true>(lds, S, B, ZS, tab.wk, wlast, R0, C0, tid);
+  const MmLds L = mm_stage<PM, KIND, XP, true, NT>(lds, S, B, ZS, tab.wk, wlast, R0, C0, tid);
   // T = w_rc (sA A[r,c] - alpha_r alpha_c), w = 2 off the diagonal (lower pairs)
   const double ar = rvalid ? alpha[r] : 0.0;
-  double tv[4][4];
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int64_t c = C0 + 16 * cb + lk + 4 * v;
-      tv[cb][v] = (rvalid && c < n && !(I == J && c > r)) ? sA * A[r + c * ld] - ar * alpha[c] : 0.0;
-    }
+  double tv[CB][4];
   double tr = 0.0;
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb)
+  for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const int64_t c = C0 + 16 * cb + lk + 4 * v;
-      if (c == r) tr += tv[cb][v];
-      else tv[cb][v] *= 2.0;
+      const int64_t c = C0 + cbase + 16 * cb + lk + 4 * v;
+      double x = 0.0;
+      if (rvalid && c < n && !(I == J && c > r)) {
+        x = sA * A[r + c * ld] - ar * alpha[c];
+        if (c == r) tr += x;
+        else x *= 2.0;
+      }
+      tv[cb][v] = x;
     }
   RowX<PM, XIL> xr;  // x_r from the staged rows when they are in LDS
   xr.load(XIL ? L.XI + rl * (PM + 1) : S.X + r * PM, lk);
-  double fc[4][4];  // Matern: 1 + sqrt3 t of slice b+1
-  d4 acc[4];
+  double fc[CB][4];  // Matern: 1 + sqrt3 t of slice b+1
+  d4 acc[CB];
   if (KIND == 1) {  // Matern, last slice: r~2 with its own weights
-    gemm1_mm<XP>(L.XJ, xr, L.W + B * PM, lr, lk, acc);
+    gemm1_mm<XP, CB>(L.XJ, xr, L.W + B * PM, lr, lk, acc, cbase);
     const double sr = L.Nr[B * 64 + rl];
-    const double *nc = L.Nc + B * 64;
+    const double *nc = L.Nc + B * 64 + cbase;
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
+    for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int cl = 16 * cb + lk + 4 * v;
         double rt2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), 0.0);
-        if (C0 + cl == r) rt2 = 0.0;
+        if (C0 + cbase + cl == r) rt2 = 0.0;
         fc[cb][v] = 1.0 + sqrt_pk(3.0 * rt2);
       }
   }
   const bool per_slice = L.red_slices == B;
   for (int b = B - 1; b >= 0; --b) {
-    double *red = L.Red + (per_slice ? b : (b & 1)) * 4 * RS;
+    double *red = L.Red + (per_slice ? b : (b & 1)) * NWV * RS;
     double zr = 0.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
     if (b > 0) {
       zr = S.Z[r * ZS + b - 1];
       if (KIND == 0) lzr = S.LZ[r * ZS + b - 1];
     }
-    gemm1_mm<XP>(L.XJ, xr, L.W + b * PM, lr, lk, acc);
+    gemm1_mm<XP, CB>(L.XJ, xr, L.W + b * PM, lr, lk, acc, cbase);
     const double sr = L.Nr[b * 64 + rl];
-    const double *nc = L.Nc + b * 64;
+    const double *nc = L.Nc + b * 64 + cbase;
+    const double *zcol = L.Z + (b - 1) * 64 + cbase;
+    const double *lzcol = L.LZ + (b - 1) * 64 + cbase;
     const double lam = tab.lam[b];
     double gl = 0.0, rs = 0.0;
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
+    for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int cl = 16 * cb + lk + 4 * v;
-        const int64_t c = C0 + cl;
+        const int64_t c = C0 + cbase + cl;
         double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), 0.0);
         if (c == r) r2 = 0.0;
         double zc = 0.0, lzc = 0.0;
         if (b > 0) {
-          zc = L.Z[(b - 1) * 64 + cl];
-          if (KIND == 0) lzc = L.LZ[(b - 1) * 64 + cl];
+          zc = zcol[cl];
+          if (KIND == 0) lzc = lzcol[cl];
         }
         const bool rlo = r < c;
         const double zlo = rlo ? zr : zc, zhi = rlo ? zc : zr;
         double kb, f = 1.0;
         if (KIND == 0) {
-          kb = kval_mm<0>(b, r2, lam, zlo, zhi, rlo ? lzr : lzc, rlo ? lzc : lzr);
+          kb = kval_mm<0>(b, r2, lam, zlo, zhi, rlo ? lzr : lzc, rlo ? lzc : lzr, L.E);
         } else {
           const double tt = sqrt_pk(r2);
           f = 1.0 + SQRT3 * tt;
-          const double e = f * exp_pk(lam - SQRT3 * tt);
+          const double e = f * exp_tb(lam - SQRT3 * tt, L.E);
           kb = (b == 0) ? e : (zlo == 0.0 ? 0.0 : (e * zlo) * zhi);
         }
         const double tk = tv[cb][v] * kb;
@@ -504,12 +558,12 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
         rs += u;
         MM_PAIR_FENCE(cb, v);
       }
-    // R_r: row sums of U over the tile (lanes of one lr hold the 4 quarters)
+    // R_r: row sums of U over the wave's columns (lanes of one lr hold the 4 quarters)
     rs += __shfl_xor(rs, 16, 64);
     rs += __shfl_xor(rs, 32, 64);
     double Rv[4];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) Rv[v] = __shfl(rs, lk + 4 * v, 64);  // row 16w + lk + 4v
+    for (int v = 0; v < 4; ++v) Rv[v] = __shfl(rs, lk + 4 * v, 64);  // row 16 wr + lk + 4v
     // GEMM2 over [x | x^2], QG column blocks per pass of the k-loop
 #pragma unroll
     for (int q0 = 0; q0 < NQ; q0 += QG) {
@@ -529,8 +583,8 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
         }
       }
 #pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const double *xc = L.XJ + (4 * kk + lk) * XP;
+      for (int kk = 0; kk < NKK; ++kk) {
+        const double *xc = L.XJ + (cbase + 4 * kk + lk) * XP;
 #pragma unroll
         for (int j = 0; j < QG; ++j) {
           if (q0 + j < NQ) {
@@ -541,7 +595,7 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      // a2[j][v] = V[row 16 w + lk + 4 v][column 16 (q0 + j) + lr]
+      // a2[j][v] = V[row 16 wr + lk + 4 v][column 16 (q0 + j) + lr]
 #pragma unroll
       for (int j = 0; j < QG; ++j) {
         if (q0 + j >= NQ) continue;
@@ -550,7 +604,7 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
         if (nn < PM) {
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
-            const int rr = 16 * w + lk + 4 * v;
+            const int rr = 16 * wr + lk + 4 * v;
             const double x = XIL ? L.XI[rr * (PM + 1) + nn] : S.X[(R0 + rr) * PM + nn];
             part += fma(x * x, Rv[v], -2.0 * x * a2[j][v]);
           }
@@ -570,15 +624,17 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
     gl += __shfl_xor(gl, 32, 64);
     if (lane == 0) red[w * RS + NC2] = gl;
     if (!per_slice) {
-      __syncthreads();  // the four waves' partials of slice b are in red
-      if (tid < PM) {
+      __syncthreads();  // the waves' partials of slice b are in red
+      if (tid <= PM) {
         double g = 0.0;
+        if (tid < PM) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) g += red[q * RS + tid] + red[q * RS + PM + tid];
+          for (int q = 0; q < NWV; ++q) g += red[q * RS + tid] + red[q * RS + PM + tid];
+        } else {
+#pragma unroll
+          for (int q = 0; q < NWV; ++q) g += red[q * RS + NC2];
+        }
         gpart[((int64_t)b * NV + tid) * ntiles + t] = g;
-      } else if (tid == PM) {
-        const double g = (red[NC2] + red[RS + NC2]) + (red[2 * RS + NC2] + red[3 * RS + NC2]);
-        gpart[((int64_t)b * NV + PM) * ntiles + t] = g;
       }
     }
   }
@@ -589,25 +645,59 @@ __global__ __launch_bounds__(256, 2) void k_grad_mm(PairSide S, int B, int ZS, T
   tr += __shfl_xor(tr, 8, 64);
   tr += __shfl_xor(tr, 16, 64);
   tr += __shfl_xor(tr, 32, 64);
-  double *str = L.Red + L.red_slices * 4 * RS;
+  double *str = L.Red + L.red_slices * NWV * RS;
   if (lane == 0) str[w] = tr;
   __syncthreads();
   if (per_slice) {  // all slices' partials at once
-    for (int e = tid; e < B * NV; e += 256) {
+    for (int e = tid; e < B * NV; e += NT) {
       const int bb = e / NV, i = e - bb * NV;
-      const double *red = L.Red + bb * 4 * RS;
-      double g;
+      const double *red = L.Red + bb * NWV * RS;
+      double g = 0.0;
       if (i < PM) {
-        g = 0.0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) g += red[q * RS + i] + red[q * RS + PM + i];
+        for (int q = 0; q < NWV; ++q) g += red[q * RS + i] + red[q * RS + PM + i];
       } else {
-        g = (red[NC2] + red[RS + NC2]) + (red[2 * RS + NC2] + red[3 * RS + NC2]);
+#pragma unroll
+        for (int q = 0; q < NWV; ++q) g += red[q * RS + NC2];
       }
       gpart[((int64_t)bb * NV + i) * ntiles + t] = g;
     }
   }
-  if (tid == 0) trpart[t] = (str[0] + str[1]) + (str[2] + str[3]);
+  if (tid == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < NWV; ++q) s += str[q];
+    trpart[t] = s;
+  }
+}
+
+// Column blocks per wave of the gradient kernel: CB = 2 (512 threads, 8
+// pairs per lane, 4 waves per SIMD) wherever it fits 128 VGPRs without
+// spilling -- every SE case and Matern up to PM = 32 -- else CB = 4.
+// ACE_MM_GRAD_CB=4 forces the 256-thread form (A/B switch).
+#ifndef ACE_MM_GRAD_CB
+#define ACE_MM_GRAD_CB 2
+#endif
+__host__ __device__ constexpr int grad_cb(int PM, int kind) {
+  return (ACE_MM_GRAD_CB == 2 && (kind == 0 || PM <= 32)) ? 2 : 4;
+}
+
+template <int PM, int KIND>
+static hipError_t grad_mm_launch(PairSide S, int B, int ZS, TabView tab, const double *A,
+                                 int64_t ld, double sA, const double *alpha, double *gpart,
+                                 double *trpart, hipStream_t st, const Tile *tiles,
+                                 int64_t nblk, int G) {
+  constexpr int CB = grad_cb(PM, KIND);
+  constexpr int NT = 64 * 4 * (4 / CB);
+  const size_t lds = (size_t)mm_layout(PM, B, KIND, true, NT / 64).total * sizeof(double);
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute((const void *)k_grad_mm<PM, KIND, CB>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((k_grad_mm<PM, KIND, CB>), dim3((unsigned)nblk), dim3(NT), lds, st, S, B, ZS,
+                     tab, A, ld, sA, alpha, gpart, trpart, nblk, tiles, G);
+  return hipGetLastError();
 }
 
 template <int PM>
@@ -618,25 +708,18 @@ static hipError_t grad_mm_pm(int kind, PairSide S, int B, int ZS, TabView tab, c
   const int64_t nt = (S.n + AT - 1) / AT;
   const int64_t nblk = tiles ? ntiles : nt * (nt + 1) / 2;
   if (nblk == 0) return hipSuccess;
-  const size_t lds = (size_t)mm_layout(PM, B, kind == 0 ? 0 : 1, true).total * sizeof(double);
-  if (lds > 65536) {
-    const void *f = kind == 0 ? (const void *)k_grad_mm<PM, 0> : (const void *)k_grad_mm<PM, 1>;
-    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
-  if (kind == 0)
-    hipLaunchKernelGGL((k_grad_mm<PM, 0>), dim3((unsigned)nblk), dim3(256), lds, st, S, B, ZS,
-                       tab, A, ld, sA, alpha, gpart, trpart, nblk, tiles, G);
-  else
-    hipLaunchKernelGGL((k_grad_mm<PM, 1>), dim3((unsigned)nblk), dim3(256), lds, st, S, B, ZS,
-                       tab, A, ld, sA, alpha, gpart, trpart, nblk, tiles, G);
-  return hipGetLastError();
+  return kind == 0 ? grad_mm_launch<PM, 0>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st,
+                                           tiles, nblk, G)
+                   : grad_mm_launch<PM, 1>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st,
+                                           tiles, nblk, G);
 }
 
 // Whether the per-tile staging of the MFMA kernels fits the LDS budget
 // (two workgroups per CU); above it the VALU kernels take over.
 bool mm_lds_ok(int PM, int B, int kind, bool grad) {
-  return (int64_t)mm_layout(PM, B, kind == 0 ? 0 : 1, grad).total * (int64_t)sizeof(double) <=
+  const int nwave = grad ? 4 * (4 / grad_cb(PM, kind)) : 4;
+  return (int64_t)mm_layout(PM, B, kind == 0 ? 0 : 1, grad, nwave).total *
+             (int64_t)sizeof(double) <=
          80 * 1024;
 }
 
