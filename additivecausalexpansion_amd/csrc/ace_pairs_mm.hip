@@ -174,15 +174,10 @@ struct MmLayout {
   int etab, xj, xi, z, lz, nc, nr, w, red, red_slices, total;
 };
 
-// Width of the staged covariate table: the gradient of a PM that is not a
-// multiple of 16 stages [x | x^2] (GEMM2's B operand, whose 16-wide column
-// blocks then mix the two halves); otherwise x only.
-__host__ __device__ constexpr int mm_table_width(int PM, bool grad) {
-  return (grad && PM % 16 != 0) ? 2 * PM : PM;
-}
-
 // Gradient partials: one buffer per slice (no barrier inside the slice
-// loop) when that fits in 16 KB, else two buffers and a barrier per slice.
+// loop) when that fits in 40 KB, else two buffers and a barrier per slice.
+// Per slice: [NWV][PM + 1] (x part of every feature, sum T K) and the
+// column sums of U of the four row blocks, [4][64].
 __host__ __device__ inline MmLayout mm_layout(int PM, int B, int KIND, bool grad, int nwave = 4) {
   MmLayout o;
   const int NS = (grad && KIND == 1) ? B + 1 : B;
@@ -190,7 +185,7 @@ __host__ __device__ inline MmLayout mm_layout(int PM, int B, int KIND, bool grad
   o.etab = off;
   off += 32;
   o.xj = off;
-  off += 64 * (mm_table_width(PM, grad) + 1);
+  off += 64 * (PM + 1);
   o.xi = off;
   if (grad && PM <= 32) off += 64 * (PM + 1);
   o.z = off;
@@ -206,8 +201,8 @@ __host__ __device__ inline MmLayout mm_layout(int PM, int B, int KIND, bool grad
   o.red = off;
   o.red_slices = 0;
   if (grad) {
-    const int per = nwave * (2 * PM + 1);
-    o.red_slices = (B * per * 8 <= 16 * 1024) ? B : 2;
+    const int per = nwave * (PM + 1) + 4 * 64;
+    o.red_slices = (B * per * 8 <= 40 * 1024) ? B : 2;
     off += o.red_slices * per + nwave;
   }
   o.total = off;
@@ -219,11 +214,12 @@ struct MmLds {
   int red_slices;
 };
 
-template <int PM, int KIND, int XP, bool GRAD, int NT = 256>
+template <int PM, int KIND, bool GRAD, int NT = 256>
 __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS,
                                           const double *__restrict__ wk,
                                           const double *__restrict__ wlast, int64_t R0,
                                           int64_t C0, int tid) {
+  constexpr int XP = PM + 1;
   const MmLayout o = mm_layout(PM, B, KIND, GRAD, NT / 64);
   const int NS = (GRAD && KIND == 1) ? B + 1 : B;
   constexpr bool XI = GRAD && PM <= 32;
@@ -242,7 +238,6 @@ __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS
     const int c = e / PM, i = e - c * PM;
     const double x = S.X[(C0 + c) * PM + i];
     L.XJ[c * XP + i] = x;
-    if (XP > PM + 1) L.XJ[c * XP + PM + i] = x * x;
     if (XI) L.XI[c * (PM + 1) + i] = S.X[(R0 + c) * PM + i];
   }
   for (int e = tid; e < (B - 1) * 64; e += NT) {
@@ -354,7 +349,7 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
   const int rl = 16 * w + lr;
   const int64_t r = R0 + rl;
   constexpr int XP = PM + 1;
-  const MmLds L = mm_stage<PM, KIND, XP, false>(lds, S, B, ZS, tab.wk, tab.wk, R0, C0, tid);
+  const MmLds L = mm_stage<PM, KIND, false>(lds, S, B, ZS, tab.wk, tab.wk, R0, C0, tid);
   RowX<PM> xr;
   xr.load(S.X + r * PM, lk);
   double kf[4][4];
@@ -433,29 +428,30 @@ __device__ __forceinline__ double rcp_nr_mm(double f) {
 // CB = 2: 512 threads, wave w holds rows 16 (w & 3).., columns 32 (w >> 2)..
 // (8 pairs per lane): half the per-lane state, so twice the waves per SIMD
 // hide the fp64 latencies.
-template <int PM, int KIND, int CB>
-__global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2)) void k_grad_mm(PairSide S, int B, int ZS,
-                                                                  TabView tab,
-                                                                  const double *__restrict__ A,
-                                                                  int64_t ld, double sA,
-                                                                  const double *__restrict__ alpha,
-                                                                  double *__restrict__ gpart,
-                                                                  double *__restrict__ trpart,
-                                                                  int64_t ntiles,
-                                                                  const Tile *__restrict__ tiles,
-                                                                  int G) {
+//
+// Per slice, with U the T-weighted derivative factors of the wave's pairs:
+//   sum_rc U d_i^2 = sum_r x_ri^2 R_r + sum_c x_ci^2 C_c - 2 sum_r x_ri V_ri,
+//   V = U X_J (GEMM2, ceil(PM/16) column blocks), R_r / C_c the row / column
+//   sums of U.  R_r: in-lane sums + 2 shuffles.  C_c: a reduce-scatter over
+//   the 16 lanes of a row group (log2 16 shuffle levels), the four row
+//   blocks' sums meet in LDS and sum_c x_ci^2 C_c is formed once per slice.
+template <int PM, int KIND, int CB, bool PS>
+__global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2)) void k_grad_mm(
+    PairSide S, int B, int ZS, TabView tab, const double *__restrict__ A, int64_t ld, double sA,
+    const double *__restrict__ alpha, double *__restrict__ gpart, double *__restrict__ trpart,
+    int64_t ntiles, const Tile *__restrict__ tiles, int G) {
   constexpr int NT = 64 * 4 * (4 / CB);      // threads
   constexpr int NWV = NT / 64;               // waves
-  constexpr int XP = mm_table_width(PM, true) + 1;
-  constexpr bool B2 = XP > PM + 1;           // x^2 staged beside x
+  constexpr int XP = PM + 1;
   constexpr bool XIL = PM <= 32;             // row covariates staged in LDS
   constexpr int NV = PM + 1;
-  constexpr int NC2 = 2 * PM;                // GEMM2 columns [x | x^2]
-  constexpr int NQ = (NC2 + 15) / 16;        // 16-wide column blocks
+  constexpr int NQ = (PM + 15) / 16;         // GEMM2 16-wide column blocks
   // GEMM2 column blocks per pass of its k-loop (one at CB = 2: register cap)
-  constexpr int QG = CB == 2 ? 1 : (NQ >= 6 ? 2 : (NQ < ACE_MM_QG ? NQ : ACE_MM_QG));
-  constexpr int RS = NC2 + 1;                // partial row: [x part | x^2 part | T K]
+  constexpr int QG = CB == 2 ? 1 : (NQ < ACE_MM_QG ? NQ : ACE_MM_QG);
+  constexpr int RS = PM + 1;                 // partial row: [x part | T K]
+  constexpr int PER = NWV * RS + 4 * 64;     // per-slice partials (+ column sums)
   constexpr int NKK = 4 * CB;                // GEMM2 k-steps (the wave's columns / 4)
+  constexpr int NVAL = 4 * CB;               // pairs per lane
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int64_t t = blockIdx.x;
   int64_t I, J;
@@ -470,7 +466,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   const int64_t r = R0 + rl;
   const bool rvalid = r < n;
   const double *wlast = (KIND == 1) ? tab.wg + (B - 1) * PM : tab.wk;
-  const MmLds L = mm_stage<PM, KIND, XP, true, NT>(lds, S, B, ZS, tab.wk, wlast, R0, C0, tid);
+  const MmLds L = mm_stage<PM, KIND, true, NT>(lds, S, B, ZS, tab.wk, wlast, R0, C0, tid);
   // T = w_rc (sA A[r,c] - alpha_r alpha_c), w = 2 off the diagonal (lower pairs)
   const double ar = rvalid ? alpha[r] : 0.0;
   double tv[CB][4];
@@ -506,9 +502,30 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
         fc[cb][v] = 1.0 + sqrt_pk(3.0 * rt2);
       }
   }
-  const bool per_slice = L.red_slices == B;
+  // gpart[b][i] of this tile from slice b's partials: the waves' x parts,
+  // sum_c x_ci^2 C_c, and (i == PM) the waves' sums of T K
+  auto finish = [&](int b, const double *red, int i) {
+    double g = 0.0;
+    if (i < PM) {
+#pragma unroll
+      for (int q = 0; q < NWV; ++q) g += red[q * RS + i];
+      const double *cc = red + NWV * RS;
+      double gc = 0.0;
+      for (int c = 0; c < 64; ++c) {
+        const double x = L.XJ[c * XP + i];
+        gc = fma(x * x, (cc[c] + cc[64 + c]) + (cc[128 + c] + cc[192 + c]), gc);
+      }
+      g += gc;
+    } else {
+#pragma unroll
+      for (int q = 0; q < NWV; ++q) g += red[q * RS + PM];
+    }
+    gpart[((int64_t)b * NV + i) * ntiles + t] = g;
+  };
+  // PS: one partial buffer per slice (the host checked L.red_slices == B)
+  constexpr bool per_slice = PS;
   for (int b = B - 1; b >= 0; --b) {
-    double *red = L.Red + (per_slice ? b : (b & 1)) * NWV * RS;
+    double *red = L.Red + (per_slice ? b : (b & 1)) * PER;
     double zr = 0.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
     if (b > 0) {
       zr = S.Z[r * ZS + b - 1];
@@ -564,38 +581,25 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
     double Rv[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) Rv[v] = __shfl(rs, lk + 4 * v, 64);  // row 16 wr + lk + 4v
-    // GEMM2 over [x | x^2], QG column blocks per pass of the k-loop
+    // GEMM2: V = U X_J, QG column blocks per pass of the k-loop
 #pragma unroll
     for (int q0 = 0; q0 < NQ; q0 += QG) {
       d4 a2[QG];
-      int fo[QG];
-      bool sq[QG];
 #pragma unroll
-      for (int j = 0; j < QG; ++j) {
-        a2[j] = d4{0.0, 0.0, 0.0, 0.0};
-        const int nn = 16 * (q0 + j) + lr;
-        if (B2) {  // [x | x^2] staged: column nn of the table
-          sq[j] = false;
-          fo[j] = nn < NC2 ? nn : 0;
-        } else {   // PM % 16 == 0: whole blocks are x or x^2
-          sq[j] = q0 + j >= PM / 16;
-          fo[j] = sq[j] ? (nn < NC2 ? nn - PM : 0) : nn;
-        }
-      }
+      for (int j = 0; j < QG; ++j) a2[j] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) {
         const double *xc = L.XJ + (cbase + 4 * kk + lk) * XP;
 #pragma unroll
         for (int j = 0; j < QG; ++j) {
-          if (q0 + j < NQ) {
-            const double x = xc[fo[j]];
-            a2[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[kk >> 2][kk & 3], sq[j] ? x * x : x,
-                                                         a2[j], 0, 0, 0);
-          }
+          const int nn = 16 * (q0 + j) + lr;
+          if (q0 + j < NQ)
+            a2[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[kk >> 2][kk & 3],
+                                                         nn < PM ? xc[nn] : 0.0, a2[j], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      // a2[j][v] = V[row 16 wr + lk + 4 v][column 16 (q0 + j) + lr]
+      // a2[j][v] = V[row 16 wr + lk + 4 v][feature 16 (q0 + j) + lr]
 #pragma unroll
       for (int j = 0; j < QG; ++j) {
         if (q0 + j >= NQ) continue;
@@ -608,13 +612,38 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
             const double x = XIL ? L.XI[rr * (PM + 1) + nn] : S.X[(R0 + rr) * PM + nn];
             part += fma(x * x, Rv[v], -2.0 * x * a2[j][v]);
           }
-        } else {
-          part = (a2[j][0] + a2[j][1]) + (a2[j][2] + a2[j][3]);
         }
         part += __shfl_xor(part, 16, 64);
         part += __shfl_xor(part, 32, 64);
-        if (lk == 0 && nn < NC2) red[w * RS + nn] = part;
+        if (lk == 0 && nn < PM) red[w * RS + nn] = part;
       }
+    }
+    // C_c: column sums of U over the wave's 16 rows, reduce-scatter over lr
+    {
+      // (after GEMM2: U's registers are free again)
+      double cv[NVAL];
+#pragma unroll
+      for (int k = 0; k < NVAL; ++k) cv[k] = acc[k >> 2][k & 3];
+      int kk0 = 0, cnt = NVAL;
+#pragma unroll
+      for (int m = 8; m >= 1; m >>= 1) {
+        if (cnt > 1) {
+          const int h = cnt / 2;
+          const bool up = (lr & m) != 0;
+#pragma unroll
+          for (int j = 0; j < h; ++j) {
+            const double mine = up ? cv[j + h] : cv[j];
+            const double other = up ? cv[j] : cv[j + h];
+            cv[j] = mine + __shfl_xor(other, m, 64);
+          }
+          if (up) kk0 += h;
+          cnt = h;
+        } else {
+          cv[0] += __shfl_xor(cv[0], m, 64);
+        }
+      }
+      if ((lr & (16 / NVAL - 1)) == 0)
+        red[NWV * RS + wr * 64 + cbase + 16 * (kk0 >> 2) + lk + 4 * (kk0 & 3)] = cv[0];
     }
     gl += __shfl_xor(gl, 1, 64);
     gl += __shfl_xor(gl, 2, 64);
@@ -622,20 +651,10 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
     gl += __shfl_xor(gl, 8, 64);
     gl += __shfl_xor(gl, 16, 64);
     gl += __shfl_xor(gl, 32, 64);
-    if (lane == 0) red[w * RS + NC2] = gl;
+    if (lane == 0) red[w * RS + PM] = gl;
     if (!per_slice) {
       __syncthreads();  // the waves' partials of slice b are in red
-      if (tid <= PM) {
-        double g = 0.0;
-        if (tid < PM) {
-#pragma unroll
-          for (int q = 0; q < NWV; ++q) g += red[q * RS + tid] + red[q * RS + PM + tid];
-        } else {
-#pragma unroll
-          for (int q = 0; q < NWV; ++q) g += red[q * RS + NC2];
-        }
-        gpart[((int64_t)b * NV + tid) * ntiles + t] = g;
-      }
+      if (tid <= PM) finish(b, red, tid);
     }
   }
   // trace of T
@@ -645,22 +664,13 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   tr += __shfl_xor(tr, 8, 64);
   tr += __shfl_xor(tr, 16, 64);
   tr += __shfl_xor(tr, 32, 64);
-  double *str = L.Red + L.red_slices * NWV * RS;
+  double *str = L.Red + L.red_slices * PER;
   if (lane == 0) str[w] = tr;
   __syncthreads();
   if (per_slice) {  // all slices' partials at once
     for (int e = tid; e < B * NV; e += NT) {
       const int bb = e / NV, i = e - bb * NV;
-      const double *red = L.Red + bb * NWV * RS;
-      double g = 0.0;
-      if (i < PM) {
-#pragma unroll
-        for (int q = 0; q < NWV; ++q) g += red[q * RS + i] + red[q * RS + PM + i];
-      } else {
-#pragma unroll
-        for (int q = 0; q < NWV; ++q) g += red[q * RS + NC2];
-      }
-      gpart[((int64_t)bb * NV + i) * ntiles + t] = g;
+      finish(bb, L.Red + bb * PER, i);
     }
   }
   if (tid == 0) {
@@ -682,6 +692,23 @@ __host__ __device__ constexpr int grad_cb(int PM, int kind) {
   return (ACE_MM_GRAD_CB == 2 && (kind == 0 || PM <= 32)) ? 2 : 4;
 }
 
+template <int PM, int KIND, bool PS>
+static hipError_t grad_mm_launch_ps(PairSide S, int B, int ZS, TabView tab, const double *A,
+                                    int64_t ld, double sA, const double *alpha, double *gpart,
+                                    double *trpart, hipStream_t st, const Tile *tiles,
+                                    int64_t nblk, int G, size_t lds) {
+  constexpr int CB = grad_cb(PM, KIND);
+  constexpr int NT = 64 * 4 * (4 / CB);
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute((const void *)k_grad_mm<PM, KIND, CB, PS>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((k_grad_mm<PM, KIND, CB, PS>), dim3((unsigned)nblk), dim3(NT), lds, st, S, B,
+                     ZS, tab, A, ld, sA, alpha, gpart, trpart, nblk, tiles, G);
+  return hipGetLastError();
+}
+
 template <int PM, int KIND>
 static hipError_t grad_mm_launch(PairSide S, int B, int ZS, TabView tab, const double *A,
                                  int64_t ld, double sA, const double *alpha, double *gpart,
@@ -689,15 +716,13 @@ static hipError_t grad_mm_launch(PairSide S, int B, int ZS, TabView tab, const d
                                  int64_t nblk, int G) {
   constexpr int CB = grad_cb(PM, KIND);
   constexpr int NT = 64 * 4 * (4 / CB);
-  const size_t lds = (size_t)mm_layout(PM, B, KIND, true, NT / 64).total * sizeof(double);
-  if (lds > 65536) {
-    const hipError_t e = hipFuncSetAttribute((const void *)k_grad_mm<PM, KIND, CB>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL((k_grad_mm<PM, KIND, CB>), dim3((unsigned)nblk), dim3(NT), lds, st, S, B, ZS,
-                     tab, A, ld, sA, alpha, gpart, trpart, nblk, tiles, G);
-  return hipGetLastError();
+  const MmLayout o = mm_layout(PM, B, KIND, true, NT / 64);
+  const size_t lds = (size_t)o.total * sizeof(double);
+  return o.red_slices == B
+             ? grad_mm_launch_ps<PM, KIND, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart,
+                                                 st, tiles, nblk, G, lds)
+             : grad_mm_launch_ps<PM, KIND, false>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart,
+                                                  st, tiles, nblk, G, lds);
 }
 
 template <int PM>
