@@ -75,7 +75,7 @@ bool mm_lds_ok(int PM, int B, int kind, bool grad);
 hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                           const double *A, int64_t ld, double sA, const double *alpha,
                           double *gpart, double *trpart, hipStream_t st, const Tile *tiles,
-                          int64_t ntiles, int G);
+                          int64_t ntiles, int G, int64_t ndiag);
 
 // ---- gradient --------------------------------------------------------------
 // T = sA * A[r,c] - alpha_r alpha_c over the lower 64x64 tiles of [0,n)
@@ -83,11 +83,14 @@ hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView t
 // gpart: [(b*(PM+1) + i) * nsuper + tile]  (i < PM: length-scale sums,
 //        i == PM: lambda sums); trpart[tile]: trace of T.
 // cube (if non-null, ld n): K_b read from the cube instead of recomputed.
+// tiles: the rank's list; ndiag >= 0 says its first ndiag entries are the
+// diagonal tiles (lets the MFMA kernel run them separately).
 hipError_t launch_grad(int kind, int PM, PairSide side, int B, int ZS,
                        TabView tab, const double *A, int64_t ld, double sA,
                        const double *alpha, const double *cube,
                        double *gpart, double *trpart, hipStream_t st,
-                       const Tile *tiles = nullptr, int64_t ntiles = 0, int G = 1);
+                       const Tile *tiles = nullptr, int64_t ntiles = 0, int G = 1,
+                       int64_t ndiag = -1);
 int64_t grad_ntiles(int64_t n);
 // Kfull * alpha partial rows from a lower-triangle copy of Kfull (ld):
 // kapart[T * npad + x] for 64-tile slot T; sum over T with launch_rowsum.

@@ -750,10 +750,10 @@ static hipError_t grad_pm(int kind, PairSide S, int B, int ZS, TabView tab, cons
 hipError_t launch_grad(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                        const double *A, int64_t ld, double sA, const double *alpha,
                        const double *cube, double *gpart, double *trpart, hipStream_t st,
-                       const Tile *tiles, int64_t ntiles, int G) {
+                       const Tile *tiles, int64_t ntiles, int G, int64_t ndiag) {
   if (!cube && pairs_use_mm(PM, true) && mm_lds_ok(PM, B, kind, true))
     return launch_grad_mm(kind, PM, S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st, tiles,
-                          ntiles, G);
+                          ntiles, G, ndiag);
   switch (PM) {
 #define ACE_CASE(P) \
   case P:           \

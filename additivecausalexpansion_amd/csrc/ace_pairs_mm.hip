@@ -18,6 +18,8 @@
 // (cb, v in 0..3) -- exactly the fragment layout of the MFMA result
 // D = X_J (w_b X_I)^T, so no data moves between the GEMM and the
 // elementwise kernel math.
+#include <type_traits>
+
 #include "ace_internal.h"
 
 namespace ace {
@@ -55,7 +57,9 @@ __device__ __forceinline__ double sgn_mm(double x) {
 // amplitude parameter.  x = (32 m + j) ln2/32 + r, |r| <= ln2/64:
 // exp(x) = 2^m * 2^(j/32) * p(r), p the degree-6 Taylor polynomial
 // (truncation < 4e-18), 2^(j/32) from a 32-entry LDS table (correctly
-// rounded by the host's pow).  Arguments below -745 give 0 like exp().
+// rounded by the host's pow).  Arguments below about -745 give 0 like exp()
+// (v_cvt_i32_f64 saturates, so even huge negative ones); never called with
+// -inf (the SE path selects 0 for z = 0 before its log|z| terms matter).
 __device__ const double kExp2Tab[32] = {
     1,
     1.0218971486541166,
@@ -91,7 +95,6 @@ __device__ const double kExp2Tab[32] = {
     1.9571441241754002};
 
 __device__ __forceinline__ double exp_tb(double x, const double *tab) {
-  x = fmax(x, -745.2);
   const double kf = __builtin_rint(x * 46.16624130844683);  // 32 / ln2
   double r = fma(-kf, 0.02166084938653512, x);               // (ln2 / 32) hi
   r = fma(-kf, 5.9631716539705866e-12, r);                   // (ln2 / 32) lo
@@ -135,8 +138,7 @@ __device__ __forceinline__ double kval_mm(int b, double r2, double lam, double z
     const double t = sqrt_pk(r2);
     const double e = (1.0 + SQRT3 * t) * exp_tb(lam - SQRT3 * t, etab);
     if (b == 0) return e;
-    if (zlo == 0.0) return 0.0;
-    return (e * zlo) * zhi;
+    return (e * zlo) * zhi;  // z = 0 gives 0 (the reference's explicit zero test)
   }
 }
 
@@ -357,36 +359,43 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
     for (int v = 0; v < 4; ++v) kf[cb][v] = 0.0;
-  for (int b = 0; b < B; ++b) {
-    double zr = 0.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
-    if (b > 0) {
-      zr = S.Z[r * ZS + b - 1];
-      if (KIND == 0) lzr = S.LZ[r * ZS + b - 1];
-    }
-    d4 acc[4];
-    gemm1_mm<XP>(L.XJ, xr, L.W + b * PM, lr, lk, acc);
-    const double sr = L.Nr[b * 64 + rl];
-    const double *nc = L.Nc + b * 64;
-    const double lam = tab.lam[b];
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int cl = 16 * cb + lk + 4 * v;
-        const int64_t c = C0 + cl;
-        double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), 0.0);
-        if (c == r) r2 = 0.0;
-        double zc = 0.0, lzc = 0.0;
-        if (b > 0) {
-          zc = L.Z[(b - 1) * 64 + cl];
-          if (KIND == 0) lzc = L.LZ[(b - 1) * 64 + cl];
-        }
-        const double kb = (r < c) ? kval_mm<KIND>(b, r2, lam, zr, zc, lzr, lzc, L.E)
-                                  : kval_mm<KIND>(b, r2, lam, zc, zr, lzc, lzr, L.E);
-        kf[cb][v] += kb;
-        MM_PAIR_FENCE(cb, v);
+  // diagonal tiles (I == J) need the r == c and r < c tests; below the
+  // diagonal r > c for every pair
+  auto slices = [&](auto diag) {
+    constexpr bool DG = decltype(diag)::value;
+    for (int b = 0; b < B; ++b) {
+      double zr = 0.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
+      if (b > 0) {
+        zr = S.Z[r * ZS + b - 1];
+        if (KIND == 0) lzr = S.LZ[r * ZS + b - 1];
       }
-  }
+      d4 acc[4];
+      gemm1_mm<XP>(L.XJ, xr, L.W + b * PM, lr, lk, acc);
+      const double sr = L.Nr[b * 64 + rl];
+      const double *nc = L.Nc + b * 64;
+      const double lam = tab.lam[b];
+  #pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+  #pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int cl = 16 * cb + lk + 4 * v;
+          const int64_t c = C0 + cl;
+          double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), 0.0);
+          if (DG && c == r) r2 = 0.0;
+          double zc = 0.0, lzc = 0.0;
+          if (b > 0) {
+            zc = L.Z[(b - 1) * 64 + cl];
+            if (KIND == 0) lzc = L.LZ[(b - 1) * 64 + cl];
+          }
+          const double kb = (DG && r < c) ? kval_mm<KIND>(b, r2, lam, zr, zc, lzr, lzc, L.E)
+                                          : kval_mm<KIND>(b, r2, lam, zc, zr, lzc, lzr, L.E);
+          kf[cb][v] += kb;
+          MM_PAIR_FENCE(cb, v);
+        }
+    }
+  };
+  if (I == J) slices(std::true_type{});
+  else slices(std::false_type{});
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
@@ -435,11 +444,11 @@ __device__ __forceinline__ double rcp_nr_mm(double f) {
 //   sums of U.  R_r: in-lane sums + 2 shuffles.  C_c: a reduce-scatter over
 //   the 16 lanes of a row group (log2 16 shuffle levels), the four row
 //   blocks' sums meet in LDS and sum_c x_ci^2 C_c is formed once per slice.
-template <int PM, int KIND, int CB, bool PS>
+template <int PM, int KIND, int CB, bool PS, bool DG>
 __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2)) void k_grad_mm(
     PairSide S, int B, int ZS, TabView tab, const double *__restrict__ A, int64_t ld, double sA,
     const double *__restrict__ alpha, double *__restrict__ gpart, double *__restrict__ trpart,
-    int64_t ntiles, const Tile *__restrict__ tiles, int G) {
+    int64_t ntiles, const Tile *__restrict__ tiles, int G, int64_t t0) {
   constexpr int NT = 64 * 4 * (4 / CB);      // threads
   constexpr int NWV = NT / 64;               // waves
   constexpr int XP = PM + 1;
@@ -453,9 +462,21 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   constexpr int NKK = 4 * CB;                // GEMM2 k-steps (the wave's columns / 4)
   constexpr int NVAL = 4 * CB;               // pairs per lane
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int64_t t = blockIdx.x;
+  // DG: diagonal tiles (the r == c and r < c tests), else strictly lower
+  // tiles (r > c for every pair).  Partial slot t = t0 + block; the tile is
+  // tiles[t] (a list with its diagonal tiles first) or, without a list,
+  // (block, block) / the block-th strictly lower tile.
+  const int64_t t = t0 + blockIdx.x;
   int64_t I, J;
-  tile_of(tiles, t, I, J);
+  if (tiles) {
+    I = tiles[t].I;
+    J = tiles[t].J;
+  } else if (DG) {
+    I = J = blockIdx.x;
+  } else {
+    tile_of(nullptr, blockIdx.x, I, J);  // row-major triangle incl. diagonal, shifted:
+    ++I;                                 // (I, J) with J <= I  ->  (I + 1, J), J < I + 1
+  }
   if (G > 1) A += (lcol(J * AT, G) - J * AT) * ld;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
@@ -498,7 +519,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
       for (int v = 0; v < 4; ++v) {
         const int cl = 16 * cb + lk + 4 * v;
         double rt2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), 0.0);
-        if (C0 + cbase + cl == r) rt2 = 0.0;
+        if (DG && C0 + cbase + cl == r) rt2 = 0.0;
         fc[cb][v] = 1.0 + sqrt_pk(3.0 * rt2);
       }
   }
@@ -545,13 +566,13 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
         const int cl = 16 * cb + lk + 4 * v;
         const int64_t c = C0 + cbase + cl;
         double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), 0.0);
-        if (c == r) r2 = 0.0;
+        if (DG && c == r) r2 = 0.0;
         double zc = 0.0, lzc = 0.0;
         if (b > 0) {
           zc = zcol[cl];
           if (KIND == 0) lzc = lzcol[cl];
         }
-        const bool rlo = r < c;
+        const bool rlo = DG && r < c;
         const double zlo = rlo ? zr : zc, zhi = rlo ? zc : zr;
         double kb, f = 1.0;
         if (KIND == 0) {
@@ -692,51 +713,72 @@ __host__ __device__ constexpr int grad_cb(int PM, int kind) {
   return (ACE_MM_GRAD_CB == 2 && (kind == 0 || PM <= 32)) ? 2 : 4;
 }
 
-template <int PM, int KIND, bool PS>
+template <int PM, int KIND, bool PS, bool DG>
 static hipError_t grad_mm_launch_ps(PairSide S, int B, int ZS, TabView tab, const double *A,
                                     int64_t ld, double sA, const double *alpha, double *gpart,
                                     double *trpart, hipStream_t st, const Tile *tiles,
-                                    int64_t nblk, int G, size_t lds) {
+                                    int64_t nblk, int64_t nslot, int G, size_t lds, int64_t t0) {
   constexpr int CB = grad_cb(PM, KIND);
   constexpr int NT = 64 * 4 * (4 / CB);
+  if (nblk == 0) return hipSuccess;
   if (lds > 65536) {
-    const hipError_t e = hipFuncSetAttribute((const void *)k_grad_mm<PM, KIND, CB, PS>,
+    const hipError_t e = hipFuncSetAttribute((const void *)k_grad_mm<PM, KIND, CB, PS, DG>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((k_grad_mm<PM, KIND, CB, PS>), dim3((unsigned)nblk), dim3(NT), lds, st, S, B,
-                     ZS, tab, A, ld, sA, alpha, gpart, trpart, nblk, tiles, G);
+  hipLaunchKernelGGL((k_grad_mm<PM, KIND, CB, PS, DG>), dim3((unsigned)nblk), dim3(NT), lds, st,
+                     S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, nslot, tiles, G, t0);
   return hipGetLastError();
+}
+
+// Two launches: the diagonal tiles (with the r == c / r < c tests) and the
+// strictly lower ones.  Without a list: slots [0, nt) diagonal, [nt, ...)
+// strictly lower.  With a list: its first ndiag entries are the diagonal
+// tiles (ndiag < 0: not partitioned -> one launch of the general form).
+template <int PM, int KIND, bool PS>
+static hipError_t grad_mm_launch_dg(PairSide S, int B, int ZS, TabView tab, const double *A,
+                                    int64_t ld, double sA, const double *alpha, double *gpart,
+                                    double *trpart, hipStream_t st, const Tile *tiles,
+                                    int64_t nslot, int64_t ndiag, int G, size_t lds) {
+  if (tiles && ndiag < 0)
+    return grad_mm_launch_ps<PM, KIND, PS, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart,
+                                                 st, tiles, nslot, nslot, G, lds, 0);
+  const int64_t nd = tiles ? ndiag : (S.n + AT - 1) / AT;
+  hipError_t e = grad_mm_launch_ps<PM, KIND, PS, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart,
+                                                       trpart, st, tiles, nd, nslot, G, lds, 0);
+  if (e != hipSuccess) return e;
+  return grad_mm_launch_ps<PM, KIND, PS, false>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st,
+                                                tiles, nslot - nd, nslot, G, lds, nd);
 }
 
 template <int PM, int KIND>
 static hipError_t grad_mm_launch(PairSide S, int B, int ZS, TabView tab, const double *A,
                                  int64_t ld, double sA, const double *alpha, double *gpart,
                                  double *trpart, hipStream_t st, const Tile *tiles,
-                                 int64_t nblk, int G) {
+                                 int64_t nslot, int64_t ndiag, int G) {
   constexpr int CB = grad_cb(PM, KIND);
   constexpr int NT = 64 * 4 * (4 / CB);
   const MmLayout o = mm_layout(PM, B, KIND, true, NT / 64);
   const size_t lds = (size_t)o.total * sizeof(double);
   return o.red_slices == B
-             ? grad_mm_launch_ps<PM, KIND, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart,
-                                                 st, tiles, nblk, G, lds)
-             : grad_mm_launch_ps<PM, KIND, false>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart,
-                                                  st, tiles, nblk, G, lds);
+             ? grad_mm_launch_dg<PM, KIND, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart,
+                                                 st, tiles, nslot, ndiag, G, lds)
+             : grad_mm_launch_dg<PM, KIND, false>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart,
+                                                  st, tiles, nslot, ndiag, G, lds);
 }
 
 template <int PM>
 static hipError_t grad_mm_pm(int kind, PairSide S, int B, int ZS, TabView tab, const double *A,
                              int64_t ld, double sA, const double *alpha, double *gpart,
                              double *trpart, hipStream_t st, const Tile *tiles, int64_t ntiles,
-                             int G) {
+                             int64_t ndiag, int G) {
   const int64_t nt = (S.n + AT - 1) / AT;
-  const int64_t nblk = tiles ? ntiles : nt * (nt + 1) / 2;
-  if (nblk == 0) return hipSuccess;
+  const int64_t nslot = tiles ? ntiles : nt * (nt + 1) / 2;
+  if (nslot == 0) return hipSuccess;
   return kind == 0 ? grad_mm_launch<PM, 0>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st,
-                                           tiles, nblk, G)
+                                           tiles, nslot, ndiag, G)
                    : grad_mm_launch<PM, 1>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st,
-                                           tiles, nblk, G);
+                                           tiles, nslot, ndiag, G);
 }
 
 // Whether the per-tile staging of the MFMA kernels fits the LDS budget
@@ -751,11 +793,12 @@ bool mm_lds_ok(int PM, int B, int kind, bool grad) {
 hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                           const double *A, int64_t ld, double sA, const double *alpha,
                           double *gpart, double *trpart, hipStream_t st, const Tile *tiles,
-                          int64_t ntiles, int G) {
+                          int64_t ntiles, int G, int64_t ndiag) {
   switch (PM) {
 #define ACE_CASE(P) \
   case P:           \
-    return grad_mm_pm<P>(kind, S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st, tiles, ntiles, G);
+    return grad_mm_pm<P>(kind, S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st, tiles, ntiles, \
+                         ndiag, G);
     ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
     ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
 #undef ACE_CASE

@@ -369,7 +369,9 @@ ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int
     const std::vector<Tile> ta = own_tiles(npad / AT, AT, world, R->r);
     R->nasm = (int64_t)ta.size();
     upload_tiles(ctx, R->tasm, ta);
-    const std::vector<Tile> tg = own_tiles(m->ntr, AT, world, R->r);
+    std::vector<Tile> tg = own_tiles(m->ntr, AT, world, R->r);
+    // diagonal tiles first: the gradient kernel runs them separately
+    std::stable_partition(tg.begin(), tg.end(), [](const Tile &t) { return t.I == t.J; });
     R->ngrad = (int64_t)tg.size();
     for (const Tile &t : tg) R->ndiag += t.I == t.J;
     upload_tiles(ctx, R->tgrad, tg);
@@ -467,7 +469,7 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
     const Tile *tg = (const Tile *)R.tgrad.p;
     if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_grad[0], st), "event");
     ck(ctx, launch_grad(s.kind, s.PM, ps, s.B, s.ZS, tv, R.A[which].d(), naug, -1.0, R.alpha.d(),
-                        nullptr, R.gpart.d(), R.trpart.d(), st, tg, R.ngrad, m->G),
+                        nullptr, R.gpart.d(), R.trpart.d(), st, tg, R.ngrad, m->G, R.ndiag),
        "grad");
     if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_grad[1], st), "event");
     ck(ctx, hipMemsetAsync(R.kapart.p, 0, R.kapart.bytes, st), "memset kapart");
