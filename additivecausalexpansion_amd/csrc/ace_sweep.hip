@@ -32,6 +32,9 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // latency-bound work) share CUs with the MFMA-heavy update tiles of the main
 // stream.  Raising their waves' issue priority lets them win the SIMD
 // arbitration instead of getting a 1/5 share of the issue slots.
+#ifndef ACE_PIVOT_RCP
+#define ACE_PIVOT_RCP 1
+#endif
 #ifndef ACE_CHAIN_PRIO
 #define ACE_CHAIN_PRIO 3
 #endif
@@ -127,7 +130,18 @@ __global__ __launch_bounds__(256) void k_pivot(const double *__restrict__ S, int
       }
       __syncthreads();
       const double d = rowb[buf][t];
+      // 1/d by v_rcp_f64 + two Newton steps (<= 1 ulp): five dependent fp64
+      // operations on the chain's critical path instead of the eleven of
+      // the IEEE division sequence
+#if ACE_PIVOT_RCP
+      double rd = __builtin_amdgcn_rcp(d);
+      double re = fma(-d, rd, 1.0);
+      rd = fma(rd, re, rd);
+      re = fma(-d, rd, 1.0);
+      rd = fma(rd, re, rd);
+#else
       const double rd = 1.0 / d;
+#endif
       const double dit = colb[buf][lane];
       double rt[16];
 #pragma unroll
