@@ -262,7 +262,7 @@ int ace_grad(ace_ctx *ctx, int kind, int64_t n, int p, int B, const double *y, c
   ck(ctx, launch_colsum(dtr.d(), nt, 1, dgs.d() + ncol, ctx->stream), "colsum tr");
   // Kfull * alpha for the RMSE (src/kernel_SE_cpp.cpp:238)
   ck(ctx, launch_gemv(dKf.d(), n, n, n, dalpha.d(), ds.d(), ctx->stream), "gemv K alpha");
-  ck(ctx, launch_final_sums(dy.d(), dmu.d(), dalpha.d(), ds.d(), n, nullptr, 0, dsums.d(),
+  ck(ctx, launch_final_sums(dy.d(), dmu.d(), dalpha.d(), ds.d(), 0.0, n, nullptr, 0, dsums.d(),
                             ctx->stream),
      "final sums");
   std::vector<double> gs((size_t)(ncol + 1)), sums(8);
@@ -296,7 +296,7 @@ int ace_stats(ace_ctx *ctx, int64_t n, const double *y, const double *Kmat, cons
   alloc(ctx, dsums, 8 * sizeof(double), "alloc");
   ck(ctx, launch_gemv(dinv.d(), n, n, n, dyb.d(), dalpha.d(), ctx->stream), "gemv");
   ck(ctx, launch_gemv(dK.d(), n, n, n, dalpha.d(), ds.d(), ctx->stream), "gemv");
-  ck(ctx, launch_final_sums(dy.d(), dmu.d(), dalpha.d(), ds.d(), n, nullptr, 0, dsums.d(),
+  ck(ctx, launch_final_sums(dy.d(), dmu.d(), dalpha.d(), ds.d(), 0.0, n, nullptr, 0, dsums.d(),
                             ctx->stream),
      "sums");
   double sums[4];
@@ -496,12 +496,11 @@ struct ace_model {
   double std_y = 1.0;
   bool has_data = false;
   SideBufs side;
-  DBuf y, tab, alpha, scal, gpart, trpart, kapart, ka, gsum, sums, kcopy;
+  DBuf y, tab, alpha, scal, gpart, trpart, gsum, sums;
   SweepWork sw;   // A = resident inverse of the last para_update
   SweepWork sw2;  // train_stats scratch (keeps sw's inverse, Q6)
   bool prof = false;
   hipEvent_t ev_asm[2] = {nullptr, nullptr}, ev_grad[2] = {nullptr, nullptr};
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // Kfull*alpha on the side stream
   std::vector<hipEvent_t> ev_upd;
   std::vector<double> upd_flops;
   int upd_used = 0;
@@ -523,8 +522,9 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   const TabView tv = tab_view(m->tab, s);
   const PairSide ps = m->side.view(m->n);
   if (timed) ck(ctx, hipEventRecord(m->ev_asm[0], st), "event");
-  ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, std::exp(theta[0]),
-                          w.A.d(), w.naug, m->kcopy.d(), st),
+  const double sig = std::exp(theta[0]);
+  ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
+                          nullptr, st),
      "assembly");
   if (timed) ck(ctx, hipEventRecord(m->ev_asm[1], st), "event");
   ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, m->n, m->y.d(), st), "aug init");
@@ -539,15 +539,8 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   ck(ctx, launch_alpha_from_aug(w.A.d(), w.naug, w.npad, m->n, theta[1], use_mu, m->alpha.d(),
                                 m->scal.d(), st),
      "alpha");
-  // Kfull * alpha (HBM-bound read of the Kfull copy) runs on the side stream
-  // under the VALU-bound gradient kernel
-  hipStream_t side = ctx->side;
-  ck(ctx, hipEventRecord(m->ev_fork, st), "event");
-  ck(ctx, hipStreamWaitEvent(side, m->ev_fork, 0), "event wait");
-  ck(ctx, launch_symv_tiles(m->kcopy.d(), w.naug, m->n, m->alpha.d(), m->kapart.d(), w.npad, side),
-     "symv");
-  ck(ctx, launch_rowsum(m->kapart.d(), m->ntr, w.npad, m->n, m->ka.d(), side), "rowsum");
-  ck(ctx, hipEventRecord(m->ev_join, side), "event");
+  // RMSE residual ybar - Kfull alpha = sig alpha (A = Kfull + sig I is what
+  // the sweep inverted): no Kfull copy and no pass over it (k_final_sums)
   if (timed) ck(ctx, hipEventRecord(m->ev_grad[0], st), "event");
   ck(ctx, launch_grad(s.kind, s.PM, ps, s.B, s.ZS, tv, w.A.d(), w.naug, -1.0, m->alpha.d(),
                       nullptr, m->gpart.d(), m->trpart.d(), st),
@@ -556,9 +549,8 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   const int ncol = s.B * (s.PM + 1);
   ck(ctx, launch_colsum(m->gpart.d(), m->ntiles, ncol, m->gsum.d(), st), "colsum");
   ck(ctx, launch_colsum(m->trpart.d(), m->ntiles, 1, m->gsum.d() + ncol, st), "colsum");
-  ck(ctx, hipStreamWaitEvent(st, m->ev_join, 0), "event wait");
-  ck(ctx, launch_final_sums(m->y.d(), m->scal.d() + 4, m->alpha.d(), m->ka.d(), m->n, w.piv.d(),
-                            w.npad, m->sums.d(), st),
+  ck(ctx, launch_final_sums(m->y.d(), m->scal.d() + 4, m->alpha.d(), nullptr, sig, m->n,
+                            w.piv.d(), w.npad, m->sums.d(), st),
      "final sums");
 }
 
@@ -611,9 +603,6 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
     alloc(ctx, m->scal, 16 * sizeof(double), "alloc scal");
     alloc(ctx, m->gpart, (size_t)(m->ntiles * s.B * (s.PM + 1)) * sizeof(double), "alloc gpart");
     alloc(ctx, m->trpart, (size_t)m->ntiles * sizeof(double), "alloc trpart");
-    alloc(ctx, m->kapart, (size_t)(m->ntr * m->npad) * sizeof(double), "alloc kapart");
-    alloc(ctx, m->kcopy, (size_t)(m->naug * m->naug) * sizeof(double), "alloc Kfull copy");
-    alloc(ctx, m->ka, (size_t)m->npad * sizeof(double), "alloc ka");
     alloc(ctx, m->gsum, (size_t)(s.B * (s.PM + 1) + 1) * sizeof(double), "alloc gsum");
     alloc(ctx, m->sums, 8 * sizeof(double), "alloc sums");
     ck(ctx, hipMemsetAsync(m->sw.A.p, 0, m->sw.A.bytes, ctx->stream), "memset A");
@@ -625,8 +614,6 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
       ck(ctx, hipEventCreate(&m->ev_asm[j]), "event");
       ck(ctx, hipEventCreate(&m->ev_grad[j]), "event");
     }
-    ck(ctx, hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming), "event");
-    ck(ctx, hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming), "event");
     sync(ctx);
   } catch (const Fail &f) {
     ace_model_destroy(m);
@@ -646,8 +633,6 @@ void ace_model_destroy(ace_model *m) {
     if (m->ev_asm[j]) (void)hipEventDestroy(m->ev_asm[j]);
     if (m->ev_grad[j]) (void)hipEventDestroy(m->ev_grad[j]);
   }
-  if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
-  if (m->ev_join) (void)hipEventDestroy(m->ev_join);
   delete m;
 }
 

@@ -56,7 +56,7 @@ struct PairSide {
 // ---- assembly --------------------------------------------------------------
 // mode 0: fused eval -- lower 64-tiles of the n_pad x n_pad block of A (ld),
 //         value K + sig on the diagonal, identity on padding rows/cols; if
-//         cube is non-null it receives the lower Kfull copy (same ld).
+//         cube is non-null it receives the lower Kfull (same ld).
 // mode 1: symmetric ABI output -- full n x n Kfull (ld = n) + optional cube.
 // mode 2: cross ABI output -- n1 x n2 Kfull + optional cube.
 hipError_t launch_assembly(int mode, int kind, int PM, PairSide rows,
@@ -92,12 +92,6 @@ hipError_t launch_grad(int kind, int PM, PairSide side, int B, int ZS,
                        const Tile *tiles = nullptr, int64_t ntiles = 0, int G = 1,
                        int64_t ndiag = -1);
 int64_t grad_ntiles(int64_t n);
-// Kfull * alpha partial rows from a lower-triangle copy of Kfull (ld):
-// kapart[T * npad + x] for 64-tile slot T; sum over T with launch_rowsum.
-hipError_t launch_symv_tiles(const double *K, int64_t ld, int64_t n,
-                             const double *alpha, double *kapart, int64_t npad,
-                             hipStream_t st, const Tile *tiles = nullptr,
-                             int64_t ntiles = 0, int G = 1);
 
 // ---- sweep -----------------------------------------------------------------
 struct SweepBufs {
@@ -178,12 +172,11 @@ hipError_t launch_alpha_from_aug(const double *A, int64_t ld, int64_t npad,
                                  double *alpha, double *scal, hipStream_t st);
 hipError_t launch_colsum(const double *in, int64_t nrows, int ncols,
                          double *out, hipStream_t st);
-hipError_t launch_rowsum(const double *in, int64_t ntile_rows, int64_t npad,
-                         int64_t n, double *out, hipStream_t st);
 // sums[0] = sum (ybar - s)^2, sums[1] = sum y*alpha, sums[2] = sum alpha,
 // sums[3] = sum log(piv[0..npiv)), with ybar = y - *mu (device scalar).
+// s == nullptr: ybar - s = sig * alpha (fused model, A = Kfull + sig I).
 hipError_t launch_final_sums(const double *y, const double *mu, const double *alpha,
-                             const double *s, int64_t n, const double *piv,
+                             const double *s, double sig, int64_t n, const double *piv,
                              int64_t npiv, double *sums, hipStream_t st);
 // y = M x for M (m x k, col-major ld) ; y = M^T x
 hipError_t launch_gemv(const double *M, int64_t ld, int64_t m, int64_t k,

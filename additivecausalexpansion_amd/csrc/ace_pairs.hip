@@ -565,77 +565,6 @@ __global__ __launch_bounds__(256) void k_grad2(PairSide S, int B, int ZS, TabVie
 }
 
 // ---------------------------------------------------------------------------
-// Kfull * alpha from the lower copy written by the assembly (RMSE,
-// src/kernel_SE_cpp.cpp:238): per 64x64 lower tile, row sums (K a_J) go to
-// slot [J][rows of I] and column sums (K^T a_I) to slot [I][rows of J]; a
-// diagonal tile is symmetrised in LDS and gives only row sums.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_symv_tiles(const double *__restrict__ K, int64_t ld,
-                                                    int64_t n, const double *__restrict__ alpha,
-                                                    double *__restrict__ kapart, int64_t npad,
-                                                    const Tile *__restrict__ tiles, int G) {
-  __shared__ double t[AT][AT + 1];
-  __shared__ double part[4][AT];
-  int64_t J = blockIdx.x, I = blockIdx.y;
-  if (tiles) {
-    const Tile tt = tiles[blockIdx.x];
-    I = tt.I;
-    J = tt.J;
-    K += (lcol(J * AT, G) - J * AT) * ld;
-  }
-  if (J > I) return;
-  const int tid = threadIdx.x, x = tid & 63, q = tid >> 6;
-  for (int e = tid; e < AT * AT; e += 256) {
-    const int a = e & 63, c = e >> 6;
-    const int64_t r = I * AT + a, cc = J * AT + c;
-    double v = 0.0;
-    if (r < n && cc < n) v = (I == J && cc > r) ? K[cc + r * ld] : K[r + cc * ld];
-    t[a][c] = v;
-  }
-  __syncthreads();
-  // row sums: thread (x, q) sums columns q, q+4, ...
-  double s = 0.0;
-  for (int c = q; c < AT; c += 4) {
-    const int64_t cc = J * AT + c;
-    s = fma(t[x][c], cc < n ? alpha[cc] : 0.0, s);
-  }
-  part[q][x] = s;
-  __syncthreads();
-  if (tid < AT) {
-    const double rs = (part[0][x] + part[1][x]) + (part[2][x] + part[3][x]);
-    kapart[J * npad + I * AT + x] = rs;
-  }
-  if (I == J) return;
-  __syncthreads();
-  double s2 = 0.0;
-  for (int a = q; a < AT; a += 4) {
-    const int64_t r = I * AT + a;
-    s2 = fma(t[a][x], r < n ? alpha[r] : 0.0, s2);
-  }
-  part[q][x] = s2;
-  __syncthreads();
-  if (tid < AT) {
-    const double cs = (part[0][x] + part[1][x]) + (part[2][x] + part[3][x]);
-    kapart[I * npad + J * AT + x] = cs;
-  }
-}
-
-hipError_t launch_symv_tiles(const double *K, int64_t ld, int64_t n, const double *alpha,
-                             double *kapart, int64_t npad, hipStream_t st, const Tile *tiles,
-                             int64_t ntiles, int G) {
-  const unsigned nt = (unsigned)((n + AT - 1) / AT);
-  if (tiles) {
-    if (ntiles > 0)
-      hipLaunchKernelGGL(k_symv_tiles, dim3((unsigned)ntiles), dim3(256), 0, st, K, ld, n, alpha,
-                         kapart, npad, tiles, G);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL(k_symv_tiles, dim3(nt, nt), dim3(256), 0, st, K, ld, n, alpha, kapart, npad,
-                     tiles, G);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
 // Dispatch over the compiled feature-count buckets.
 // ---------------------------------------------------------------------------
 static const int kBuckets[] = {4, 8, 12, 16, 20, 24, 32, 48, 64};

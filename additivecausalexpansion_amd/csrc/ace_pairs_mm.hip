@@ -743,12 +743,16 @@ static hipError_t grad_mm_launch_dg(PairSide S, int B, int ZS, TabView tab, cons
   if (tiles && ndiag < 0)
     return grad_mm_launch_ps<PM, KIND, PS, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart,
                                                  st, tiles, nslot, nslot, G, lds, 0);
+  // strictly lower tiles first: the diagonal launch (one tile per CU) is
+  // then a short tail instead of sharing the machine with the side stream's
+  // Kfull * alpha pass at the start of the gradient phase
   const int64_t nd = tiles ? ndiag : (S.n + AT - 1) / AT;
-  hipError_t e = grad_mm_launch_ps<PM, KIND, PS, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart,
-                                                       trpart, st, tiles, nd, nslot, G, lds, 0);
+  hipError_t e = grad_mm_launch_ps<PM, KIND, PS, false>(S, B, ZS, tab, A, ld, sA, alpha, gpart,
+                                                        trpart, st, tiles, nslot - nd, nslot, G,
+                                                        lds, nd);
   if (e != hipSuccess) return e;
-  return grad_mm_launch_ps<PM, KIND, PS, false>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st,
-                                                tiles, nslot - nd, nslot, G, lds, nd);
+  return grad_mm_launch_ps<PM, KIND, PS, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st,
+                                               tiles, nd, nslot, G, lds, 0);
 }
 
 template <int PM, int KIND>

@@ -3,8 +3,7 @@
 // Layout: A (naug x naug, lower triangle, the AUG rows [y; 1] appended) is
 // split into NB-wide column blocks, block j on rank j % G, stored as local
 // block j / G of a naug x (nloc NB) column-major array with the global row
-// index (ace_internal.h lcol).  The Kfull copy for the RMSE uses the same
-// layout.  X, Z, y are replicated (<= 26 MB at C4).
+// index (ace_internal.h lcol).  X, Z, y are replicated (<= 26 MB at C4).
 //
 // One evaluation on rank r:
 //   assembly      own lower 64-tiles (+ identity padding, sigma diagonal)
@@ -17,9 +16,9 @@
 //                 block k+1 is updated first, then pack/exchange/chain of
 //                 panel k+1 run on the side stream under the bulk update.
 //   alpha         AUG rows of own columns -> all-reduce (u, v, corner)
-//   gradient      own 64-tiles of T = -A^-1 - alpha alpha^T; Kfull*alpha
-//                 partial rows from own tiles of the Kfull copy
-//   reduce        one all-reduce of [gradient sums | Kfull*alpha]
+//   gradient      own 64-tiles of T = -A^-1 - alpha alpha^T
+//   reduce        one all-reduce of the gradient sums (the RMSE residual is
+//                 sig alpha, k_final_sums: no pass over Kfull)
 // Every rank then holds identical sums and composes the same P-gradient.
 //
 // The communicator is RCCL (one process per GPU, loaded with dlopen so the
@@ -101,12 +100,12 @@ void nck(ace_ctx *ctx, ncclResult_t e, const char *what) {
 // ------------------------------------------------------------------ rank
 struct RankState {
   int r = 0;
-  DBuf A[2], kcopy;  // A[1]: train_stats scratch (keeps A[0]'s inverse, Q6)
+  DBuf A[2];  // A[1]: train_stats scratch (keeps A[0]'s inverse, Q6)
   DBuf P[2], W[2], SW, S[2], piv, flag, low, send, recv;
   DBuf tupd, tasm, tgrad;  // device tile lists
   int64_t nupd = 0, nasm = 0, ngrad = 0, ndiag = 0;
   std::vector<Tile> hupd;  // host copy (flop accounting)
-  DBuf y, tab, alpha, scal, gpart, trpart, kapart, red, sums, augvec;
+  DBuf y, tab, alpha, scal, gpart, trpart, red, sums, augvec;
   SideBufs side;
 };
 
@@ -348,9 +347,7 @@ ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int
     R->r = m->sim ? j : rank;
     const int64_t nloc = ncols_local(naug, world, R->r);
     alloc(ctx, R->A[0], (size_t)(naug * nloc) * sizeof(double), "alloc local A");
-    alloc(ctx, R->kcopy, (size_t)(naug * nloc) * sizeof(double), "alloc local Kfull copy");
     ck(ctx, hipMemsetAsync(R->A[0].p, 0, R->A[0].bytes, ctx->stream), "memset A");
-    ck(ctx, hipMemsetAsync(R->kcopy.p, 0, R->kcopy.bytes, ctx->stream), "memset Kfull copy");
     for (int b = 0; b < 2; ++b) {
       alloc(ctx, R->P[b], (size_t)(naug * NB) * sizeof(double), "alloc panel");
       alloc(ctx, R->W[b], (size_t)(naug * NB) * sizeof(double), "alloc panel");
@@ -382,7 +379,6 @@ ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int
     alloc(ctx, R->gpart, (size_t)(std::max<int64_t>(R->ngrad, 1) * ncol) * sizeof(double),
           "alloc gpart");
     alloc(ctx, R->trpart, (size_t)std::max<int64_t>(R->ngrad, 1) * sizeof(double), "alloc trpart");
-    alloc(ctx, R->kapart, (size_t)(m->ntr * npad) * sizeof(double), "alloc kapart");
     alloc(ctx, R->red, (size_t)(ncol + 1 + npad) * sizeof(double), "alloc reduction");
     alloc(ctx, R->sums, 8 * sizeof(double), "alloc sums");
     alloc(ctx, R->augvec, (size_t)(2 * npad + 8) * sizeof(double), "alloc aug vector");
@@ -427,6 +423,7 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
   const int ncol = s.B * (s.PM + 1);
   const int64_t naug = m->naug, npad = m->npad, n = m->n;
   std::vector<double> tab = make_tab(theta, s);
+  const double sig = std::exp(theta[0]);
   for (auto &R : m->ranks) {
     if (which == 1) {
       alloc(ctx, R->A[1], R->A[0].bytes, "alloc local A (train stats)");
@@ -443,8 +440,8 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
     const TabView tv = tab_view(R.tab, s);
     const PairSide ps = R.side.view(n);
     if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_asm[0], st), "event");
-    ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, npad, s.B, s.ZS, tv, std::exp(theta[0]),
-                            R.A[which].d(), naug, R.kcopy.d(), st, R.tasm.p ? (const Tile *)R.tasm.p : nullptr,
+    ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, npad, s.B, s.ZS, tv, sig, R.A[which].d(),
+                            naug, nullptr, st, R.tasm.p ? (const Tile *)R.tasm.p : nullptr,
                             R.nasm, m->G),
        "assembly");
     if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_asm[1], st), "event");
@@ -461,7 +458,7 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
     ck(ctx, launch_alpha_from_vec(R->augvec.d(), npad, n, theta[1], use_mu, R->alpha.d(),
                                   R->scal.d(), st),
        "alpha");
-  // gradient partial sums and Kfull * alpha partial rows of own tiles
+  // gradient partial sums of own tiles
   for (size_t j = 0; j < m->ranks.size(); ++j) {
     RankState &R = *m->ranks[j];
     const TabView tv = tab_view(R.tab, s);
@@ -472,20 +469,16 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
                         nullptr, R.gpart.d(), R.trpart.d(), st, tg, R.ngrad, m->G, R.ndiag),
        "grad");
     if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_grad[1], st), "event");
-    ck(ctx, hipMemsetAsync(R.kapart.p, 0, R.kapart.bytes, st), "memset kapart");
-    ck(ctx, launch_symv_tiles(R.kcopy.d(), naug, n, R.alpha.d(), R.kapart.d(), npad, st, tg,
-                              R.ngrad, m->G),
-       "symv");
     ck(ctx, hipMemsetAsync(R.red.p, 0, R.red.bytes, st), "memset reduction");
     if (R.ngrad > 0) {
       ck(ctx, launch_colsum(R.gpart.d(), R.ngrad, ncol, R.red.d(), st), "colsum");
       ck(ctx, launch_colsum(R.trpart.d(), R.ngrad, 1, R.red.d() + ncol, st), "colsum");
     }
-    ck(ctx, launch_rowsum(R.kapart.d(), m->ntr, npad, n, R.red.d() + ncol + 1, st), "rowsum");
   }
-  allreduce(*m, 1, ncol + 1 + npad, st);
+  allreduce(*m, 1, ncol + 1, st);
+  // RMSE residual ybar - Kfull alpha = sig alpha (k_final_sums): no Kfull pass
   for (auto &R : m->ranks)
-    ck(ctx, launch_final_sums(R->y.d(), R->scal.d() + 4, R->alpha.d(), R->red.d() + ncol + 1, n,
+    ck(ctx, launch_final_sums(R->y.d(), R->scal.d() + 4, R->alpha.d(), nullptr, sig, n,
                               R->piv.d(), npad, R->sums.d(), st),
        "final sums");
   RankState &R0 = *m->ranks[0];

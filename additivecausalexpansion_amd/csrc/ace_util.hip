@@ -162,34 +162,22 @@ hipError_t launch_colsum(const double *in, int64_t nrows, int ncols, double *out
   return hipGetLastError();
 }
 
-__global__ void k_rowsum(const double *__restrict__ in, int64_t ntr, int64_t npad, int64_t n,
-                         double *__restrict__ out) {
-  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= n) return;
-  double s = 0.0;
-  for (int64_t T = 0; T < ntr; ++T) s += in[T * npad + x];
-  out[x] = s;
-}
-
-hipError_t launch_rowsum(const double *in, int64_t ntr, int64_t npad, int64_t n, double *out,
-                         hipStream_t st) {
-  hipLaunchKernelGGL(k_rowsum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, ntr,
-                     npad, n, out);
-  return hipGetLastError();
-}
-
+// s = Kfull alpha (explicit, the ABI path) or null: then the fused model's
+// identity ybar - Kfull alpha = sig alpha is used -- A = Kfull + sig I is the
+// matrix the sweep inverted and alpha = A^-1 ybar, so the residual of
+// src/stats_cpp.cpp:25 needs no pass over Kfull.
 __global__ __launch_bounds__(256) void k_final_sums(const double *__restrict__ y,
                                                     const double *__restrict__ mup,
                                                     const double *__restrict__ alpha,
-                                                    const double *__restrict__ s, int64_t n,
-                                                    const double *__restrict__ piv,
+                                                    const double *__restrict__ s, double sig,
+                                                    int64_t n, const double *__restrict__ piv,
                                                     int64_t npiv, double *__restrict__ sums) {
   __shared__ double sh[4];
   const double mu = *mup;
   double e2 = 0.0, ya = 0.0, sa = 0.0, ld = 0.0;
   for (int64_t x = threadIdx.x; x < n; x += 256) {
     const double ybar = y[x] - mu;
-    const double e = ybar - s[x];
+    const double e = s ? ybar - s[x] : sig * alpha[x];
     e2 += e * e;
     ya += y[x] * alpha[x];
     sa += alpha[x];
@@ -208,9 +196,9 @@ __global__ __launch_bounds__(256) void k_final_sums(const double *__restrict__ y
 }
 
 hipError_t launch_final_sums(const double *y, const double *mu, const double *alpha, const double *s,
-                             int64_t n, const double *piv, int64_t npiv, double *sums,
-                             hipStream_t st) {
-  hipLaunchKernelGGL(k_final_sums, dim3(1), dim3(256), 0, st, y, mu, alpha, s, n, piv, npiv,
+                             double sig, int64_t n, const double *piv, int64_t npiv,
+                             double *sums, hipStream_t st) {
+  hipLaunchKernelGGL(k_final_sums, dim3(1), dim3(256), 0, st, y, mu, alpha, s, sig, n, piv, npiv,
                      sums);
   return hipGetLastError();
 }

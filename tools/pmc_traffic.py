@@ -26,7 +26,7 @@ KERNELS = {
     "k_panel_gemm": "ace::k_panel_gemm(",
     "k_grad2": "ace::k_grad2<",
     "k_asm_mm": "ace::k_asm_mm<",
-    "k_symv_tiles": "ace::k_symv_tiles(",
+    "k_grad_mm": "ace::k_grad_mm<",
 }
 
 
