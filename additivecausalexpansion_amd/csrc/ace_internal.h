@@ -124,7 +124,7 @@ struct SweepTiming {
 // (A^-1 R)^T and the corner -R^T A^-1 R.
 hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sync,
                      const SweepTiming *timing);
-int64_t update_gemm_tiles(int64_t naug, int64_t k0, int kx, bool look);
+double update_gemm_tiles(int64_t naug, int64_t k0, int kx, bool look);
 
 // ---- sharded sweep (one rank's view; ace_shard.cpp drives the steps) --------
 // Step k on rank r:  shard_pack -> [exchange: broadcast `low` from rank k%G,

@@ -185,17 +185,18 @@ ShardSweep sweep_view(const ShardModel &m, RankState &R, int which) {
 }
 
 // GEMM flops of one k_update launch on a tile list (tiles outside block k
-// and outside the cross of kx)
-double update_flops(const std::vector<Tile> &tl, int64_t k0, int kx) {
+// and outside the cross of kx; a tile of the AUG row block computes 16 rows)
+double update_flops(const std::vector<Tile> &tl, int64_t naug, int64_t k0, int kx) {
   const int KT = NB / UT, kt0 = (int)(k0 / UT), kt1 = kt0 + KT;
-  int64_t cnt = 0;
+  const int taug = (int)(naug / UT) - 1;
+  double cnt = 0.0;
   for (const Tile &t : tl) {
     if (kx >= 0 && ((t.I >= kx * KT && t.I < (kx + 1) * KT) || (t.J >= kx * KT && t.J < (kx + 1) * KT)))
       continue;
     const bool Ik = t.I >= kt0 && t.I < kt1, Jk = t.J >= kt0 && t.J < kt1;
-    if (!(Ik || Jk)) ++cnt;
+    if (!(Ik || Jk)) cnt += (t.I == taug) ? 16.0 / UT : 1.0;
   }
-  return (double)cnt * 2.0 * UT * UT * NB;
+  return cnt * 2.0 * UT * UT * NB;
 }
 
 // ---- collectives over the local ranks -------------------------------------
@@ -298,7 +299,7 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
       if (tm && j == 0) {
         ck(ctx, hipEventRecord(m.ev_upd[(size_t)m.upd_used + 1], st), "event");
         m.upd_flops[(size_t)m.upd_used / 2] =
-            update_flops(m.ranks[0]->hupd, (int64_t)k * NB, more ? k + 1 : -1);
+            update_flops(m.ranks[0]->hupd, m.naug, (int64_t)k * NB, more ? k + 1 : -1);
         m.upd_used += 2;
       }
     }

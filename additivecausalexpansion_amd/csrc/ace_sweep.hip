@@ -421,8 +421,33 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
   }
 
   const int lane = tid & 63, wv = tid >> 6;
-  const int wr = wv & 1, wc = wv >> 1;  // rows 64*wr.., cols 32*wc..
   const int lr = lane & 15, lk = lane >> 4;
+  if (R0 >= ld - AUG) {
+    // tile of the AUG row block: only its first 16 rows (y, 1 and zero
+    // padding) are live, the rest stay zero.  Wave wv does the 16 x 16 block
+    // of columns 16 wv.. straight from the panels (same k order as below, so
+    // the same results), 1/8 of a full tile's MFMAs.
+    d4 acc;
+    const int64_t r = R0 + lr;
+    const int64_t c = L0 + 16 * wv + lk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = A[r + (c + 4 * j) * ld];
+    const double *gr = Rop + R0 + lr + (int64_t)lk * ldp;
+    const double *gc = Cop + C0 + 16 * wv + lr + (int64_t)lk * ldp;
+    double an = gc[0], bn = gr[0];
+    for (int kk = 0; kk < NB / 4; ++kk) {
+      const double a = an, bb = bn;
+      if (kk + 1 < NB / 4) {
+        an = gc[(int64_t)(4 * (kk + 1)) * ldp];
+        bn = gr[(int64_t)(4 * (kk + 1)) * ldp];
+      }
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) A[r + (c + 4 * j) * ld] = acc[j];
+    return;
+  }
+  const int wr = wv & 1, wc = wv >> 1;  // rows 64*wr.., cols 32*wc..
   d4 acc[2][4];
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci)
@@ -520,6 +545,7 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
   }
   const int64_t R0 = (int64_t)I * XT, C0 = (int64_t)J * XT;
   if (!owns_col(C0, G, rank)) return;
+  if (R0 >= ld - AUG + XT) return;  // AUG rows 64..127: zero padding, stays zero
   const int64_t L0 = lcol(C0, G);
   const int kt0 = (int)(k0 / XT), kt1 = kt0 + KX;
   const bool Ik = I >= kt0 && I < kt1, Jk = J >= kt0 && J < kt1;
@@ -721,16 +747,18 @@ static hipError_t panel_sweep(const SweepBufs &b, int buf, int64_t k0, hipStream
   return hipGetLastError();
 }
 
-int64_t update_gemm_tiles(int64_t naug, int64_t k0, int kx, bool look) {
+// GEMM tiles of one k_update launch, in full-tile units: a tile of the AUG
+// row block computes 16 of its 128 rows.
+double update_gemm_tiles(int64_t naug, int64_t k0, int kx, bool look) {
   const int64_t nT = naug / UT, KT = NB / UT, kt0 = k0 / UT, kt1 = kt0 + KT;
-  int64_t cnt = 0;
+  double cnt = 0.0;
   for (int64_t I = 0; I < nT; ++I)
     for (int64_t J = 0; J <= I; ++J) {
       const bool inx = kx >= 0 && ((I >= kx * KT && I < (kx + 1) * KT) ||
                                    (J >= kx * KT && J < (kx + 1) * KT));
       if (inx != look) continue;
       const bool Ik = I >= kt0 && I < kt1, Jk = J >= kt0 && J < kt1;
-      if (!(Ik || Jk)) ++cnt;
+      if (!(Ik || Jk)) cnt += (I == nT - 1) ? 16.0 / UT : 1.0;
     }
   return cnt;
 }
@@ -793,7 +821,7 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
     if (timed) {
       (void)hipEventRecord(tm->ev[used + 1], st);
       if (tm->flops) tm->flops[used / 2] =
-          (double)update_gemm_tiles(naug, k0, more ? k + 1 : -1, false) * 2.0 * UT * UT * NB;
+          update_gemm_tiles(naug, k0, more ? k + 1 : -1, false) * 2.0 * UT * UT * NB;
       used += 2;
     }
     e = hipGetLastError();
