@@ -680,9 +680,15 @@ hipError_t launch_grad(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                        const double *A, int64_t ld, double sA, const double *alpha,
                        const double *cube, double *gpart, double *trpart, hipStream_t st,
                        const Tile *tiles, int64_t ntiles, int G, int64_t ndiag) {
-  if (!cube && pairs_use_mm(PM, true) && mm_lds_ok(PM, B, kind, true))
+  // The all-VALU gradient kernels keep per-lane p-long arrays and static LDS
+  // that outgrow the 64 KB default at PM = 64: above PM = 48 the MFMA kernel
+  // always runs, and it recomputes K_b instead of reading a given cube (the
+  // cube is kernmat's K_b for the same theta, so the traces are the same).
+  const bool valu_ok = PM <= 48;
+  if ((!cube || !valu_ok) && (pairs_use_mm(PM, true) || !valu_ok) && mm_lds_ok(PM, B, kind, true))
     return launch_grad_mm(kind, PM, S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st, tiles,
                           ntiles, G, ndiag);
+  if (!valu_ok) return hipErrorInvalidValue;
   switch (PM) {
 #define ACE_CASE(P) \
   case P:           \

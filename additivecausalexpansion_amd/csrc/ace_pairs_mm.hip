@@ -785,13 +785,15 @@ static hipError_t grad_mm_pm(int kind, PairSide S, int B, int ZS, TabView tab, c
                                            tiles, nslot, ndiag, G);
 }
 
-// Whether the per-tile staging of the MFMA kernels fits the LDS budget
-// (two workgroups per CU); above it the VALU kernels take over.
+// Whether the per-tile staging of the MFMA kernels fits the 160 KB of LDS
+// a gfx950 workgroup can use (up to 80 KB two workgroups share a CU; above
+// it one, at large B and p).  Every supported shape (B <= 32, p <= 64)
+// fits: the largest, SE at PM = 64 and B = 32, stages 127 KB.
 bool mm_lds_ok(int PM, int B, int kind, bool grad) {
   const int nwave = grad ? 4 * (4 / grad_cb(PM, kind)) : 4;
   return (int64_t)mm_layout(PM, B, kind == 0 ? 0 : 1, grad, nwave).total *
              (int64_t)sizeof(double) <=
-         80 * 1024;
+         160 * 1024;
 }
 
 hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView tab,

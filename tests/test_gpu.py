@@ -156,6 +156,30 @@ def test_grad_golden(A, O, name, with_cube):
     assert A.mu_solution_cpp(d["y"], d["inv"]) == pytest.approx(float(d["mu"]), rel=1e-9)
 
 
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+@pytest.mark.parametrize("p", [48, 64])
+@pytest.mark.parametrize("with_cube", [True, False])
+def test_grad_abi_large_p(A, O, kernel, p, with_cube):
+    """ABI gradient at the largest feature buckets, with and without the K
+    cube (above PM = 48 the MFMA kernel recomputes K_b instead of reading the
+    cube; the all-VALU kernels are only used up to PM = 48)."""
+    from additivecausalexpansion_amd.synthetic import make_problem
+    n, B = 150, 5
+    y, X, Z, th, sy = make_problem(n, p, B, seed=11)
+    sym, _, grad = O.KERNELS[kernel]
+    Kl = sym(X, Z, th)
+    inv = O.invkernel_cpp(Kl["full"], th[0])
+    st_ref = np.zeros(2)
+    g_ref = grad(y, X, Z, Kl["full"], Kl["elements"], inv["inv"], inv["eigenval"], th.copy(),
+                 st_ref, B, sy)
+    _, _, gdev = kern_fns(A, kernel)
+    st = np.zeros(2)
+    g = gdev(y, X, Z, Kl["full"], Kl["elements"] if with_cube else None, inv["inv"],
+             inv["eigenval"], th.copy(), st, B, sy)
+    close(g, g_ref)
+    close(st, st_ref)
+
+
 # ------------------------------------------------------------------ prediction
 @pytest.mark.parametrize("kernel", ["SE", "Matern32"])
 def test_pred_golden(A, kernel):
@@ -180,12 +204,14 @@ def test_pred_golden(A, kernel):
 # ------------------------------------------------------------------ fused model
 @pytest.mark.parametrize("kernel", ["SE", "Matern32"])
 @pytest.mark.parametrize("n,p,B", [(300, 2, 5), (513, 3, 4), (1000, 20, 10), (130, 1, 2),
-                                   (600, 32, 5), (700, 40, 6), (300, 64, 3)])
+                                   (600, 32, 5), (700, 40, 6), (300, 64, 3), (200, 50, 32)])
 def test_model_para_update_matches_oracle(A, O, kernel, n, p, B):
     """One device-resident para_update (kernel + sweep + fused gradient) vs the
     oracle's kernmat_sym -> invkernel -> grad chain, at iter 1 (mu first) and 2.
-    p >= 25 runs the MFMA-expansion pair kernels (feature buckets 32/48/64),
-    p <= 24 the all-VALU ones."""
+    Every case runs the MFMA-expansion pair kernels (both gradient workgroup
+    shapes, diagonal and strictly lower tiles, per-slice and double-buffered
+    partials) except (200, 50, 32): its per-tile staging exceeds the LDS
+    budget and takes the all-VALU fallback."""
     from additivecausalexpansion_amd.synthetic import make_problem
     y, X, Z, th, sy = make_problem(n, p, B, seed=7)
     m = A.DeviceModel(kernel, n, p, B)
