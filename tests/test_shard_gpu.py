@@ -45,10 +45,12 @@ def _oracle_eval(O, kernel, y, X, Z, th, sy, B, it):
 
 @pytest.mark.parametrize("kernel", ["SE", "Matern32"])
 @pytest.mark.parametrize("world,n,p,B", [(2, 300, 2, 5), (3, 700, 3, 4), (4, 1000, 20, 10),
-                                          (8, 1100, 5, 3), (5, 130, 1, 2)])
+                                          (8, 1100, 5, 3), (5, 130, 1, 2), (3, 600, 50, 16),
+                                          (2, 400, 32, 12)])
 def test_sharded_sim_matches_oracle(A, O, kernel, world, n, p, B):
     """world simulated ranks; n not a multiple of 256, ranks owning no pivot
-    block (world 8 / 5 at small n), both kernels, iter 1 (mu first) and 2."""
+    block (world 8 / 5 at small n), both kernels, iter 1 (mu first) and 2;
+    C4- and C3-shaped feature/basis counts (p = 50, B = 16; p = 32, B = 12)."""
     from additivecausalexpansion_amd.synthetic import make_problem
     y, X, Z, th, sy = make_problem(n, p, B, seed=11)
     m = A.DeviceModel(kernel, n, p, B, world=world, rank=0, sharded=True)
