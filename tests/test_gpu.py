@@ -101,6 +101,28 @@ def test_assembly_every_feature_bucket(A, O, kernel, p):
     close(sym(X, Z, th)["full"], O.KERNELS[kernel][0](X, Z, th)["full"], 1e-12, 1e-12)
 
 
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+@pytest.mark.parametrize("p,B", [(50, 16), (64, 32), (20, 10)])
+def test_assembly_large_shapes_cube_and_cross(A, O, kernel, p, B):
+    """Symmetric and cross kernels with their n x n x B cubes at the largest
+    feature / basis counts (the ABI modes run the all-VALU assembly)."""
+    rng = np.random.default_rng(p + B)
+    n1, n2 = 70, 45
+    X1, X2 = rng.uniform(-1, 1, (n1, p)), rng.uniform(-1, 1, (n2, p))
+    Z1, Z2 = rng.normal(size=(n1, B - 1)), rng.normal(size=(n2, B - 1))
+    Z1[rng.random((n1, B - 1)) < 0.3] = 0
+    Z2[rng.random((n2, B - 1)) < 0.3] = 0
+    th = np.concatenate([[-1.0, 0.0], rng.normal(0, .3, B), rng.normal(2.5, .3, B * p)])
+    sym, cross, _ = kern_fns(A, kernel)
+    osym, ocross = O.KERNELS[kernel][0], O.KERNELS[kernel][1]
+    r, ref = sym(X1, Z1, th), osym(X1, Z1, th)
+    close(r["full"], ref["full"], 1e-12, 1e-12)
+    close(r["elements"], ref["elements"], 1e-12, 1e-12)
+    r, ref = cross(X1, X2, Z1, Z2, th), ocross(X1, X2, Z1, Z2, th)
+    close(r["full"], ref["full"], 1e-12, 1e-12)
+    close(r["elements"], ref["elements"], 1e-12, 1e-12)
+
+
 def test_assembly_unsupported_shape_raises(A):
     with pytest.raises(A.AceError):
         A.kernmat_SE_symmetric_cpp(np.zeros((5, 65)), np.zeros((5, 1)), np.zeros(2 + 2 * 66))
