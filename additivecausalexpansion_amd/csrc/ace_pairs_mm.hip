@@ -109,9 +109,11 @@ __device__ __forceinline__ double exp_tb(double x, const double *tab) {
   return __builtin_amdgcn_ldexp(q * tab[ki & 31], ki >> 5);
 }
 
-// sqrt(x), x >= 0 and normal or 0 (r2 values): hardware rsq + the
-// Goldschmidt refinement of the library sequence, without its denormal
-// rescaling.  x = 0 gives 0 (the estimate is taken at max(x, 1e-300)).
+// sqrt(x), x >= 0 and normal or 0 (r2 values): hardware rsq (~2^-24
+// relative), one Goldschmidt step and one correction -- 0 ulp against the
+// correctly rounded sqrt over 4M samples (tools/probe_trans.hip; the
+// library adds a second correction and denormal rescaling).  x = 0 gives 0
+// (the estimate is taken at max(x, 1e-300)).
 __device__ __forceinline__ double sqrt_pk(double x) {
   const double y = __builtin_amdgcn_rsq(fmax(x, 1e-300));
   double s = x * y;
@@ -119,9 +121,7 @@ __device__ __forceinline__ double sqrt_pk(double x) {
   const double e = fma(-h, s, 0.5);
   s = fma(s, e, s);
   h = fma(h, e, h);
-  double d = fma(-s, s, x);
-  s = fma(d, h, s);
-  d = fma(-s, s, x);
+  const double d = fma(-s, s, x);
   return fma(d, h, s);
 }
 
@@ -424,11 +424,11 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
 // kernel weights (Q1), so the factor 1 + sqrt3 t of slice b+1 is cached per
 // pair; the last slice gets its own GEMM with wg[B-1].
 // ---------------------------------------------------------------------------
+// 1/f for f >= 1: v_rcp_f64 (~2^-24 relative) and one Newton step, <= 11
+// ulp (tools/probe_trans.hip) -- ample for a factor of the trace sums.
 __device__ __forceinline__ double rcp_nr_mm(double f) {
-  double q = __builtin_amdgcn_rcp(f);
-  double e = fma(-f, q, 1.0);
-  q = fma(q, e, q);
-  e = fma(-f, q, 1.0);
+  const double q = __builtin_amdgcn_rcp(f);
+  const double e = fma(-f, q, 1.0);
   return fma(q, e, q);
 }
 
