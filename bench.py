@@ -101,6 +101,29 @@ def pmc_traffic(kernel="k_update"):
         return None, None
 
 
+def pair_hbm_gbs(asm_ms, grad_ms):
+    """HBM GB/s of the fused assembly and gradient phases (SURVEY §8d asks for
+    them beside their VALU/MFMA rates): PMC bytes per eval from the newest
+    profiles/rNN_pmc_traffic.json (one assembly launch and the gradient
+    launches of each eval) over this run's phase times."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None
+    try:
+        ks = json.load(open(files[-1]))["kernels"]
+        a, g = ks["k_asm_mm"], ks["k_grad_mm"]
+        evals = a["launches"]
+        asm_b = a["traffic"]
+        grad_b = g["traffic"] * g["launches"] / evals
+    except (KeyError, ValueError, OSError, ZeroDivisionError):
+        return None
+    return {"assembly": asm_b / (asm_ms * 1e-3) / 1e9 if asm_ms else None,
+            "gradient": grad_b / (grad_ms * 1e-3) / 1e9 if grad_ms else None,
+            "bytes_per_eval": {"assembly": asm_b, "gradient": grad_b},
+            "source": os.path.relpath(files[-1], ROOT)}
+
+
 def cpu_baseline(cfg, timeout=240):
     """Rank 0 / N=1 only: the oracle leg in a subprocess (bounded)."""
     from additivecausalexpansion_amd.synthetic import CONFIGS
@@ -288,6 +311,7 @@ def main():
             "pair_kernels_tflops": {
                 "assembly": asm_work / (asm_ms * 1e-3) / 1e12 if asm_ms else None,
                 "gradient": grad_work / (grad_ms * 1e-3) / 1e12 if grad_ms else None},
+            "pair_kernels_hbm_gbs": pair_hbm_gbs(asm_ms / a.steps, grad_ms / a.steps),
             "last_stats": [float(stats[0]), float(stats[1])],
         }
         if world == 1 and not a.no_cpu_baseline:
