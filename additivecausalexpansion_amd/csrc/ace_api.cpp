@@ -159,7 +159,7 @@ struct SweepWork {
     const size_t need = (size_t)(2 * (npad / NB) + 1);
     while (ev.size() < need) {
       hipEvent_t e;
-      ck(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+      ck(ctx, hipEventCreateWithFlags(&e, ACE_SYNC_EVENT_FLAGS), "event");
       ev.push_back(e);
     }
   }
@@ -609,10 +609,10 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
     const int steps = (int)(m->npad / NB);
     m->ev_upd.assign((size_t)(2 * steps), nullptr);
     m->upd_flops.assign((size_t)steps, 0.0);
-    for (auto &e : m->ev_upd) ck(ctx, hipEventCreate(&e), "event");
+    for (auto &e : m->ev_upd) ck(ctx, hipEventCreateWithFlags(&e, ACE_TIMING_EVENT_FLAGS), "event");
     for (int j = 0; j < 2; ++j) {
-      ck(ctx, hipEventCreate(&m->ev_asm[j]), "event");
-      ck(ctx, hipEventCreate(&m->ev_grad[j]), "event");
+      ck(ctx, hipEventCreateWithFlags(&m->ev_asm[j], ACE_TIMING_EVENT_FLAGS), "event");
+      ck(ctx, hipEventCreateWithFlags(&m->ev_grad[j], ACE_TIMING_EVENT_FLAGS), "event");
     }
     sync(ctx);
   } catch (const Fail &f) {

@@ -387,14 +387,14 @@ ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int
   }
   if (!m->sim) {
     m->ev.assign((size_t)(2 * steps + 1), nullptr);
-    for (auto &e : m->ev) ck(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+    for (auto &e : m->ev) ck(ctx, hipEventCreateWithFlags(&e, ACE_SYNC_EVENT_FLAGS), "event");
   }
   m->ev_upd.assign((size_t)(2 * steps), nullptr);
   m->upd_flops.assign((size_t)steps, 0.0);
-  for (auto &e : m->ev_upd) ck(ctx, hipEventCreate(&e), "event");
+  for (auto &e : m->ev_upd) ck(ctx, hipEventCreateWithFlags(&e, ACE_TIMING_EVENT_FLAGS), "event");
   for (int j = 0; j < 2; ++j) {
-    ck(ctx, hipEventCreate(&m->ev_asm[j]), "event");
-    ck(ctx, hipEventCreate(&m->ev_grad[j]), "event");
+    ck(ctx, hipEventCreateWithFlags(&m->ev_asm[j], ACE_TIMING_EVENT_FLAGS), "event");
+    ck(ctx, hipEventCreateWithFlags(&m->ev_grad[j], ACE_TIMING_EVENT_FLAGS), "event");
   }
   sync(ctx);
   return m.release();
