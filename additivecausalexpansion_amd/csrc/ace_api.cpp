@@ -3,6 +3,7 @@
 // and the device-resident para_update pipeline.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -11,6 +12,7 @@
 #include <vector>
 
 #include "../../include/ace_hip.h"
+
 #include "ace_common.h"
 #include "ace_internal.h"
 
@@ -497,6 +499,7 @@ struct ace_model {
   bool has_data = false;
   SideBufs side;
   DBuf y, tab, alpha, scal, gpart, trpart, gsum, sums;
+  PinnedBuf hio;  // [theta tables | gsum | sums | scal | flag] host staging
   SweepWork sw;   // A = resident inverse of the last para_update
   SweepWork sw2;  // train_stats scratch (keeps sw's inverse, Q6)
   bool prof = false;
@@ -517,7 +520,11 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   hipStream_t st = ctx->stream;
   const Shape &s = m->s;
   std::vector<double> tab = make_tab(theta, s);
-  ck(ctx, hipMemcpy(m->tab.p, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice),
+  // pinned staging, async on the stream: the previous evaluation's results
+  // were synchronised before this one started, so the region is free
+  double *h = m->hio.ensure(ctx, tab.size() + (size_t)(s.B * (s.PM + 1) + 1) + 4 + 5 + 1);
+  std::copy(tab.begin(), tab.end(), h);
+  ck(ctx, hipMemcpyAsync(m->tab.p, h, tab.size() * sizeof(double), hipMemcpyHostToDevice, st),
      "upload tables");
   const TabView tv = tab_view(m->tab, s);
   const PairSide ps = m->side.view(m->n);
@@ -684,12 +691,19 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, d
     if (timed) shard_collect_timing(m->shard, m->t_ms, m->t_launch, m->t_work);
   } else {
     model_pipeline(m, m->sw, theta, iter == 1 ? 1 : 0, timed);
-    download(ctx, gs.data(), m->gsum.d(), gs.size(), "download gsum");
-    download(ctx, sums, m->sums.d(), 4, "download sums");
-    download(ctx, scal, m->scal.d(), 5, "download scal");
-    ck(ctx, hipMemcpyAsync(&flag, m->sw.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
+    // into the pinned region behind the tables, one synchronisation
+    double *h = m->hio.p + (2 * s.B * s.PM + s.B);
+    download(ctx, h, m->gsum.d(), gs.size(), "download gsum");
+    download(ctx, h + gs.size(), m->sums.d(), 4, "download sums");
+    download(ctx, h + gs.size() + 4, m->scal.d(), 5, "download scal");
+    int *hflag = reinterpret_cast<int *>(h + gs.size() + 9);
+    ck(ctx, hipMemcpyAsync(hflag, m->sw.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
        "download flag");
     sync(ctx);
+    std::copy(h, h + gs.size(), gs.begin());
+    std::copy(h + gs.size(), h + gs.size() + 4, sums);
+    std::copy(h + gs.size() + 4, h + gs.size() + 9, scal);
+    flag = *hflag;
     if (timed) model_collect_timing(m);
   }
   if (iter == 1) theta[1] = scal[3];  // mean_solution before the gradient (R/kernel_SE_R6.R:45)

@@ -95,6 +95,31 @@ inline void download(ace_ctx *ctx, double *h, const double *d, size_t count, con
                                     ctx->stream), what);
 }
 
+// Pinned host staging for the per-evaluation traffic (theta tables up, the
+// gradient sums and statistics down): pageable copies each take a host
+// round trip through the runtime's staging buffer (~100 us apiece).
+struct PinnedBuf {
+  double *p = nullptr;
+  size_t n = 0;
+  PinnedBuf() = default;
+  PinnedBuf(const PinnedBuf &) = delete;
+  PinnedBuf &operator=(const PinnedBuf &) = delete;
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  double *ensure(ace_ctx *ctx, size_t count) {
+    if (count > n) {
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      n = 0;
+      ck(ctx, hipHostMalloc((void **)&p, count * sizeof(double), hipHostMallocDefault),
+         "pinned host alloc");
+      n = count;
+    }
+    return p;
+  }
+};
+
 inline void sync(ace_ctx *ctx) { ck(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize"); }
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
