@@ -528,15 +528,25 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
      "upload tables");
   const TabView tv = tab_view(m->tab, s);
   const PairSide ps = m->side.view(m->n);
-  if (timed) ck(ctx, hipEventRecord(m->ev_asm[0], st), "event");
   const double sig = std::exp(theta[0]);
-  ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
-                          nullptr, st),
-     "assembly");
-  if (timed) ck(ctx, hipEventRecord(m->ev_asm[1], st), "event");
   ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, m->n, m->y.d(), st), "aug init");
   ck(ctx, hipMemsetAsync(w.flag.p, 0, sizeof(int), st), "memset flag");
-  const SweepSync sy = w.sync(ctx);
+  SweepSync sy = w.sync(ctx);
+  // the first panel's columns first: the sweep's first pivot chain (side
+  // stream) then runs under the rest of the assembly
+  if (timed) ck(ctx, hipEventRecord(m->ev_asm[0], st), "event");
+  ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
+                          nullptr, st, nullptr, 0, 1, 1),
+     "assembly (first panel)");
+  const int steps = (int)(w.npad / NB);
+  if (sy.side && sy.nev >= 2 * steps + 1) {  // run_sweep's "inputs ready" event
+    ck(ctx, hipEventRecord(sy.ev[2 * steps], st), "event");
+    sy.ready_recorded = true;
+  }
+  ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
+                          nullptr, st, nullptr, 0, 1, 2),
+     "assembly");
+  if (timed) ck(ctx, hipEventRecord(m->ev_asm[1], st), "event");
   SweepTiming tmg;
   tmg.ev = m->ev_upd.data();
   tmg.nev = (int)m->ev_upd.size();

@@ -59,17 +59,20 @@ struct PairSide {
 //         cube is non-null it receives the lower Kfull (same ld).
 // mode 1: symmetric ABI output -- full n x n Kfull (ld = n) + optional cube.
 // mode 2: cross ABI output -- n1 x n2 Kfull + optional cube.
+// part (mode 0 without a tile list): 0 all tiles, 1 the first panel's
+// columns (J < NB/AT), 2 the rest -- 1 then 2 lets the sweep's first pivot
+// chain start while part 2 runs.
 hipError_t launch_assembly(int mode, int kind, int PM, PairSide rows,
                            PairSide cols, int64_t npad, int B, int ZS,
                            TabView tab, double sig, double *out, int64_t ld,
                            double *cube, hipStream_t st, const Tile *tiles = nullptr,
-                           int64_t ntiles = 0, int G = 1);
+                           int64_t ntiles = 0, int G = 1, int part = 0);
 
 // MFMA-expansion variant of mode 0 (ace_pairs_mm.hip)
 hipError_t launch_assembly_mm(int kind, int PM, PairSide S, int64_t npad, int B, int ZS,
                               TabView tab, double sig, double *out, int64_t ld,
                               double *kcopy, hipStream_t st, const Tile *tiles,
-                              int64_t ntiles, int G);
+                              int64_t ntiles, int G, int part = 0);
 bool pairs_use_mm(int PM, bool grad);
 bool mm_lds_ok(int PM, int B, int kind, bool grad);
 hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
@@ -111,6 +114,7 @@ struct SweepSync {
   hipStream_t side;
   hipEvent_t *ev;
   int nev;
+  bool ready_recorded = false;  // caller already recorded ev[2 * steps] ("inputs ready")
 };
 // Optional timing of the dominant update launches (k_update<false>): event
 // pairs in ev, executed GEMM flops per timed launch in flops[].

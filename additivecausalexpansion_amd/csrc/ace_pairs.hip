@@ -635,10 +635,11 @@ bool pairs_use_mm(int PM, bool grad) {
 hipError_t launch_assembly(int mode, int kind, int PM, PairSide R, PairSide C, int64_t npad,
                            int B, int ZS, TabView tab, double sig, double *out, int64_t ld,
                            double *cube, hipStream_t st, const Tile *tiles, int64_t ntiles,
-                           int G) {
+                           int G, int part) {
   if (mode == 0 && pairs_use_mm(PM, false) && mm_lds_ok(PM, B, kind, false))
     return launch_assembly_mm(kind, PM, R, npad, B, ZS, tab, sig, out, ld, cube, st, tiles,
-                              ntiles, G);
+                              ntiles, G, part);
+  if (part == 2) return hipSuccess;  // the all-VALU path assembles everything in part 1
   switch (PM) {
 #define ACE_CASE(P) \
   case P:           \

@@ -336,10 +336,29 @@ template <int PM, int KIND>
 __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, int B, int ZS, TabView tab,
                                                 double sig, double *__restrict__ out, int64_t ld,
                                                 double *__restrict__ kcopy,
-                                                const Tile *__restrict__ tiles, int G) {
+                                                const Tile *__restrict__ tiles, int G, int part,
+                                                int nt) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   int64_t I, J;
-  tile_of(tiles, blockIdx.x, I, J);
+  // part 1: the tiles of the first panel's columns (J < NB / AT, column by
+  // column) -- what the sweep's first pivot chain needs; part 2: the rest
+  // (the lower triangle of tiles >= NB / AT); 0: every lower tile / the list
+  constexpr int JB = NB / AT;
+  if (tiles || part == 0) {
+    tile_of(tiles, blockIdx.x, I, J);
+  } else if (part == 1) {
+    int64_t idx = blockIdx.x;
+    J = 0;
+    while (idx >= nt - J) {
+      idx -= nt - J;
+      ++J;
+    }
+    I = J + idx;
+  } else {
+    tile_of(nullptr, blockIdx.x, I, J);
+    I += JB;
+    J += JB;
+  }
   if (G > 1) {
     const int64_t coff = lcol(J * AT, G) - J * AT;
     out += coff * ld;
@@ -815,9 +834,13 @@ hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView t
 template <int PM>
 static hipError_t asm_mm_pm(int kind, PairSide S, int64_t npad, int B, int ZS, TabView tab,
                             double sig, double *out, int64_t ld, double *kcopy, hipStream_t st,
-                            const Tile *tiles, int64_t ntiles, int G) {
-  const int64_t nt = npad / AT;
-  const int64_t nblk = tiles ? ntiles : nt * (nt + 1) / 2;
+                            const Tile *tiles, int64_t ntiles, int G, int part) {
+  const int64_t nt = npad / AT, JB = NB / AT;
+  if (tiles) part = 0;
+  const int64_t nblk = tiles ? ntiles
+                       : part == 1 ? JB * nt - JB * (JB - 1) / 2
+                       : part == 2 ? (nt - JB) * (nt - JB + 1) / 2
+                                   : nt * (nt + 1) / 2;
   if (nblk == 0) return hipSuccess;
   const size_t lds = (size_t)mm_layout(PM, B, kind == 0 ? 0 : 1, false).total * sizeof(double);
   if (lds > 65536) {
@@ -827,19 +850,20 @@ static hipError_t asm_mm_pm(int kind, PairSide S, int64_t npad, int B, int ZS, T
   }
   if (kind == 0)
     hipLaunchKernelGGL((k_asm_mm<PM, 0>), dim3((unsigned)nblk), dim3(256), lds, st, S, B, ZS,
-                       tab, sig, out, ld, kcopy, tiles, G);
+                       tab, sig, out, ld, kcopy, tiles, G, part, (int)nt);
   else
     hipLaunchKernelGGL((k_asm_mm<PM, 1>), dim3((unsigned)nblk), dim3(256), lds, st, S, B, ZS,
-                       tab, sig, out, ld, kcopy, tiles, G);
+                       tab, sig, out, ld, kcopy, tiles, G, part, (int)nt);
   return hipGetLastError();
 }
 
 hipError_t launch_assembly_mm(int kind, int PM, PairSide S, int64_t npad, int B, int ZS,
                               TabView tab, double sig, double *out, int64_t ld, double *kcopy,
-                              hipStream_t st, const Tile *tiles, int64_t ntiles, int G) {
+                              hipStream_t st, const Tile *tiles, int64_t ntiles, int G, int part) {
   switch (PM) {
 #define ACE_CASE(P) \
-  case P: return asm_mm_pm<P>(kind, S, npad, B, ZS, tab, sig, out, ld, kcopy, st, tiles, ntiles, G);
+  case P:           \
+    return asm_mm_pm<P>(kind, S, npad, B, ZS, tab, sig, out, ld, kcopy, st, tiles, ntiles, G, part);
     ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
     ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
 #undef ACE_CASE

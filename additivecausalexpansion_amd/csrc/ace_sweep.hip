@@ -778,8 +778,10 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
   int used = 0;
   hipError_t e;
   if (two) {
-    e = hipEventRecord(sy->ev[2 * steps], st);  // inputs ready
-    if (e != hipSuccess) return e;
+    if (!sy->ready_recorded) {
+      e = hipEventRecord(sy->ev[2 * steps], st);  // inputs ready
+      if (e != hipSuccess) return e;
+    }
     e = hipStreamWaitEvent(side, sy->ev[2 * steps], 0);
     if (e != hipSuccess) return e;
   }
