@@ -139,9 +139,9 @@ int ace_kernmat_cross(ace_ctx *ctx, int kind, int64_t n1, int64_t n2, int p, int
 // ------------------------------------------------------------ inverse
 namespace {
 struct SweepWork {
-  DBuf A, P0, P1, W0, W1, SW, S0, S1, piv, flag;
+  DBuf A, P0, P1, W0, W1, SW, S0, S1, piv, flag, order;
   std::vector<hipEvent_t> ev;
-  int64_t n = 0, npad = 0, naug = 0;
+  int64_t n = 0, npad = 0, naug = 0, norder = 0;
   SweepWork() = default;
   SweepWork(const SweepWork &) = delete;
   ~SweepWork() {
@@ -158,6 +158,14 @@ struct SweepWork {
     alloc(ctx, S1, (size_t)(SUB * NB) * sizeof(double), "alloc S");
     alloc(ctx, piv, (size_t)npad * sizeof(double), "alloc piv");
     alloc(ctx, flag, 16, "alloc flag");
+    norder = 0;
+    if (const int S = update_order_block(); S > 0) {
+      const std::vector<Tile> t = xcd_update_order(own_tiles(naug / UT, UT, 1, 0), S);
+      alloc(ctx, order, t.size() * sizeof(Tile), "alloc tile order");
+      ck(ctx, hipMemcpy(order.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
+         "upload tile order");
+      norder = (int64_t)t.size();
+    }
     const size_t need = (size_t)(2 * (npad / NB) + 1);
     while (ev.size() < need) {
       hipEvent_t e;
@@ -179,6 +187,8 @@ struct SweepWork {
     b.S[1] = S1.d();
     b.piv = piv.d();
     b.flag = flag.i();
+    b.order = norder ? reinterpret_cast<const Tile *>(order.p) : nullptr;
+    b.norder = norder;
     return b;
   }
   SweepSync sync(ace_ctx *ctx) {

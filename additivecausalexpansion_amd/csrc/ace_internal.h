@@ -1,6 +1,7 @@
 // ace_internal.h -- shared declarations between the HIP kernels
 // (ace_kernels.hip, ace_sweep.hip) and the host orchestration (ace_api.cpp).
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -107,7 +108,18 @@ struct SweepBufs {
   double *S[2];   // SUB x NB col-major: pivot rows before their sub-sweep (ping-pong)
   double *piv;    // npad pivots
   int *flag;      // set to 1 on a non-positive / non-finite pivot
+  const Tile *order = nullptr;  // k_update tile order (xcd_update_order), or row-major
+  int64_t norder = 0;
 };
+// k_update tile order: the tiles of `tl` grouped into S x S super-blocks of
+// 128-tiles that are dealt whole to the 8 XCDs; list index b runs on XCD
+// b % 8 (dispatch is round-robin).  Entries with I < 0 are padding.
+std::vector<Tile> xcd_update_order(const std::vector<Tile> &tl, int S);
+// own lower tiles of size T over [0, ntile*T) in row-major order (ace_shard.cpp)
+std::vector<Tile> own_tiles(int64_t ntile, int T, int G, int r);
+// super-block size S of that order (0: row-major grid); ACE_UPD_ORDER=S
+// overrides (diagnostic A/B switch)
+int update_order_block();
 // Lookahead: the panel sweep of step k+1 runs on `side` while the main
 // stream updates the rest of step k.  `ev` needs 2*steps + 1 events.
 struct SweepSync {

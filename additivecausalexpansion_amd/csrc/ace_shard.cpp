@@ -145,14 +145,6 @@ int64_t ncols_local(int64_t naug, int G, int r) {
   return cnt * NB;
 }
 
-// own lower tiles of size T over [0, ntile*T) in row-major order
-std::vector<Tile> own_tiles(int64_t ntile, int T, int G, int r) {
-  std::vector<Tile> t;
-  for (int64_t I = 0; I < ntile; ++I)
-    for (int64_t J = 0; J <= I; ++J)
-      if (owns_col(J * T, G, r)) t.push_back(Tile{(int)I, (int)J});
-  return t;
-}
 
 void upload_tiles(ace_ctx *ctx, DBuf &b, const std::vector<Tile> &t) {
   alloc(ctx, b, std::max<size_t>(t.size(), 1) * sizeof(Tile), "alloc tiles");
@@ -191,6 +183,7 @@ double update_flops(const std::vector<Tile> &tl, int64_t naug, int64_t k0, int k
   const int taug = (int)(naug / UT) - 1;
   double cnt = 0.0;
   for (const Tile &t : tl) {
+    if (t.I < 0) continue;  // padding of the XCD order
     if (kx >= 0 && ((t.I >= kx * KT && t.I < (kx + 1) * KT) || (t.J >= kx * KT && t.J < (kx + 1) * KT)))
       continue;
     const bool Ik = t.I >= kt0 && t.I < kt1, Jk = t.J >= kt0 && t.J < kt1;
@@ -362,6 +355,7 @@ ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int
     alloc(ctx, R->recv, (size_t)world * std::max(1, maxslots) * NB * NB * sizeof(double),
           "alloc exchange");
     R->hupd = own_tiles(naug / UT, UT, world, R->r);
+    if (const int S = update_order_block(); S > 0) R->hupd = xcd_update_order(R->hupd, S);
     R->nupd = (int64_t)R->hupd.size();
     upload_tiles(ctx, R->tupd, R->hupd);
     const std::vector<Tile> ta = own_tiles(npad / AT, AT, world, R->r);

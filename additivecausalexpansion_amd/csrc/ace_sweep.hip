@@ -24,6 +24,8 @@
 // y.alpha with no extra pass over the inverse.
 #include "ace_internal.h"
 
+#include <map>
+
 namespace ace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -359,6 +361,36 @@ constexpr int NCH = NB / BK;
 constexpr int UTHREADS = 512;
 static_assert(BK == 16, "staging maps 512 threads x 4 doubles onto a 128 x 16 chunk");
 
+// Write-back of an updated A element.  ACE_UPD_STORE 1: write-through store
+// that drops the line from the XCD's L2 (A tiles are read once per step, on
+// any XCD; keeping them out of L2 leaves it to the re-read panels); 2:
+// nontemporal; 0: plain.
+#ifndef ACE_UPD_STORE
+#define ACE_UPD_STORE 2
+#endif
+__device__ __forceinline__ void st_a(double *p, double v) {
+#if ACE_UPD_STORE == 1
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#elif ACE_UPD_STORE == 2
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+#ifndef ACE_UPD_X
+#define ACE_UPD_X 0  // 1: k_update_x uses the same load/store policy
+#endif
+#ifndef ACE_UPD_LOAD
+#define ACE_UPD_LOAD 1
+#endif
+__device__ __forceinline__ double ld_a(const double *p) {
+#if ACE_UPD_LOAD == 1
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 // Every lower tile except the "cross" of block kx (tiles with I or J in
 // block kx, updated earlier by k_update_x for the lookahead; kx < 0: none).
 // tiles == nullptr: all lower tiles, 1-D grid in row-major order; otherwise
@@ -377,6 +409,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
     const Tile tt = tiles[blockIdx.x];
     I = tt.I;
     J = tt.J;
+    if (I < 0) return;  // padding of the XCD order
   } else {
     const int t = blockIdx.x;
     int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
@@ -431,7 +464,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
     const int64_t r = R0 + lr;
     const int64_t c = L0 + 16 * wv + lk;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = A[r + (c + 4 * j) * ld];
+    for (int j = 0; j < 4; ++j) acc[j] = ld_a(&A[r + (c + 4 * j) * ld]);
     const double *gr = Rop + R0 + lr + (int64_t)lk * ldp;
     const double *gc = Cop + C0 + 16 * wv + lr + (int64_t)lk * ldp;
     double an = gc[0], bn = gr[0];
@@ -444,7 +477,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
       acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) A[r + (c + 4 * j) * ld] = acc[j];
+    for (int j = 0; j < 4; ++j) st_a(&A[r + (c + 4 * j) * ld], acc[j]);
     return;
   }
   const int wr = wv & 1, wc = wv >> 1;  // rows 64*wr.., cols 32*wc..
@@ -456,7 +489,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
       const int64_t r = R0 + 64 * wr + 16 * ri + lr;
       const int64_t c = L0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[ci][ri][j] = A[r + (c + 4 * j) * ld];
+      for (int j = 0; j < 4; ++j) acc[ci][ri][j] = ld_a(&A[r + (c + 4 * j) * ld]);
     }
   // staging: each thread moves 4 doubles of each operand per chunk
   const int sk = tid >> 5, sm = (tid & 31) * 4;
@@ -513,7 +546,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
       const int64_t r = R0 + 64 * wr + 16 * ri + lr;
       const int64_t c = L0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) A[r + (c + 4 * j) * ld] = acc[ci][ri][j];
+      for (int j = 0; j < 4; ++j) st_a(&A[r + (c + 4 * j) * ld], acc[ci][ri][j]);
     }
 }
 
@@ -581,7 +614,7 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
       const int64_t r = R0 + 32 * wr + 16 * ri + lr;
       const int64_t c = L0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[ci][ri][j] = A[r + (c + 4 * j) * ld];
+      for (int j = 0; j < 4; ++j) acc[ci][ri][j] = ACE_UPD_X ? ld_a(&A[r + (c + 4 * j) * ld]) : A[r + (c + 4 * j) * ld];
     }
   // staging: 256 threads x (4 doubles of each operand) per 64 x 16 chunk
   const int sk = tid >> 4, sm = (tid & 15) * 4;
@@ -638,7 +671,10 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
       const int64_t r = R0 + 32 * wr + 16 * ri + lr;
       const int64_t c = L0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) A[r + (c + 4 * j) * ld] = acc[ci][ri][j];
+      for (int j = 0; j < 4; ++j) {
+        if (ACE_UPD_X) st_a(&A[r + (c + 4 * j) * ld], acc[ci][ri][j]);
+        else A[r + (c + 4 * j) * ld] = acc[ci][ri][j];
+      }
     }
 }
 
@@ -763,6 +799,46 @@ double update_gemm_tiles(int64_t naug, int64_t k0, int kx, bool look) {
   return cnt;
 }
 
+int update_order_block() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_UPD_ORDER");
+    v = e ? std::max(0, atoi(e)) : 4;
+  }
+  return v;
+}
+
+std::vector<Tile> own_tiles(int64_t ntile, int T, int G, int r) {
+  std::vector<Tile> t;
+  for (int64_t I = 0; I < ntile; ++I)
+    for (int64_t J = 0; J <= I; ++J)
+      if (owns_col(J * T, G, r)) t.push_back(Tile{(int)I, (int)J});
+  return t;
+}
+
+std::vector<Tile> xcd_update_order(const std::vector<Tile> &tl, int S) {
+  // super-blocks (I / S, J / S) in row-major order; each goes whole to the
+  // XCD with the fewest tiles so far, so an XCD's in-flight tiles share few
+  // row / column panel blocks in its L2 (about -1 % per update launch at C2
+  // against every-eighth-tile dealing, profiles/r01_pairs_ab.txt)
+  constexpr int X = 8;
+  std::vector<std::vector<Tile>> q(X);
+  std::map<std::pair<int, int>, std::vector<Tile>> sb;
+  for (const Tile &t : tl) sb[{t.I / S, t.J / S}].push_back(t);
+  for (auto &kv : sb) {
+    int x = 0;
+    for (int i = 1; i < X; ++i)
+      if (q[i].size() < q[x].size()) x = i;
+    q[x].insert(q[x].end(), kv.second.begin(), kv.second.end());
+  }
+  size_t len = 0;
+  for (auto &v : q) len = std::max(len, v.size());
+  std::vector<Tile> out(len * X, Tile{-1, -1});
+  for (int x = 0; x < X; ++x)
+    for (size_t i = 0; i < q[x].size(); ++i) out[i * X + x] = q[x][i];
+  return out;
+}
+
 // Step k: the main stream runs only the bulk update of step k (every tile
 // outside the cross of block k+1).  The high-priority side stream, once the
 // bulk update of step k-1 is done, updates the cross of block k+1 with panel
@@ -817,9 +893,9 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
     }
     const bool timed = tm && tm->ev && used + 2 <= tm->nev;
     if (timed) (void)hipEventRecord(tm->ev[used], st);
-    hipLaunchKernelGGL(k_update, dim3(nT * (nT + 1) / 2), dim3(UTHREADS), 0, st, b.A, b.ld,
-                       b.W[buf], b.P[buf], b.W[buf], b.ld, k0, more ? k + 1 : -1,
-                       (const Tile *)nullptr, 1);
+    hipLaunchKernelGGL(k_update, dim3(b.order ? (unsigned)b.norder : nT * (nT + 1) / 2),
+                       dim3(UTHREADS), 0, st, b.A, b.ld, b.W[buf], b.P[buf], b.W[buf], b.ld, k0,
+                       more ? k + 1 : -1, b.order, 1);
     if (timed) {
       (void)hipEventRecord(tm->ev[used + 1], st);
       if (tm->flops) tm->flops[used / 2] =
