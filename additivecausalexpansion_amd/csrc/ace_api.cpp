@@ -513,10 +513,13 @@ struct ace_model {
   SweepWork sw;   // A = resident inverse of the last para_update
   SweepWork sw2;  // train_stats scratch (keeps sw's inverse, Q6)
   bool prof = false;
-  hipEvent_t ev_asm[2] = {nullptr, nullptr}, ev_grad[2] = {nullptr, nullptr};
-  std::vector<hipEvent_t> ev_upd;
-  std::vector<double> upd_flops;
-  int upd_used = 0;
+  // timing events in two sets: the set of evaluation t is read back while
+  // evaluation t+1 runs (no host queries between evaluations)
+  hipEvent_t ev_asm[4] = {}, ev_grad[4] = {};
+  std::vector<hipEvent_t> ev_upd;  // 2 sets x 2 * steps
+  std::vector<double> upd_flops;   // 2 sets x steps
+  int upd_used[2] = {0, 0};
+  int tset = 0, pend = -1;  // set the next timed evaluation records; set not yet read
   double t_ms[3] = {0, 0, 0};
   int64_t t_launch[3] = {0, 0, 0};
   double t_work[3] = {0, 0, 0};
@@ -544,7 +547,8 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   SweepSync sy = w.sync(ctx);
   // the first panel's columns first: the sweep's first pivot chain (side
   // stream) then runs under the rest of the assembly
-  if (timed) ck(ctx, hipEventRecord(m->ev_asm[0], st), "event");
+  const int ts = m->tset;
+  if (timed) ck(ctx, hipEventRecord(m->ev_asm[2 * ts], st), "event");
   ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
                           nullptr, st, nullptr, 0, 1, 1),
      "assembly (first panel)");
@@ -556,23 +560,24 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
                           nullptr, st, nullptr, 0, 1, 2),
      "assembly");
-  if (timed) ck(ctx, hipEventRecord(m->ev_asm[1], st), "event");
+  if (timed) ck(ctx, hipEventRecord(m->ev_asm[2 * ts + 1], st), "event");
   SweepTiming tmg;
-  tmg.ev = m->ev_upd.data();
-  tmg.nev = (int)m->ev_upd.size();
-  tmg.used = &m->upd_used;
-  tmg.flops = m->upd_flops.data();
+  const size_t nset = m->ev_upd.size() / 2;
+  tmg.ev = m->ev_upd.data() + ts * nset;
+  tmg.nev = (int)nset;
+  tmg.used = &m->upd_used[ts];
+  tmg.flops = m->upd_flops.data() + ts * (nset / 2);
   ck(ctx, run_sweep(w.bufs(), st, &sy, timed ? &tmg : nullptr), "sweep");
   ck(ctx, launch_alpha_from_aug(w.A.d(), w.naug, w.npad, m->n, theta[1], use_mu, m->alpha.d(),
                                 m->scal.d(), st),
      "alpha");
   // RMSE residual ybar - Kfull alpha = sig alpha (A = Kfull + sig I is what
   // the sweep inverted): no Kfull copy and no pass over it (k_final_sums)
-  if (timed) ck(ctx, hipEventRecord(m->ev_grad[0], st), "event");
+  if (timed) ck(ctx, hipEventRecord(m->ev_grad[2 * ts], st), "event");
   ck(ctx, launch_grad(s.kind, s.PM, ps, s.B, s.ZS, tv, w.A.d(), w.naug, -1.0, m->alpha.d(),
                       nullptr, m->gpart.d(), m->trpart.d(), st),
      "grad");
-  if (timed) ck(ctx, hipEventRecord(m->ev_grad[1], st), "event");
+  if (timed) ck(ctx, hipEventRecord(m->ev_grad[2 * ts + 1], st), "event");
   const int ncol = s.B * (s.PM + 1);
   ck(ctx, launch_colsum(m->gpart.d(), m->ntiles, ncol, m->gsum.d(), st), "colsum");
   ck(ctx, launch_colsum(m->trpart.d(), m->ntiles, 1, m->gsum.d() + ncol, st), "colsum");
@@ -581,21 +586,24 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
      "final sums");
 }
 
-void model_collect_timing(ace_model *m) {
-  const int nupd = m->upd_used;
+// Reads the event set `ts` of an evaluation whose work has completed.
+void model_collect_timing(ace_model *m, int ts) {
+  const int nupd = m->upd_used[ts];
+  const size_t nset = m->ev_upd.size() / 2;
+  const hipEvent_t *ev = m->ev_upd.data() + ts * nset;
+  const double *fl = m->upd_flops.data() + ts * (nset / 2);
   float ms = 0.f;
-  ck(m->ctx, hipEventElapsedTime(&ms, m->ev_asm[0], m->ev_asm[1]), "elapsed");
+  ck(m->ctx, hipEventElapsedTime(&ms, m->ev_asm[2 * ts], m->ev_asm[2 * ts + 1]), "elapsed");
   m->t_ms[1] += ms;
   m->t_launch[1] += 1;
-  ck(m->ctx, hipEventElapsedTime(&ms, m->ev_grad[0], m->ev_grad[1]), "elapsed");
+  ck(m->ctx, hipEventElapsedTime(&ms, m->ev_grad[2 * ts], m->ev_grad[2 * ts + 1]), "elapsed");
   m->t_ms[2] += ms;
   m->t_launch[2] += 1;
   for (int j = 0; j + 1 < nupd; j += 2) {
-    ck(m->ctx, hipEventElapsedTime(&ms, m->ev_upd[(size_t)j], m->ev_upd[(size_t)j + 1]),
-       "elapsed");
+    ck(m->ctx, hipEventElapsedTime(&ms, ev[j], ev[j + 1]), "elapsed");
     m->t_ms[0] += ms;
     m->t_launch[0] += 1;
-    m->t_work[0] += m->upd_flops[(size_t)(j / 2)];
+    m->t_work[0] += fl[j / 2];
   }
   const double n = (double)m->n, pairs = n * (n + 1) / 2, B = m->s.B, p = m->s.p;
   // work: the update launches' GEMM flops (counted per launch
@@ -634,10 +642,10 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
     alloc(ctx, m->sums, 8 * sizeof(double), "alloc sums");
     ck(ctx, hipMemsetAsync(m->sw.A.p, 0, m->sw.A.bytes, ctx->stream), "memset A");
     const int steps = (int)(m->npad / NB);
-    m->ev_upd.assign((size_t)(2 * steps), nullptr);
-    m->upd_flops.assign((size_t)steps, 0.0);
+    m->ev_upd.assign((size_t)(4 * steps), nullptr);
+    m->upd_flops.assign((size_t)(2 * steps), 0.0);
     for (auto &e : m->ev_upd) ck(ctx, hipEventCreateWithFlags(&e, ACE_TIMING_EVENT_FLAGS), "event");
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < 4; ++j) {
       ck(ctx, hipEventCreateWithFlags(&m->ev_asm[j], ACE_TIMING_EVENT_FLAGS), "event");
       ck(ctx, hipEventCreateWithFlags(&m->ev_grad[j], ACE_TIMING_EVENT_FLAGS), "event");
     }
@@ -656,7 +664,7 @@ void ace_model_destroy(ace_model *m) {
   if (m->shard) shard_destroy(m->shard);
   for (auto &e : m->ev_upd)
     if (e) (void)hipEventDestroy(e);
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < 4; ++j) {
     if (m->ev_asm[j]) (void)hipEventDestroy(m->ev_asm[j]);
     if (m->ev_grad[j]) (void)hipEventDestroy(m->ev_grad[j]);
   }
@@ -711,6 +719,12 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, d
     if (timed) shard_collect_timing(m->shard, m->t_ms, m->t_launch, m->t_work);
   } else {
     model_pipeline(m, m->sw, theta, iter == 1 ? 1 : 0, timed);
+    // the previous timed evaluation's events completed before its results
+    // were read: read them back while this evaluation runs
+    if (m->pend >= 0) {
+      model_collect_timing(m, m->pend);
+      m->pend = -1;
+    }
     // into the pinned region behind the tables, one synchronisation
     double *h = m->hio.p + (2 * s.B * s.PM + s.B);
     download(ctx, h, m->gsum.d(), gs.size(), "download gsum");
@@ -724,7 +738,10 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, d
     std::copy(h + gs.size(), h + gs.size() + 4, sums);
     std::copy(h + gs.size() + 4, h + gs.size() + 9, scal);
     flag = *hflag;
-    if (timed) model_collect_timing(m);
+    if (timed) {
+      m->pend = m->tset;
+      m->tset ^= 1;
+    }
   }
   if (iter == 1) theta[1] = scal[3];  // mean_solution before the gradient (R/kernel_SE_R6.R:45)
   compose_grad(s, theta, gs.data(), sums[2], grad);
@@ -791,6 +808,7 @@ int ace_model_get_inverse(ace_model *m, double *inv) {
 int ace_model_profile(ace_model *m, int enable) {
   if (!m) return ACE_ERR_ARG;
   m->prof = enable != 0;
+  m->pend = -1;  // counters restart: drop an unread set
   for (int j = 0; j < 3; ++j) {
     m->t_ms[j] = 0;
     m->t_launch[j] = 0;
@@ -801,6 +819,14 @@ int ace_model_profile(ace_model *m, int enable) {
 
 int ace_model_kernel_time(ace_model *m, int which, double *ms, int64_t *launches, double *work) {
   if (!m || which < 0 || which > 2) return ACE_ERR_ARG;
+  if (m->pend >= 0) {  // the last timed evaluation's set (its work is complete)
+    try {
+      model_collect_timing(m, m->pend);
+    } catch (const Fail &f) {
+      return f.code;
+    }
+    m->pend = -1;
+  }
   if (ms) *ms = m->t_ms[which];
   if (launches) *launches = m->t_launch[which];
   if (work) *work = m->t_work[which];

@@ -171,10 +171,10 @@ def make_step(kernel, p, B, theta, std_y, ctx, y, X, Z, model=None):
     return step, model
 
 
-def timed_steps(dist, step, steps, warmup, model):
+def timed_steps(dist, step, steps, warmup, model, profile=True):
     for _ in range(warmup):
         step()
-    model.profile(True)
+    model.profile(profile)
     _barrier_sync(dist)
     t0 = time.perf_counter()
     stats = None
@@ -231,6 +231,8 @@ def main():
     ap.add_argument("--shard-steps", type=int, default=2)
     ap.add_argument("--shard-timeout", type=float, default=240.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="diagnostic: no per-launch HIP events (no roofline / phase times)")
     a = ap.parse_args()
 
     dist, rank, world, local = _dist_init()
@@ -258,7 +260,7 @@ def main():
     n, p, B, kernel = CONFIGS[a.config]
     y, X, Z, theta, std_y = make_problem(n, p, B, seed=1000 + rank)
     step, model = make_step(kernel, p, B, theta, std_y, ctx, y, X, Z)
-    dt_max, stats = timed_steps(dist, step, a.steps, a.warmup, model)
+    dt_max, stats = timed_steps(dist, step, a.steps, a.warmup, model, not a.no_profile)
     upd_ms, upd_n, upd_work = model.kernel_time(0)
     asm_ms, _, asm_work = model.kernel_time(1)
     grad_ms, _, grad_work = model.kernel_time(2)
