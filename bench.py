@@ -84,12 +84,18 @@ def _allreduce_max(dist, x):
     return float(t.item())
 
 
+def _newest_first_last(files):
+    """Sort rNN_vMM_* profile files by (round, version) numerically."""
+    import re
+    return sorted(files, key=lambda f: [int(x) for x in re.findall(r"\d+", os.path.basename(f))])
+
+
 def pmc_traffic(kernel="k_update"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/rNN_pmc_traffic.json, written by tools/pmc_traffic.py from two
     separate rocprofv3 --pmc passes of this bench).  None if absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    files = _newest_first_last(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
     if not files:
         return None, None
     try:
@@ -107,14 +113,14 @@ def pair_hbm_gbs(asm_ms, grad_ms):
     profiles/rNN_pmc_traffic.json (one assembly launch and the gradient
     launches of each eval) over this run's phase times."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    files = _newest_first_last(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
     if not files:
         return None
     try:
         ks = json.load(open(files[-1]))["kernels"]
         a, g = ks["k_asm_mm"], ks["k_grad_mm"]
-        evals = a["launches"]
-        asm_b = a["traffic"]
+        evals = ks["k_update"]["launches"] / (N1 // 256)  # 64 sweep steps per C2 eval
+        asm_b = a["traffic"] * a["launches"] / evals  # the assembly is 2 launches per eval
         grad_b = g["traffic"] * g["launches"] / evals
     except (KeyError, ValueError, OSError, ZeroDivisionError):
         return None
