@@ -407,3 +407,39 @@ def test_sweep_large_residual_and_logdet(A):
     assert np.abs(R).max() < 1e-8
     s, ld = np.linalg.slogdet(Am)
     assert s > 0 and np.sum(np.log(r["eigenval"])) == pytest.approx(ld, rel=1e-10)
+
+
+_ORDER_SNIPPET = """
+import sys, numpy as np
+sys.path.insert(0, {root!r})
+import additivecausalexpansion_amd as A
+d = np.load({inp!r})
+r = A.invkernel_cpp(d["K"], float(d["s"]))
+np.save({out!r}, r["inv"])
+"""
+
+
+def test_update_tile_order_is_bitwise_neutral(A, tmp_path):
+    """The XCD super-block tile order of k_update (ACE_UPD_ORDER=S, default
+    4) only changes which workgroup runs a tile, never its arithmetic: the
+    inverse is bit-identical to the row-major grid (S = 0) and to S = 2."""
+    import os
+    import subprocess
+    import sys
+    from additivecausalexpansion_amd.synthetic import make_problem
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = 1500  # 6 sweep steps, 13 x 13 tiles: padding entries in every order
+    y, X, Z, th, _ = make_problem(n, 4, 5, seed=7)
+    K = A.kernmat_SE_symmetric_cpp(X, Z, th)["full"]
+    inp = str(tmp_path / "k.npz")
+    np.savez(inp, K=K, s=th[0])
+    outs = {}
+    for S in ("0", "2", "4"):
+        out = str(tmp_path / f"inv{S}.npy")
+        env = dict(os.environ, ACE_UPD_ORDER=S)
+        subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
+                       env=env, check=True, timeout=100)
+        outs[S] = np.load(out)
+    assert np.array_equal(outs["0"], outs["4"]) and np.array_equal(outs["2"], outs["4"])
+    mine = A.invkernel_cpp(K, th[0])["inv"]  # this process: default order
+    assert np.array_equal(mine, outs["4"])
