@@ -377,6 +377,9 @@ __device__ __forceinline__ void st_a(double *p, double v) {
   *p = v;
 #endif
 }
+#ifndef ACE_UPD_STAGE_FIRST
+#define ACE_UPD_STAGE_FIRST 1  // staging loads of chunk 0 issued before the C tile
+#endif
 #ifndef ACE_UPD_X
 #define ACE_UPD_X 0  // 1: k_update_x uses the same load/store policy
 #endif
@@ -480,6 +483,31 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
     for (int j = 0; j < 4; ++j) st_a(&A[r + (c + 4 * j) * ld], acc[j]);
     return;
   }
+#if ACE_UPD_STAGE_FIRST
+  // staging: each thread moves 4 doubles of each operand per chunk (issued
+  // before the C tile, so chunk 0 reaches LDS without waiting for C)
+  const int sk = tid >> 5, sm = (tid & 31) * 4;
+  const double *gW = Rop + (R0 + sm) + (int64_t)sk * ldp;
+  const double *gP = Cop + (C0 + sm) + (int64_t)sk * ldp;
+  double2 rw[2], rp[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    rw[e] = *reinterpret_cast<const double2 *>(gW + 2 * e);
+    rp[e] = *reinterpret_cast<const double2 *>(gP + 2 * e);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the C-tile loads behind them
+  const int wr = wv & 1, wc = wv >> 1;  // rows 64*wr.., cols 32*wc..
+  d4 acc[2][4];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 4; ++ri) {
+      const int64_t r = R0 + 64 * wr + 16 * ri + lr;
+      const int64_t c = L0 + 32 * wc + 16 * ci + lk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[ci][ri][j] = ld_a(&A[r + (c + 4 * j) * ld]);
+    }
+#else
   const int wr = wv & 1, wc = wv >> 1;  // rows 64*wr.., cols 32*wc..
   d4 acc[2][4];
 #pragma unroll
@@ -501,6 +529,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
     rw[e] = *reinterpret_cast<const double2 *>(gW + 2 * e);
     rp[e] = *reinterpret_cast<const double2 *>(gP + 2 * e);
   }
+#endif
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2 * e]) = rw[e];
