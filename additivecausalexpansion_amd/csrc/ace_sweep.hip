@@ -38,7 +38,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 #define ACE_PIVOT_RCP 1
 #endif
 #ifndef ACE_CHAIN_PRIO
-#define ACE_CHAIN_PRIO 3
+#define ACE_CHAIN_PRIO 1
 #endif
 #define CHAIN_PRIO() \
   do {               \
