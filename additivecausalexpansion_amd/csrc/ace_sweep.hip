@@ -361,38 +361,12 @@ constexpr int NCH = NB / BK;
 constexpr int UTHREADS = 512;
 static_assert(BK == 16, "staging maps 512 threads x 4 doubles onto a 128 x 16 chunk");
 
-// Write-back of an updated A element.  ACE_UPD_STORE 1: write-through store
-// that drops the line from the XCD's L2 (A tiles are read once per step, on
-// any XCD; keeping them out of L2 leaves it to the re-read panels); 2:
-// nontemporal; 0: plain.
-#ifndef ACE_UPD_STORE
-#define ACE_UPD_STORE 2
-#endif
-__device__ __forceinline__ void st_a(double *p, double v) {
-#if ACE_UPD_STORE == 1
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#elif ACE_UPD_STORE == 2
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
-}
-#ifndef ACE_UPD_STAGE_FIRST
-#define ACE_UPD_STAGE_FIRST 1  // staging loads of chunk 0 issued before the C tile
-#endif
-#ifndef ACE_UPD_X
-#define ACE_UPD_X 0  // 1: k_update_x uses the same load/store policy
-#endif
-#ifndef ACE_UPD_LOAD
-#define ACE_UPD_LOAD 1
-#endif
-__device__ __forceinline__ double ld_a(const double *p) {
-#if ACE_UPD_LOAD == 1
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
-}
+// A tiles are read and written once per sweep step, by whichever XCD runs
+// the tile: nontemporal loads and stores leave the XCD L2s to the re-read
+// panels (profiles/r01_pairs_ab.txt: plain 85.3, write-through stores 85.0,
+// nontemporal stores 84.5, nontemporal loads + stores 84.3 ms/eval).
+__device__ __forceinline__ void st_a(double *p, double v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ double ld_a(const double *p) { return __builtin_nontemporal_load(p); }
 
 // Every lower tile except the "cross" of block kx (tiles with I or J in
 // block kx, updated earlier by k_update_x for the lookahead; kx < 0: none).
@@ -483,7 +457,6 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
     for (int j = 0; j < 4; ++j) st_a(&A[r + (c + 4 * j) * ld], acc[j]);
     return;
   }
-#if ACE_UPD_STAGE_FIRST
   // staging: each thread moves 4 doubles of each operand per chunk (issued
   // before the C tile, so chunk 0 reaches LDS without waiting for C)
   const int sk = tid >> 5, sm = (tid & 31) * 4;
@@ -507,29 +480,6 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[ci][ri][j] = ld_a(&A[r + (c + 4 * j) * ld]);
     }
-#else
-  const int wr = wv & 1, wc = wv >> 1;  // rows 64*wr.., cols 32*wc..
-  d4 acc[2][4];
-#pragma unroll
-  for (int ci = 0; ci < 2; ++ci)
-#pragma unroll
-    for (int ri = 0; ri < 4; ++ri) {
-      const int64_t r = R0 + 64 * wr + 16 * ri + lr;
-      const int64_t c = L0 + 32 * wc + 16 * ci + lk;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[ci][ri][j] = ld_a(&A[r + (c + 4 * j) * ld]);
-    }
-  // staging: each thread moves 4 doubles of each operand per chunk
-  const int sk = tid >> 5, sm = (tid & 31) * 4;
-  const double *gW = Rop + (R0 + sm) + (int64_t)sk * ldp;
-  const double *gP = Cop + (C0 + sm) + (int64_t)sk * ldp;
-  double2 rw[2], rp[2];
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    rw[e] = *reinterpret_cast<const double2 *>(gW + 2 * e);
-    rp[e] = *reinterpret_cast<const double2 *>(gP + 2 * e);
-  }
-#endif
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2 * e]) = rw[e];
@@ -643,7 +593,7 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
       const int64_t r = R0 + 32 * wr + 16 * ri + lr;
       const int64_t c = L0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[ci][ri][j] = ACE_UPD_X ? ld_a(&A[r + (c + 4 * j) * ld]) : A[r + (c + 4 * j) * ld];
+      for (int j = 0; j < 4; ++j) acc[ci][ri][j] = A[r + (c + 4 * j) * ld];
     }
   // staging: 256 threads x (4 doubles of each operand) per 64 x 16 chunk
   const int sk = tid >> 4, sm = (tid & 15) * 4;
@@ -700,10 +650,7 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
       const int64_t r = R0 + 32 * wr + 16 * ri + lr;
       const int64_t c = L0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (ACE_UPD_X) st_a(&A[r + (c + 4 * j) * ld], acc[ci][ri][j]);
-        else A[r + (c + 4 * j) * ld] = acc[ci][ri][j];
-      }
+      for (int j = 0; j < 4; ++j) A[r + (c + 4 * j) * ld] = acc[ci][ri][j];
     }
 }
 
