@@ -24,6 +24,21 @@ __device__ __forceinline__ double block_sum256(double v, double *sh) {
   return r;
 }
 
+// Block-wide sum for 1024 threads (deterministic order): the latency-bound
+// per-evaluation reductions (colsum of the tile partials, final sums with
+// n logs) run 4x shorter loops per thread than at 256.
+__device__ __forceinline__ double block_sum1024(double v, double *sh) {
+  v = wsum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) sh[wv] = v;
+  __syncthreads();
+  double r = 0.0;
+#pragma unroll
+  for (int q = 0; q < 16; q += 4) r += (sh[q] + sh[q + 1]) + (sh[q + 2] + sh[q + 3]);
+  __syncthreads();
+  return r;
+}
+
 // ---------------------------------------------------------------- AUG rows
 // rows npad .. npad+AUG-1 of A: row 0 = y (j < n), row 1 = 1 (j < n), 0 else
 __global__ void k_aug_init(double *__restrict__ A, int64_t ld, int64_t npad, int64_t n,
@@ -145,20 +160,20 @@ hipError_t launch_alpha_from_aug(const double *A, int64_t ld, int64_t npad, int6
 }
 
 // ---------------------------------------------------------------- reductions
-__global__ __launch_bounds__(256) void k_colsum(const double *__restrict__ in, int64_t nrows,
-                                                double *__restrict__ out) {
-  __shared__ double sh[4];
+__global__ __launch_bounds__(1024) void k_colsum(const double *__restrict__ in, int64_t nrows,
+                                                 double *__restrict__ out) {
+  __shared__ double sh[16];
   const int j = blockIdx.x;
   const double *p = in + (int64_t)j * nrows;
   double s = 0.0;
-  for (int64_t t = threadIdx.x; t < nrows; t += 256) s += p[t];
-  s = block_sum256(s, sh);
+  for (int64_t t = threadIdx.x; t < nrows; t += 1024) s += p[t];
+  s = block_sum1024(s, sh);
   if (threadIdx.x == 0) out[j] = s;
 }
 
 hipError_t launch_colsum(const double *in, int64_t nrows, int ncols, double *out,
                          hipStream_t st) {
-  hipLaunchKernelGGL(k_colsum, dim3(ncols), dim3(256), 0, st, in, nrows, out);
+  hipLaunchKernelGGL(k_colsum, dim3(ncols), dim3(1024), 0, st, in, nrows, out);
   return hipGetLastError();
 }
 
@@ -166,27 +181,27 @@ hipError_t launch_colsum(const double *in, int64_t nrows, int ncols, double *out
 // identity ybar - Kfull alpha = sig alpha is used -- A = Kfull + sig I is the
 // matrix the sweep inverted and alpha = A^-1 ybar, so the residual of
 // src/stats_cpp.cpp:25 needs no pass over Kfull.
-__global__ __launch_bounds__(256) void k_final_sums(const double *__restrict__ y,
+__global__ __launch_bounds__(1024) void k_final_sums(const double *__restrict__ y,
                                                     const double *__restrict__ mup,
                                                     const double *__restrict__ alpha,
                                                     const double *__restrict__ s, double sig,
                                                     int64_t n, const double *__restrict__ piv,
                                                     int64_t npiv, double *__restrict__ sums) {
-  __shared__ double sh[4];
+  __shared__ double sh[16];
   const double mu = *mup;
   double e2 = 0.0, ya = 0.0, sa = 0.0, ld = 0.0;
-  for (int64_t x = threadIdx.x; x < n; x += 256) {
+  for (int64_t x = threadIdx.x; x < n; x += 1024) {
     const double ybar = y[x] - mu;
     const double e = s ? ybar - s[x] : sig * alpha[x];
     e2 += e * e;
     ya += y[x] * alpha[x];
     sa += alpha[x];
   }
-  for (int64_t x = threadIdx.x; x < npiv; x += 256) ld += log(piv[x]);
-  e2 = block_sum256(e2, sh);
-  ya = block_sum256(ya, sh);
-  sa = block_sum256(sa, sh);
-  ld = block_sum256(ld, sh);
+  for (int64_t x = threadIdx.x; x < npiv; x += 1024) ld += log(piv[x]);
+  e2 = block_sum1024(e2, sh);
+  ya = block_sum1024(ya, sh);
+  sa = block_sum1024(sa, sh);
+  ld = block_sum1024(ld, sh);
   if (threadIdx.x == 0) {
     sums[0] = e2;
     sums[1] = ya;
@@ -198,7 +213,7 @@ __global__ __launch_bounds__(256) void k_final_sums(const double *__restrict__ y
 hipError_t launch_final_sums(const double *y, const double *mu, const double *alpha, const double *s,
                              double sig, int64_t n, const double *piv, int64_t npiv,
                              double *sums, hipStream_t st) {
-  hipLaunchKernelGGL(k_final_sums, dim3(1), dim3(256), 0, st, y, mu, alpha, s, sig, n, piv, npiv,
+  hipLaunchKernelGGL(k_final_sums, dim3(1), dim3(1024), 0, st, y, mu, alpha, s, sig, n, piv, npiv,
                      sums);
   return hipGetLastError();
 }
