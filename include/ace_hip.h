@@ -199,7 +199,11 @@ int ace_model_get_inverse(ace_model *m, double *inv);
  * events bracket every launch of the dense update kernel (`which` = 0),
  * the assembly kernel (1) and the gradient kernel (2) on the model's
  * stream.  *ms = summed duration, *launches = count, *work = algorithmic
- * flops issued by those launches. */
+ * flops issued by those launches.  Enabling resets the
+ * counters.  An evaluation's events are read back while the next one runs
+ * (no host queries between evaluations); ace_model_kernel_time reads the
+ * last timed evaluation's set first, so its totals cover every timed
+ * evaluation. */
 int ace_model_profile(ace_model *m, int enable);
 int ace_model_kernel_time(ace_model *m, int which, double *ms,
                           int64_t *launches, double *work);
