@@ -63,6 +63,12 @@ SIGNATURES = {
     "ace_model_para_update": (ctypes.c_int, [_vp, ctypes.c_int, _D, _D, _D, _D]),
     "ace_model_train_stats": (ctypes.c_int, [_vp, _D, _D]),
     "ace_model_get_inverse": (ctypes.c_int, [_vp, _D]),
+    "ace_model_apply_inverse": (ctypes.c_int, [_vp, _I64, _D, _D]),
+    "ace_model_predict": (ctypes.c_int, [_vp, _D, _I64, _D, _D, ctypes.c_double, ctypes.c_double,
+                                         _D, _D, _D]),
+    "ace_model_predict_marginal": (ctypes.c_int, [_vp, _D, _I64, _D, _D, _D, ctypes.c_double,
+                                                  ctypes.c_double, ctypes.c_int, _D, _D, _D,
+                                                  _D]),
     "ace_model_profile": (ctypes.c_int, [_vp, ctypes.c_int]),
     "ace_model_kernel_time": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(_I64),

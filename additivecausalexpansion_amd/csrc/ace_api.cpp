@@ -15,6 +15,7 @@
 
 #include "ace_common.h"
 #include "ace_internal.h"
+#include "ace_model.h"
 
 using namespace ace;
 
@@ -93,7 +94,7 @@ int ace_kernmat_sym(ace_ctx *ctx, int kind, int64_t n, int p, int B, const doubl
   arg(ctx, n >= 1 && theta && Kfull && (p == 0 || X) && (B == 1 || Z), "null argument");
   SideBufs sb;
   upload_side(ctx, sb, s, X, Z, n, n);
-  std::vector<double> tab = make_tab(theta, s);
+  std::vector<double> tab = make_tab(theta, s, false);
   DBuf dtab, dK, dC;
   upload(ctx, dtab, tab.data(), tab.size(), "upload tables");
   alloc(ctx, dK, (size_t)(n * n) * sizeof(double), "alloc Kfull");
@@ -120,7 +121,7 @@ int ace_kernmat_cross(ace_ctx *ctx, int kind, int64_t n1, int64_t n2, int p, int
   SideBufs s1, s2;
   upload_side(ctx, s1, s, X1, Z1, n1, n1);
   upload_side(ctx, s2, s, X2, Z2, n2, n2);
-  std::vector<double> tab = make_tab(theta, s);
+  std::vector<double> tab = make_tab(theta, s, false);
   DBuf dtab, dK, dC;
   upload(ctx, dtab, tab.data(), tab.size(), "upload tables");
   alloc(ctx, dK, (size_t)(n1 * n2) * sizeof(double), "alloc Kfull");
@@ -137,69 +138,6 @@ int ace_kernmat_cross(ace_ctx *ctx, int kind, int64_t n1, int64_t n2, int p, int
 }
 
 // ------------------------------------------------------------ inverse
-namespace {
-struct SweepWork {
-  DBuf A, P0, P1, W0, W1, SW, S0, S1, piv, flag, order;
-  std::vector<hipEvent_t> ev;
-  int64_t n = 0, npad = 0, naug = 0, norder = 0;
-  SweepWork() = default;
-  SweepWork(const SweepWork &) = delete;
-  ~SweepWork() {
-    for (auto &e : ev) (void)hipEventDestroy(e);
-  }
-  void ensure(ace_ctx *ctx, int64_t n_) {
-    n = n_;
-    npad = round_up(n, NB);
-    naug = npad + AUG;
-    alloc(ctx, A, (size_t)(naug * naug) * sizeof(double), "alloc A");
-    for (DBuf *b : {&P0, &P1, &W0, &W1}) alloc(ctx, *b, (size_t)(naug * NB) * sizeof(double), "alloc panel");
-    alloc(ctx, SW, (size_t)(SUB * SUB) * sizeof(double), "alloc SW");
-    alloc(ctx, S0, (size_t)(SUB * NB) * sizeof(double), "alloc S");
-    alloc(ctx, S1, (size_t)(SUB * NB) * sizeof(double), "alloc S");
-    alloc(ctx, piv, (size_t)npad * sizeof(double), "alloc piv");
-    alloc(ctx, flag, 16, "alloc flag");
-    norder = 0;
-    if (const int S = update_order_block(); S > 0) {
-      const std::vector<Tile> t = xcd_update_order(own_tiles(naug / UT, UT, 1, 0), S);
-      alloc(ctx, order, t.size() * sizeof(Tile), "alloc tile order");
-      ck(ctx, hipMemcpy(order.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
-         "upload tile order");
-      norder = (int64_t)t.size();
-    }
-    const size_t need = (size_t)(2 * (npad / NB) + 1);
-    while (ev.size() < need) {
-      hipEvent_t e;
-      ck(ctx, hipEventCreateWithFlags(&e, ACE_SYNC_EVENT_FLAGS), "event");
-      ev.push_back(e);
-    }
-  }
-  SweepBufs bufs() const {
-    SweepBufs b;
-    b.A = A.d();
-    b.ld = naug;
-    b.npad = npad;
-    b.P[0] = P0.d();
-    b.P[1] = P1.d();
-    b.W[0] = W0.d();
-    b.W[1] = W1.d();
-    b.SW = SW.d();
-    b.S[0] = S0.d();
-    b.S[1] = S1.d();
-    b.piv = piv.d();
-    b.flag = flag.i();
-    b.order = norder ? reinterpret_cast<const Tile *>(order.p) : nullptr;
-    b.norder = norder;
-    return b;
-  }
-  SweepSync sync(ace_ctx *ctx) {
-    SweepSync s;
-    s.side = ctx->side;
-    s.ev = ev.data();
-    s.nev = (int)ev.size();
-    return s;
-  }
-};
-}  // namespace
 
 int ace_invkernel(ace_ctx *ctx, int64_t n, const double *K, double sigma, double *eigenval,
                   double *inv) {
@@ -249,7 +187,7 @@ int ace_grad(ace_ctx *ctx, int kind, int64_t n, int p, int B, const double *y, c
   std::vector<double> tab = make_tab(theta, s);
   std::vector<double> ybar((size_t)n);
   for (int64_t r = 0; r < n; ++r) ybar[(size_t)r] = y[r] - theta[1];
-  DBuf dtab, dy, dyb, dinv, dKf, dC, dalpha, ds, dg, dtr, dgs, dsums, dmu;
+  DBuf dtab, dy, dyb, dinv, dKf, dC, dalpha, ds, dg, dwork, dgs, dsums, dmu;
   upload(ctx, dtab, tab.data(), tab.size(), "upload tables");
   upload(ctx, dy, y, (size_t)n, "upload y");
   upload(ctx, dyb, ybar.data(), (size_t)n, "upload ybar");
@@ -261,17 +199,17 @@ int ace_grad(ace_ctx *ctx, int kind, int64_t n, int p, int B, const double *y, c
   alloc(ctx, ds, (size_t)n * sizeof(double), "alloc s");
   const int64_t nt = grad_ntiles(n);
   const int ncol = B * (s.PM + 1);
-  alloc(ctx, dg, (size_t)(nt * ncol) * sizeof(double), "alloc gpart");
-  alloc(ctx, dtr, (size_t)nt * sizeof(double), "alloc trpart");
-  alloc(ctx, dgs, (size_t)(ncol + 1) * sizeof(double), "alloc gsum");
+  const int ldg = grad_part_cols(s.PM, B);  // ncol + trace
+  alloc(ctx, dg, (size_t)(nt * ldg) * sizeof(double), "alloc gpart");
+  alloc(ctx, dwork, (size_t)tile_sums_work(ldg) * sizeof(double), "alloc tile sums");
+  alloc(ctx, dgs, (size_t)ldg * sizeof(double), "alloc gsum");
   alloc(ctx, dsums, 8 * sizeof(double), "alloc sums");
   // alpha = invKmatn * ybar (src/kernel_SE_cpp.cpp:215)
   ck(ctx, launch_gemv(dinv.d(), n, n, n, dyb.d(), dalpha.d(), ctx->stream), "gemv alpha");
   ck(ctx, launch_grad(kind, s.PM, sb.view(n), B, s.ZS, tab_view(dtab, s), dinv.d(), n, 1.0,
-                      dalpha.d(), Kel ? dC.d() : nullptr, dg.d(), dtr.d(), ctx->stream),
+                      dalpha.d(), Kel ? dC.d() : nullptr, dg.d(), ctx->stream),
      "grad");
-  ck(ctx, launch_colsum(dg.d(), nt, ncol, dgs.d(), ctx->stream), "colsum");
-  ck(ctx, launch_colsum(dtr.d(), nt, 1, dgs.d() + ncol, ctx->stream), "colsum tr");
+  ck(ctx, launch_tile_sums(dg.d(), nt, ldg, dwork.d(), dgs.d(), ctx->stream), "tile sums");
   // Kfull * alpha for the RMSE (src/kernel_SE_cpp.cpp:238)
   ck(ctx, launch_gemv(dKf.d(), n, n, n, dalpha.d(), ds.d(), ctx->stream), "gemv K alpha");
   ck(ctx, launch_final_sums(dy.d(), dmu.d(), dalpha.d(), ds.d(), 0.0, n, nullptr, 0, dsums.d(),
@@ -372,16 +310,9 @@ int ace_pred(ace_ctx *ctx, int64_t nX, int64_t nx, const double *y_X, double sig
   download(ctx, a.data(), da.d(), (size_t)nx, "download");
   download(ctx, q.data(), dq.d(), (size_t)nx, "download");
   sync(ctx);
-  const double es = std::exp(sigma);
-  for (int64_t r = 0; r < nx; ++r) {
-    const double yx = mean_y + std_y * (a[(size_t)r] + mu);
-    const double d = (K_xx[r + r * nx] - q[(size_t)r]) + es;
-    const double sd = std_y * std::sqrt(std::fabs(d));
-    map[r] = yx;
-    ci[r] = yx - 1.96 * sd;
-    ci[r + nx] = yx + 1.96 * sd;
-    var[r] = std::pow(sd, 2);
-  }
+  std::vector<double> kd((size_t)nx);
+  for (int64_t r = 0; r < nx; ++r) kd[(size_t)r] = K_xx[r + r * nx];
+  finish_pred(nx, a.data(), kd.data(), q.data(), sigma, mu, mean_y, std_y, map, ci, var);
   return ACE_OK;
   ACE_CATCH
 }
@@ -451,80 +382,23 @@ int ace_pred_marginal(ace_ctx *ctx, int64_t nX, int64_t nx, int B, const double 
     download(ctx, kw.data(), dkw.d(), kw.size(), "download");
   }
   sync(ctx);
-  std::vector<double> yx((size_t)nx);
-  for (int64_t r = 0; r < nx; ++r) {
-    yx[(size_t)r] = std_y * a[(size_t)r] / std_Z;
-    const double d = dg[(size_t)r] - q[(size_t)r];
-    const double sd = std_y * std::sqrt(std::fabs(d)) / std_Z;
-    map[r] = yx[(size_t)r];
-    ci[r] = yx[(size_t)r] - 1.96 * sd;
-    ci[r + nx] = yx[(size_t)r] + 1.96 * sd;
-    var[r] = std::pow(sd, 2);
-  }
+  std::vector<double> post;
   if (calculate_ate) {
     // posterior quadratic forms w^T (Km_xx - tmp Km_xX^T) w (src/pred_cpp.cpp:89-106)
-    double post[3];
+    post.assign(3, 0.0);
     for (int j = 0; j < 3; ++j) {
       double cross = 0.0;
       for (int64_t c = 0; c < nX; ++c) cross += tw[(size_t)(j * nX + c)] * kw[(size_t)(j * nX + c)];
-      post[j] = q3[(size_t)j] - cross;
-    }
-    double sy = 0.0, syz = 0.0, sz = 0.0;
-    for (int64_t r = 0; r < nx; ++r) {
-      sy += yx[(size_t)r];
-      syz += yx[(size_t)r] * zx[(size_t)r];
-      sz += zx[(size_t)r];
-    }
-    const double ate = sy / (double)nx;
-    double ate_sd = std_y * std::sqrt(post[0]) / (double)nx;
-    const unsigned int ntx = (unsigned int)sz;  // unsigned int in the reference
-    const double att = syz / ntx;
-    double att_sd = std_y * std::sqrt(post[1]) / ntx;
-    const unsigned int nux = (unsigned int)nx - ntx;
-    const double atu = (ate * nx - att * ntx) / nux;
-    double atu_sd = std_y * std::sqrt(post[2]) / nux;
-    const double m3[3] = {ate, att, atu}, s3[3] = {ate_sd, att_sd, atu_sd};
-    for (int j = 0; j < 3; ++j) {
-      avg[4 * j + 0] = m3[j];
-      avg[4 * j + 1] = m3[j] - 1.96 * s3[j];
-      avg[4 * j + 2] = m3[j] + 1.96 * s3[j];
-      avg[4 * j + 3] = std::pow(s3[j], 2);
+      post[(size_t)j] = q3[(size_t)j] - cross;
     }
   }
+  finish_marginal(nx, a.data(), dg.data(), q.data(), std_y, std_Z, calculate_ate ? zx.data() : nullptr,
+                  calculate_ate ? post.data() : nullptr, map, ci, var, avg);
   return ACE_OK;
   ACE_CATCH
 }
 
 }  // extern "C"
-
-// =====================================================================
-// Device-resident model: one para_update per call, nothing materialised
-// beyond A (the swept matrix) and O(n * tiles) partial sums.
-// =====================================================================
-struct ace_model {
-  ace_ctx *ctx = nullptr;
-  Shape s{};
-  int64_t n = 0, npad = 0, naug = 0, ntiles = 0, ntr = 0;
-  double std_y = 1.0;
-  bool has_data = false;
-  SideBufs side;
-  DBuf y, tab, alpha, scal, gpart, trpart, gsum, sums;
-  PinnedBuf hio;  // [theta tables | gsum | sums | scal | flag] host staging
-  SweepWork sw;   // A = resident inverse of the last para_update
-  SweepWork sw2;  // train_stats scratch (keeps sw's inverse, Q6)
-  bool prof = false;
-  // timing events in two sets: the set of evaluation t is read back while
-  // evaluation t+1 runs (no host queries between evaluations)
-  hipEvent_t ev_asm[4] = {}, ev_grad[4] = {};
-  std::vector<hipEvent_t> ev_upd;  // 2 sets x 2 * steps
-  std::vector<double> upd_flops;   // 2 sets x steps
-  int upd_used[2] = {0, 0};
-  int tset = 0, pend = -1;  // set the next timed evaluation records; set not yet read
-  double t_ms[3] = {0, 0, 0};
-  int64_t t_launch[3] = {0, 0, 0};
-  double t_work[3] = {0, 0, 0};
-  ShardModel *shard = nullptr;  // block-column-sharded model (ace_shard.cpp)
-};
 
 namespace {
 
@@ -575,12 +449,12 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   // the sweep inverted): no Kfull copy and no pass over it (k_final_sums)
   if (timed) ck(ctx, hipEventRecord(m->ev_grad[2 * ts], st), "event");
   ck(ctx, launch_grad(s.kind, s.PM, ps, s.B, s.ZS, tv, w.A.d(), w.naug, -1.0, m->alpha.d(),
-                      nullptr, m->gpart.d(), m->trpart.d(), st),
+                      nullptr, m->gpart.d(), st),
      "grad");
   if (timed) ck(ctx, hipEventRecord(m->ev_grad[2 * ts + 1], st), "event");
-  const int ncol = s.B * (s.PM + 1);
-  ck(ctx, launch_colsum(m->gpart.d(), m->ntiles, ncol, m->gsum.d(), st), "colsum");
-  ck(ctx, launch_colsum(m->trpart.d(), m->ntiles, 1, m->gsum.d() + ncol, st), "colsum");
+  const int ldg = grad_part_cols(s.PM, s.B);
+  ck(ctx, launch_tile_sums(m->gpart.d(), m->ntiles, ldg, m->gwork.d(), m->gsum.d(), st),
+     "tile sums");
   ck(ctx, launch_final_sums(m->y.d(), m->scal.d() + 4, m->alpha.d(), nullptr, sig, m->n,
                             w.piv.d(), w.npad, m->sums.d(), st),
      "final sums");
@@ -636,9 +510,10 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
     alloc(ctx, m->tab, (size_t)(2 * s.B * s.PM + s.B) * sizeof(double), "alloc tab");
     alloc(ctx, m->alpha, (size_t)m->npad * sizeof(double), "alloc alpha");
     alloc(ctx, m->scal, 16 * sizeof(double), "alloc scal");
-    alloc(ctx, m->gpart, (size_t)(m->ntiles * s.B * (s.PM + 1)) * sizeof(double), "alloc gpart");
-    alloc(ctx, m->trpart, (size_t)m->ntiles * sizeof(double), "alloc trpart");
-    alloc(ctx, m->gsum, (size_t)(s.B * (s.PM + 1) + 1) * sizeof(double), "alloc gsum");
+    const int ldg = grad_part_cols(s.PM, s.B);
+    alloc(ctx, m->gpart, (size_t)(m->ntiles * ldg) * sizeof(double), "alloc gpart");
+    alloc(ctx, m->gwork, (size_t)tile_sums_work(ldg) * sizeof(double), "alloc tile sums");
+    alloc(ctx, m->gsum, (size_t)ldg * sizeof(double), "alloc gsum");
     alloc(ctx, m->sums, 8 * sizeof(double), "alloc sums");
     ck(ctx, hipMemsetAsync(m->sw.A.p, 0, m->sw.A.bytes, ctx->stream), "memset A");
     const int steps = (int)(m->npad / NB);
@@ -700,11 +575,15 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, d
                           double *mu_post) {
   if (!m) return ACE_ERR_ARG;
   ace_ctx *ctx = m->ctx;
-  if (ctx->poll && ctx->poll(ctx->poll_user)) {
+  ACE_TRY
+  int stop = (ctx->poll && ctx->poll(ctx->poll_user)) ? 1 : 0;
+  // sharded over RCCL: every rank votes (also ranks without a poll), so that
+  // all of them stop before the same evaluation
+  if (m->shard) stop = shard_any(m->shard, stop);
+  if (stop) {
     ctx->err = "interrupted";
     return ACE_ERR_INTERRUPTED;
   }
-  ACE_TRY
   ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
   arg(ctx, m->has_data, "ace_model_set_data() not called");
   arg(ctx, theta && grad && stats, "null argument");
@@ -743,6 +622,7 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, d
       m->tset ^= 1;
     }
   }
+  m->has_inverse = true;
   if (iter == 1) theta[1] = scal[3];  // mean_solution before the gradient (R/kernel_SE_R6.R:45)
   compose_grad(s, theta, gs.data(), sums[2], grad);
   stats[0] = m->std_y * std::sqrt(sums[0]) / std::sqrt((double)m->n);

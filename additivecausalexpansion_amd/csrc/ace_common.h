@@ -152,14 +152,18 @@ inline std::vector<double> pack_rows(const double *M, int64_t n, int cols, int w
   return out;
 }
 
-// theta tables (b-major), see TabView in ace_internal.h
-inline std::vector<double> make_tab(const double *theta, const Shape &s) {
+// theta tables (b-major), see TabView in ace_internal.h.  The kernel reads
+// theta up to index 1 + B (p + 1) - 1 = P - 2 only, so the kernel-matrix
+// entry points (with_grad = false) accept a theta one entry short, as the
+// reference's kernmat_* do; the gradient-indexed weights need all P.
+inline std::vector<double> make_tab(const double *theta, const Shape &s, bool with_grad = true) {
   const int B = s.B, PM = s.PM;
   std::vector<double> t((size_t)(2 * B * PM + B), 0.0);
   for (int b = 0; b < B; ++b) {
     for (int i = 0; i < s.p; ++i) {
-      t[(size_t)(b * PM + i)] = std::exp(-theta[1 + b + B * (i + 1)]);        // Q1 kernel index
-      t[(size_t)(B * PM + b * PM + i)] = std::exp(-theta[2 + B + b + B * i]);  // gradient index
+      t[(size_t)(b * PM + i)] = std::exp(-theta[1 + b + B * (i + 1)]);  // Q1 kernel index
+      if (with_grad)
+        t[(size_t)(B * PM + b * PM + i)] = std::exp(-theta[2 + B + b + B * i]);  // gradient index
     }
     t[(size_t)(2 * B * PM + b)] = theta[2 + b];
   }
@@ -228,6 +232,64 @@ inline void compose_grad(const Shape &s, const double *theta, const double *gsum
   grad[1] = (s.kind == ACE_KERNEL_SE) ? sum_alpha : 0.0;
 }
 
+// Host tail of pred_cpp (src/pred_cpp.cpp:20-33): from a = tmp (y - mu),
+// kd = diag(K_xx), qd = diag(tmp K_xX^T).
+inline void finish_pred(int64_t nx, const double *a, const double *kd, const double *qd,
+                        double sigma, double mu, double mean_y, double std_y, double *map,
+                        double *ci, double *var) {
+  const double es = std::exp(sigma);
+  for (int64_t r = 0; r < nx; ++r) {
+    const double yx = mean_y + std_y * (a[r] + mu);
+    const double d = (kd[r] - qd[r]) + es;
+    const double sd = std_y * std::sqrt(std::fabs(d));
+    map[r] = yx;
+    ci[r] = yx - 1.96 * sd;
+    ci[r + nx] = yx + 1.96 * sd;
+    var[r] = std::pow(sd, 2);
+  }
+}
+
+// Host tail of pred_marginal_cpp (src/pred_cpp.cpp:69-126): a, kd, qd of the
+// marginal kernels; with zx != NULL also ATE / ATT / ATU from the posterior
+// quadratic forms post[j] = w_j^T (Km_xx - tmp Km_xX^T) w_j for w = 1, Z_x,
+// (Z_x == 0).  avg (12) as ace_pred_marginal.
+inline void finish_marginal(int64_t nx, const double *a, const double *kd, const double *qd,
+                            double std_y, double std_Z, const double *zx, const double *post,
+                            double *map, double *ci, double *var, double *avg) {
+  std::vector<double> yx((size_t)nx);
+  for (int64_t r = 0; r < nx; ++r) {
+    yx[(size_t)r] = std_y * a[r] / std_Z;
+    const double d = kd[r] - qd[r];
+    const double sd = std_y * std::sqrt(std::fabs(d)) / std_Z;
+    map[r] = yx[(size_t)r];
+    ci[r] = yx[(size_t)r] - 1.96 * sd;
+    ci[r + nx] = yx[(size_t)r] + 1.96 * sd;
+    var[r] = std::pow(sd, 2);
+  }
+  if (!zx || !post) return;
+  double sy = 0.0, syz = 0.0, sz = 0.0;
+  for (int64_t r = 0; r < nx; ++r) {
+    sy += yx[(size_t)r];
+    syz += yx[(size_t)r] * zx[r];
+    sz += zx[r];
+  }
+  const double ate = sy / (double)nx;
+  const double ate_sd = std_y * std::sqrt(post[0]) / (double)nx;
+  const unsigned int ntx = (unsigned int)sz;  // unsigned int in the reference
+  const double att = syz / ntx;
+  const double att_sd = std_y * std::sqrt(post[1]) / ntx;
+  const unsigned int nux = (unsigned int)nx - ntx;
+  const double atu = (ate * nx - att * ntx) / nux;
+  const double atu_sd = std_y * std::sqrt(post[2]) / nux;
+  const double m3[3] = {ate, att, atu}, s3[3] = {ate_sd, att_sd, atu_sd};
+  for (int j = 0; j < 3; ++j) {
+    avg[4 * j + 0] = m3[j];
+    avg[4 * j + 1] = m3[j] - 1.96 * s3[j];
+    avg[4 * j + 2] = m3[j] + 1.96 * s3[j];
+    avg[4 * j + 3] = std::pow(s3[j], 2);
+  }
+}
+
 }  // namespace ace_host
 using namespace ace_host;
 
@@ -248,4 +310,11 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
 void shard_get_inverse(ShardModel *m, double *inv);
 void shard_collect_timing(ShardModel *m, double *t_ms, int64_t *t_launch, double *t_work);
 int shard_world(const ShardModel *m);
+int shard_any(ShardModel *m, int local);  // collective OR (RCCL), local value (simulated)
+int shard_nlocal(const ShardModel *m);                // ranks simulated in this process (1 with RCCL)
+PairSide shard_train_side(const ShardModel *m);       // the replicated training X, Z, log|Z|
+const double *shard_train_y(const ShardModel *m);     // the replicated y (npad, device)
+const double *shard_A0(const ShardModel *m, int j);   // local rank j's resident A (column blocks)
+int shard_rank_of(const ShardModel *m, int j);
+void shard_allreduce_sum(ShardModel *m, double *buf, int64_t count);
 int shard_rank(const ShardModel *m);

@@ -63,11 +63,17 @@ struct PairSide {
 // part (mode 0 without a tile list): 0 all tiles, 1 the first panel's
 // columns (J < NB/AT), 2 the rest -- 1 then 2 lets the sweep's first pivot
 // chain start while part 2 runs.
+// b0 / b1 (modes 1 and 2, no cube): sum only slices [b0, b1) -- the
+// marginal kernels of prediction (src/pred_cpp.cpp:55-67); b1 < 0 means B.
 hipError_t launch_assembly(int mode, int kind, int PM, PairSide rows,
                            PairSide cols, int64_t npad, int B, int ZS,
                            TabView tab, double sig, double *out, int64_t ld,
                            double *cube, hipStream_t st, const Tile *tiles = nullptr,
-                           int64_t ntiles = 0, int G = 1, int part = 0);
+                           int64_t ntiles = 0, int G = 1, int part = 0, int b0 = 0,
+                           int b1 = -1);
+// out[r] = sum over b in [b0, b1) of K_b(r, r) (symmetric kernel diagonal)
+hipError_t launch_kdiag(int kind, PairSide S, int ZS, TabView tab, int b0, int b1, double *out,
+                        hipStream_t st);
 
 // MFMA-expansion variant of mode 0 (ace_pairs_mm.hip)
 hipError_t launch_assembly_mm(int kind, int PM, PairSide S, int64_t npad, int B, int ZS,
@@ -78,24 +84,31 @@ bool pairs_use_mm(int PM, bool grad);
 bool mm_lds_ok(int PM, int B, int kind, bool grad);
 hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                           const double *A, int64_t ld, double sA, const double *alpha,
-                          double *gpart, double *trpart, hipStream_t st, const Tile *tiles,
-                          int64_t ntiles, int G, int64_t ndiag);
+                          double *gpart, hipStream_t st, const Tile *tiles, int64_t ntiles, int G,
+                          int64_t ndiag);
 
 // ---- gradient --------------------------------------------------------------
 // T = sA * A[r,c] - alpha_r alpha_c over the lower 64x64 tiles of [0,n)
 // (grad_ntiles(n) of them).
-// gpart: [(b*(PM+1) + i) * nsuper + tile]  (i < PM: length-scale sums,
-//        i == PM: lambda sums); trpart[tile]: trace of T.
+// gpart: tile-major partial sums, one contiguous row of grad_part_cols(PM, B)
+//        doubles per tile: [b*(PM+1) + i] (i < PM: length-scale sums,
+//        i == PM: lambda sums), then [B*(PM+1)] the trace of T.  Each tile's
+//        workgroup writes one contiguous run (launch_tile_sums reduces).
 // cube (if non-null, ld n): K_b read from the cube instead of recomputed.
 // tiles: the rank's list; ndiag >= 0 says its first ndiag entries are the
 // diagonal tiles (lets the MFMA kernel run them separately).
+__host__ __device__ constexpr int grad_part_cols(int PM, int B) { return B * (PM + 1) + 1; }
 hipError_t launch_grad(int kind, int PM, PairSide side, int B, int ZS,
                        TabView tab, const double *A, int64_t ld, double sA,
-                       const double *alpha, const double *cube,
-                       double *gpart, double *trpart, hipStream_t st,
+                       const double *alpha, const double *cube, double *gpart, hipStream_t st,
                        const Tile *tiles = nullptr, int64_t ntiles = 0, int G = 1,
                        int64_t ndiag = -1);
 int64_t grad_ntiles(int64_t n);
+// out[j] = sum_t part[t * ncols + j], j < ncols (deterministic order); work
+// needs tile_sums_work(ncols) doubles.
+hipError_t launch_tile_sums(const double *part, int64_t ntiles, int ncols, double *work,
+                            double *out, hipStream_t st);
+int64_t tile_sums_work(int ncols);
 
 // ---- sweep -----------------------------------------------------------------
 struct SweepBufs {
@@ -203,10 +216,15 @@ hipError_t launch_gemv_t(const double *M, int64_t ld, int64_t m, int64_t k,
 hipError_t launch_gemm_nn(int64_t m, int64_t n, int64_t k, const double *A,
                           int64_t lda, const double *B, int64_t ldb, double *C,
                           int64_t ldc, hipStream_t st);
-// Copies -A (lower) into a full symmetric n x n matrix (ld_out).
+// Copies scale * A (lower) into a full symmetric n x n matrix (ld_out).
 hipError_t launch_sym_from_lower(const double *A, int64_t ld, int64_t n,
                                  double scale, double *out, int64_t ld_out,
                                  hipStream_t st);
+// Same from block-cyclic column storage: global column c of A lives in
+// slot (c / NB) % G (slot_elems doubles each) at local column lcol(c, G).
+hipError_t launch_sym_from_cyclic(const double *A, int64_t ld, int64_t n, int G,
+                                  int64_t slot_elems, double scale, double *out,
+                                  int64_t ld_out, hipStream_t st);
 // dst[0:npad, 0:npad] (ld_dst) = src (n x n, ld n) + diag I, identity padding
 hipError_t launch_prepare_A(const double *src, int64_t n, double diag,
                             double *dst, int64_t ld_dst, int64_t npad,
@@ -224,5 +242,18 @@ hipError_t launch_quad3(const double *M, int64_t ld, int64_t n,
                         const double *W, double *q, hipStream_t st);
 hipError_t launch_log_abs(const double *Z, double *LZ, int64_t count,
                           hipStream_t st);
+
+// ---- products with the resident inverse (ace_symm.hip) -----------------------
+// out (n x k, ldo) = scale * S V, S = symmetric matrix with lower triangle in
+// A (ld; block-cyclic columns for G > 1: only the rank's stored entries are
+// used, so the ranks' outputs sum to S V).  vt: V[p][c] = V[c + p ldv].
+hipError_t launch_symm(const double *A, int64_t ld, int64_t n, int G, int rank, const double *V,
+                       int64_t ldv, bool vt, int64_t k, double scale, double *out, int64_t ldo,
+                       hipStream_t st);
+// a[c] = sum_q T[q + c ldt] w[q], d[c] = sum_q T[q + c ldt] K[c + q ldk], c < nx
+hipError_t launch_pred_cols(const double *T, int64_t ldt, const double *K, int64_t ldk, int64_t n,
+                            int64_t nx, const double *w, double *a, double *d, hipStream_t st);
+// w = y - mu
+hipError_t launch_center(const double *y, int64_t n, double mu, double *w, hipStream_t st);
 
 }  // namespace ace

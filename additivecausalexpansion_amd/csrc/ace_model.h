@@ -1,0 +1,99 @@
+// ace_model.h -- the device-resident model shared by the C ABI (ace_api.cpp)
+// and the resident-inverse products / prediction (ace_predict.cpp).
+#pragma once
+#include "ace_common.h"
+#include "ace_internal.h"
+
+// Buffers of one Gauss-Jordan sweep and its lookahead events.
+struct SweepWork {
+  DBuf A, P0, P1, W0, W1, SW, S0, S1, piv, flag, order;
+  std::vector<hipEvent_t> ev;
+  int64_t n = 0, npad = 0, naug = 0, norder = 0;
+  SweepWork() = default;
+  SweepWork(const SweepWork &) = delete;
+  ~SweepWork() {
+    for (auto &e : ev) (void)hipEventDestroy(e);
+  }
+  void ensure(ace_ctx *ctx, int64_t n_) {
+    n = n_;
+    npad = round_up(n, NB);
+    naug = npad + AUG;
+    alloc(ctx, A, (size_t)(naug * naug) * sizeof(double), "alloc A");
+    for (DBuf *b : {&P0, &P1, &W0, &W1}) alloc(ctx, *b, (size_t)(naug * NB) * sizeof(double), "alloc panel");
+    alloc(ctx, SW, (size_t)(SUB * SUB) * sizeof(double), "alloc SW");
+    alloc(ctx, S0, (size_t)(SUB * NB) * sizeof(double), "alloc S");
+    alloc(ctx, S1, (size_t)(SUB * NB) * sizeof(double), "alloc S");
+    alloc(ctx, piv, (size_t)npad * sizeof(double), "alloc piv");
+    alloc(ctx, flag, 16, "alloc flag");
+    norder = 0;
+    if (const int S = update_order_block(); S > 0) {
+      const std::vector<Tile> t = xcd_update_order(own_tiles(naug / UT, UT, 1, 0), S);
+      alloc(ctx, order, t.size() * sizeof(Tile), "alloc tile order");
+      ck(ctx, hipMemcpy(order.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
+         "upload tile order");
+      norder = (int64_t)t.size();
+    }
+    const size_t need = (size_t)(2 * (npad / NB) + 1);
+    while (ev.size() < need) {
+      hipEvent_t e;
+      ck(ctx, hipEventCreateWithFlags(&e, ACE_SYNC_EVENT_FLAGS), "event");
+      ev.push_back(e);
+    }
+  }
+  SweepBufs bufs() const {
+    SweepBufs b;
+    b.A = A.d();
+    b.ld = naug;
+    b.npad = npad;
+    b.P[0] = P0.d();
+    b.P[1] = P1.d();
+    b.W[0] = W0.d();
+    b.W[1] = W1.d();
+    b.SW = SW.d();
+    b.S[0] = S0.d();
+    b.S[1] = S1.d();
+    b.piv = piv.d();
+    b.flag = flag.i();
+    b.order = norder ? reinterpret_cast<const Tile *>(order.p) : nullptr;
+    b.norder = norder;
+    return b;
+  }
+  SweepSync sync(ace_ctx *ctx) {
+    SweepSync s;
+    s.side = ctx->side;
+    s.ev = ev.data();
+    s.nev = (int)ev.size();
+    return s;
+  }
+};
+
+// =====================================================================
+// Device-resident model: one para_update per call, nothing materialised
+// beyond A (the swept matrix) and O(n * tiles) partial sums.
+// =====================================================================
+struct ace_model {
+  ace_ctx *ctx = nullptr;
+  Shape s{};
+  int64_t n = 0, npad = 0, naug = 0, ntiles = 0, ntr = 0;
+  double std_y = 1.0;
+  bool has_data = false;
+  bool has_inverse = false;  // a para_update has left a resident inverse
+  SideBufs side;
+  DBuf y, tab, alpha, scal, gpart, gwork, gsum, sums;
+  PinnedBuf hio;  // [theta tables | gsum | sums | scal | flag] host staging
+  SweepWork sw;   // A = resident inverse of the last para_update
+  SweepWork sw2;  // train_stats scratch (keeps sw's inverse, Q6)
+  bool prof = false;
+  // timing events in two sets: the set of evaluation t is read back while
+  // evaluation t+1 runs (no host queries between evaluations)
+  hipEvent_t ev_asm[4] = {}, ev_grad[4] = {};
+  std::vector<hipEvent_t> ev_upd;  // 2 sets x 2 * steps
+  std::vector<double> upd_flops;   // 2 sets x steps
+  int upd_used[2] = {0, 0};
+  int tset = 0, pend = -1;  // set the next timed evaluation records; set not yet read
+  double t_ms[3] = {0, 0, 0};
+  int64_t t_launch[3] = {0, 0, 0};
+  double t_work[3] = {0, 0, 0};
+  ShardModel *shard = nullptr;  // block-column-sharded model (ace_shard.cpp)
+};
+

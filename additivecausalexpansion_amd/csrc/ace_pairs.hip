@@ -63,7 +63,8 @@ __global__ __launch_bounds__(256) void k_assembly(PairSide R, PairSide C, int64_
                                                   int B, int ZS, TabView tab, double sig,
                                                   double *__restrict__ out, int64_t ld,
                                                   double *__restrict__ cube,
-                                                  const Tile *__restrict__ tiles, int G) {
+                                                  const Tile *__restrict__ tiles, int G, int b0,
+                                                  int b1) {
   int I = blockIdx.y, J = blockIdx.x;
   if (MODE == 0 && tiles) {  // sharded: the rank's own lower tiles, 1-D grid
     const Tile tt = tiles[blockIdx.x];
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(256) void k_assembly(PairSide R, PairSide C, int64_
     }
     const bool rlo = (MODE == 2) || (r < c);  // row is the reference's first operand
     double kf = 0.0;
-    for (int b = 0; b < B; ++b) {
+    for (int b = b0; b < b1; ++b) {  // [0, B), or the marginal slices of prediction
       const double *w = tab.wk + b * PM;
       double r2 = 0.0;
 #pragma unroll
@@ -168,8 +169,7 @@ __global__ __launch_bounds__(256) void k_grad(PairSide S, int B, int ZS, TabView
                                               const double *__restrict__ A, int64_t ld,
                                               double sA, const double *__restrict__ alpha,
                                               const double *__restrict__ cube,
-                                              double *__restrict__ gpart,
-                                              double *__restrict__ trpart, int64_t ntiles,
+                                              double *__restrict__ gpart, int64_t ldg,
                                               const Tile *__restrict__ tiles, int G) {
   constexpr int NV = PM + 1;
   constexpr int NM = AT / 4;
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(256) void k_grad(PairSide S, int B, int ZS, TabView
     __syncthreads();
     if (tid < NV) {
       const double s = (red2[tid][0] + red2[tid][1]) + (red2[tid][2] + red2[tid][3]);
-      gpart[((int64_t)b * NV + tid) * ntiles + t] = s;
+      gpart[t * ldg + (int64_t)b * NV + tid] = s;
     }
   }
   // trace of T (diagonal pairs)
@@ -326,7 +326,7 @@ __global__ __launch_bounds__(256) void k_grad(PairSide S, int B, int ZS, TabView
   if (tid == 0) {
     double s = 0.0;
     for (int k = 0; k < 64; ++k) s += red[0][k];
-    trpart[t] = s;
+    gpart[t * ldg + (int64_t)B * NV] = s;
   }
 }
 
@@ -398,8 +398,7 @@ template <int PM, int KIND>
 __global__ __launch_bounds__(256) void k_grad2(PairSide S, int B, int ZS, TabView tab,
                                                const double *__restrict__ A, int64_t ld,
                                                double sA, const double *__restrict__ alpha,
-                                               double *__restrict__ gpart,
-                                               double *__restrict__ trpart, int64_t ntiles,
+                                               double *__restrict__ gpart, int64_t ldg,
                                                const Tile *__restrict__ tiles, int G) {
   constexpr int NV = PM + 1;
   constexpr int NM = AT / 4;
@@ -542,11 +541,11 @@ __global__ __launch_bounds__(256) void k_grad2(PairSide S, int B, int ZS, TabVie
         for (int i = 0; i < PM; ++i) g0[i] = fma(U0, d2[i], g0[i]);
       }
     }
-    grad_block_reduce<PM>(g1, gl1, red, red2, tid, lane, wv, gpart + (int64_t)b1 * NV * ntiles + t,
-                          ntiles);
+    grad_block_reduce<PM>(g1, gl1, red, red2, tid, lane, wv, gpart + t * ldg + (int64_t)b1 * NV,
+                          1);
     if (two)
-      grad_block_reduce<PM>(g0, gl0, red, red2, tid, lane, wv,
-                            gpart + (int64_t)b0 * NV * ntiles + t, ntiles);
+      grad_block_reduce<PM>(g0, gl0, red, red2, tid, lane, wv, gpart + t * ldg + (int64_t)b0 * NV,
+                            1);
   }
   // trace of T (diagonal pairs)
   {
@@ -560,8 +559,39 @@ __global__ __launch_bounds__(256) void k_grad2(PairSide S, int B, int ZS, TabVie
   if (tid == 0) {
     double s = 0.0;
     for (int k = 0; k < 64; ++k) s += red[0][k];
-    trpart[t] = s;
+    gpart[t * ldg + (int64_t)B * NV] = s;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Diagonal of a symmetric kernel matrix over slices [b0, b1): r2 = 0 on the
+// diagonal, so K_b(r, r) is the reference expression at r2 = 0 with both z
+// operands z_r (kernmat_*_symmetric_cpp's r == c entries; prediction needs
+// only diag(K_xx), src/pred_cpp.cpp:22-28, 71-77).
+// ---------------------------------------------------------------------------
+template <int KIND>
+__global__ void k_kdiag(PairSide S, int ZS, TabView tab, int b0, int b1, double *__restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= S.n) return;
+  double s = 0.0;
+  for (int b = b0; b < b1; ++b) {
+    double z = 0.0, lz = 0.0;
+    if (b > 0) {
+      z = S.Z[r * ZS + b - 1];
+      if (KIND == 0) lz = S.LZ[r * ZS + b - 1];
+    }
+    s += kval<KIND, false>(b, 0.0, tab.lam[b], z, z, lz, lz);
+  }
+  out[r] = s;
+}
+
+hipError_t launch_kdiag(int kind, PairSide S, int ZS, TabView tab, int b0, int b1, double *out,
+                        hipStream_t st) {
+  if (S.n <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((S.n + 255) / 256));
+  if (kind == 0) hipLaunchKernelGGL(k_kdiag<0>, grid, dim3(256), 0, st, S, ZS, tab, b0, b1, out);
+  else hipLaunchKernelGGL(k_kdiag<1>, grid, dim3(256), 0, st, S, ZS, tab, b0, b1, out);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -583,7 +613,8 @@ int64_t grad_ntiles(int64_t n) {
 template <int PM>
 static hipError_t asm_pm(int mode, int kind, PairSide R, PairSide C, int64_t npad, int B,
                          int ZS, TabView tab, double sig, double *out, int64_t ld,
-                         double *cube, hipStream_t st, const Tile *tiles, int64_t ntiles, int G) {
+                         double *cube, hipStream_t st, const Tile *tiles, int64_t ntiles, int G,
+                         int b0, int b1) {
   dim3 blk(256);
   dim3 grid;
   if (mode == 0 && tiles) {
@@ -600,7 +631,7 @@ static hipError_t asm_pm(int mode, int kind, PairSide R, PairSide C, int64_t npa
   }
 #define ACE_ASM(K, M) \
   hipLaunchKernelGGL((k_assembly<PM, K, M>), grid, blk, 0, st, R, C, npad, B, ZS, tab, sig, out, ld, \
-                     cube, tiles, G)
+                     cube, tiles, G, b0, b1)
   if (kind == 0) {
     if (mode == 0) ACE_ASM(0, 0);
     else if (mode == 1) ACE_ASM(0, 1);
@@ -635,7 +666,8 @@ bool pairs_use_mm(int PM, bool grad) {
 hipError_t launch_assembly(int mode, int kind, int PM, PairSide R, PairSide C, int64_t npad,
                            int B, int ZS, TabView tab, double sig, double *out, int64_t ld,
                            double *cube, hipStream_t st, const Tile *tiles, int64_t ntiles,
-                           int G, int part) {
+                           int G, int part, int b0, int b1) {
+  if (b1 < 0) b1 = B;
   if (mode == 0 && pairs_use_mm(PM, false) && mm_lds_ok(PM, B, kind, false))
     return launch_assembly_mm(kind, PM, R, npad, B, ZS, tab, sig, out, ld, cube, st, tiles,
                               ntiles, G, part);
@@ -643,7 +675,8 @@ hipError_t launch_assembly(int mode, int kind, int PM, PairSide R, PairSide C, i
   switch (PM) {
 #define ACE_CASE(P) \
   case P:           \
-    return asm_pm<P>(mode, kind, R, C, npad, B, ZS, tab, sig, out, ld, cube, st, tiles, ntiles, G);
+    return asm_pm<P>(mode, kind, R, C, npad, B, ZS, tab, sig, out, ld, cube, st, tiles, ntiles, G, \
+                     b0, b1);
     ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
     ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
 #undef ACE_CASE
@@ -654,24 +687,25 @@ hipError_t launch_assembly(int mode, int kind, int PM, PairSide R, PairSide C, i
 template <int PM>
 static hipError_t grad_pm(int kind, PairSide S, int B, int ZS, TabView tab, const double *A,
                           int64_t ld, double sA, const double *alpha, const double *cube,
-                          double *gpart, double *trpart, hipStream_t st, const Tile *tiles,
-                          int64_t ntiles, int G) {
+                          double *gpart, hipStream_t st, const Tile *tiles, int64_t ntiles,
+                          int G) {
   const int64_t nsuper = tiles ? ntiles : grad_ntiles(S.n);
   if (nsuper == 0) return hipSuccess;
+  const int64_t ldg = grad_part_cols(PM, B);
   dim3 grid((unsigned)nsuper), blk(256);
 #define ACE_G(K, CB)                                                                          \
   hipLaunchKernelGGL((k_grad<PM, K, CB>), grid, blk, 0, st, S, B, ZS, tab, A, ld, sA, alpha, \
-                     cube, gpart, trpart, nsuper, tiles, G)
+                     cube, gpart, ldg, tiles, G)
   const bool cb = cube != nullptr;
   if (cb) {
     if (kind == 0) ACE_G(0, true);
     else ACE_G(1, true);
   } else if (kind == 0) {
     hipLaunchKernelGGL((k_grad2<PM, 0>), grid, blk, 0, st, S, B, ZS, tab, A, ld, sA, alpha,
-                       gpart, trpart, nsuper, tiles, G);
+                       gpart, ldg, tiles, G);
   } else {
     hipLaunchKernelGGL((k_grad2<PM, 1>), grid, blk, 0, st, S, B, ZS, tab, A, ld, sA, alpha,
-                       gpart, trpart, nsuper, tiles, G);
+                       gpart, ldg, tiles, G);
   }
 #undef ACE_G
   return hipGetLastError();
@@ -679,7 +713,7 @@ static hipError_t grad_pm(int kind, PairSide S, int B, int ZS, TabView tab, cons
 
 hipError_t launch_grad(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                        const double *A, int64_t ld, double sA, const double *alpha,
-                       const double *cube, double *gpart, double *trpart, hipStream_t st,
+                       const double *cube, double *gpart, hipStream_t st,
                        const Tile *tiles, int64_t ntiles, int G, int64_t ndiag) {
   // The all-VALU gradient kernels keep per-lane p-long arrays and static LDS
   // that outgrow the 64 KB default at PM = 64: above PM = 48 the MFMA kernel
@@ -687,16 +721,18 @@ hipError_t launch_grad(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
   // cube is kernmat's K_b for the same theta, so the traces are the same).
   const bool valu_ok = PM <= 48;
   if ((!cube || !valu_ok) && (pairs_use_mm(PM, true) || !valu_ok) && mm_lds_ok(PM, B, kind, true))
-    return launch_grad_mm(kind, PM, S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st, tiles,
-                          ntiles, G, ndiag);
+    return launch_grad_mm(kind, PM, S, B, ZS, tab, A, ld, sA, alpha, gpart, st, tiles, ntiles,
+                          G, ndiag);
   if (!valu_ok) return hipErrorInvalidValue;
   switch (PM) {
 #define ACE_CASE(P) \
   case P:           \
-    return grad_pm<P>(kind, S, B, ZS, tab, A, ld, sA, alpha, cube, gpart, trpart, st, tiles, \
-                      ntiles, G);
+    return grad_pm<P>(kind, S, B, ZS, tab, A, ld, sA, alpha, cube, gpart, st, tiles, ntiles, G);
+    // no PM = 64 instantiation: the all-VALU gradient's per-lane arrays and
+    // static LDS outgrow their budget there (it returned wrong traces); the
+    // MFMA kernel above serves every PM > 48
     ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
-    ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
+    ACE_CASE(32) ACE_CASE(48)
 #undef ACE_CASE
     default: return hipErrorInvalidValue;
   }

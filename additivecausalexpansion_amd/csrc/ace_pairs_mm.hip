@@ -48,6 +48,15 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 #define SQRT3 1.7320508075688772
 
+// Lane-dependent select of two registers as two v_cndmask_b32 (no array
+// indexing the compiler could lower to a scratch gather).
+__device__ __forceinline__ double sel_f64(bool c, double a, double b) {
+  const unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+  const unsigned lo = c ? (unsigned)ua : (unsigned)ub;
+  const unsigned hi = c ? (unsigned)(ua >> 32) : (unsigned)(ub >> 32);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 __device__ __forceinline__ double sgn_mm(double x) {
   return (double)((0.0 < x) - (x < 0.0));
 }
@@ -466,8 +475,8 @@ __device__ __forceinline__ double rcp_nr_mm(double f) {
 template <int PM, int KIND, int CB, bool PS, bool DG>
 __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2)) void k_grad_mm(
     PairSide S, int B, int ZS, TabView tab, const double *__restrict__ A, int64_t ld, double sA,
-    const double *__restrict__ alpha, double *__restrict__ gpart, double *__restrict__ trpart,
-    int64_t ntiles, const Tile *__restrict__ tiles, int G, int64_t t0) {
+    const double *__restrict__ alpha, double *__restrict__ gpart, int64_t ldg,
+    const Tile *__restrict__ tiles, int G, int64_t t0) {
   constexpr int NT = 64 * 4 * (4 / CB);      // threads
   constexpr int NWV = NT / 64;               // waves
   constexpr int XP = PM + 1;
@@ -560,7 +569,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
 #pragma unroll
       for (int q = 0; q < NWV; ++q) g += red[q * RS + PM];
     }
-    gpart[((int64_t)b * NV + i) * ntiles + t] = g;
+    gpart[t * ldg + (int64_t)b * NV + i] = g;
   };
   // PS: one partial buffer per slice (the host checked L.red_slices == B)
   constexpr bool per_slice = PS;
@@ -672,8 +681,12 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
           const bool up = (lr & m) != 0;
 #pragma unroll
           for (int j = 0; j < h; ++j) {
-            const double mine = up ? cv[j + h] : cv[j];
-            const double other = up ? cv[j] : cv[j + h];
+            // both halves into named values first: selecting between the
+            // array elements themselves (a lane-dependent index) made the
+            // compiler spill cv to scratch and gather it back per lane
+            const double lo = cv[j], hi = cv[j + h];
+            const double mine = sel_f64(up, hi, lo);
+            const double other = sel_f64(up, lo, hi);
             cv[j] = mine + __shfl_xor(other, m, 64);
           }
           if (up) kk0 += h;
@@ -717,7 +730,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
     double s = 0.0;
 #pragma unroll
     for (int q = 0; q < NWV; ++q) s += str[q];
-    trpart[t] = s;
+    gpart[t * ldg + (int64_t)B * NV] = s;
   }
 }
 
@@ -735,8 +748,8 @@ __host__ __device__ constexpr int grad_cb(int PM, int kind) {
 template <int PM, int KIND, bool PS, bool DG>
 static hipError_t grad_mm_launch_ps(PairSide S, int B, int ZS, TabView tab, const double *A,
                                     int64_t ld, double sA, const double *alpha, double *gpart,
-                                    double *trpart, hipStream_t st, const Tile *tiles,
-                                    int64_t nblk, int64_t nslot, int G, size_t lds, int64_t t0) {
+                                    hipStream_t st, const Tile *tiles, int64_t nblk, int G,
+                                    size_t lds, int64_t t0) {
   constexpr int CB = grad_cb(PM, KIND);
   constexpr int NT = 64 * 4 * (4 / CB);
   if (nblk == 0) return hipSuccess;
@@ -746,7 +759,8 @@ static hipError_t grad_mm_launch_ps(PairSide S, int B, int ZS, TabView tab, cons
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL((k_grad_mm<PM, KIND, CB, PS, DG>), dim3((unsigned)nblk), dim3(NT), lds, st,
-                     S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, nslot, tiles, G, t0);
+                     S, B, ZS, tab, A, ld, sA, alpha, gpart, (int64_t)grad_part_cols(PM, B), tiles,
+                     G, t0);
   return hipGetLastError();
 }
 
@@ -757,51 +771,50 @@ static hipError_t grad_mm_launch_ps(PairSide S, int B, int ZS, TabView tab, cons
 template <int PM, int KIND, bool PS>
 static hipError_t grad_mm_launch_dg(PairSide S, int B, int ZS, TabView tab, const double *A,
                                     int64_t ld, double sA, const double *alpha, double *gpart,
-                                    double *trpart, hipStream_t st, const Tile *tiles,
-                                    int64_t nslot, int64_t ndiag, int G, size_t lds) {
+                                    hipStream_t st, const Tile *tiles, int64_t nslot,
+                                    int64_t ndiag, int G, size_t lds) {
   if (tiles && ndiag < 0)
-    return grad_mm_launch_ps<PM, KIND, PS, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart,
-                                                 st, tiles, nslot, nslot, G, lds, 0);
+    return grad_mm_launch_ps<PM, KIND, PS, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart, st, tiles,
+                                                 nslot, G, lds, 0);
   // strictly lower tiles first: the diagonal launch (one tile per CU) is
   // then a short tail instead of sharing the machine with the side stream's
   // Kfull * alpha pass at the start of the gradient phase
   const int64_t nd = tiles ? ndiag : (S.n + AT - 1) / AT;
-  hipError_t e = grad_mm_launch_ps<PM, KIND, PS, false>(S, B, ZS, tab, A, ld, sA, alpha, gpart,
-                                                        trpart, st, tiles, nslot - nd, nslot, G,
-                                                        lds, nd);
+  hipError_t e = grad_mm_launch_ps<PM, KIND, PS, false>(S, B, ZS, tab, A, ld, sA, alpha, gpart, st,
+                                                        tiles, nslot - nd, G, lds, nd);
   if (e != hipSuccess) return e;
-  return grad_mm_launch_ps<PM, KIND, PS, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st,
-                                               tiles, nd, nslot, G, lds, 0);
+  return grad_mm_launch_ps<PM, KIND, PS, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart, st, tiles,
+                                               nd, G, lds, 0);
 }
 
 template <int PM, int KIND>
 static hipError_t grad_mm_launch(PairSide S, int B, int ZS, TabView tab, const double *A,
                                  int64_t ld, double sA, const double *alpha, double *gpart,
-                                 double *trpart, hipStream_t st, const Tile *tiles,
-                                 int64_t nslot, int64_t ndiag, int G) {
+                                 hipStream_t st, const Tile *tiles, int64_t nslot, int64_t ndiag,
+                                 int G) {
   constexpr int CB = grad_cb(PM, KIND);
   constexpr int NT = 64 * 4 * (4 / CB);
   const MmLayout o = mm_layout(PM, B, KIND, true, NT / 64);
   const size_t lds = (size_t)o.total * sizeof(double);
   return o.red_slices == B
-             ? grad_mm_launch_dg<PM, KIND, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart,
-                                                 st, tiles, nslot, ndiag, G, lds)
-             : grad_mm_launch_dg<PM, KIND, false>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart,
-                                                  st, tiles, nslot, ndiag, G, lds);
+             ? grad_mm_launch_dg<PM, KIND, true>(S, B, ZS, tab, A, ld, sA, alpha, gpart, st, tiles,
+                                                 nslot, ndiag, G, lds)
+             : grad_mm_launch_dg<PM, KIND, false>(S, B, ZS, tab, A, ld, sA, alpha, gpart, st,
+                                                  tiles, nslot, ndiag, G, lds);
 }
 
 template <int PM>
 static hipError_t grad_mm_pm(int kind, PairSide S, int B, int ZS, TabView tab, const double *A,
                              int64_t ld, double sA, const double *alpha, double *gpart,
-                             double *trpart, hipStream_t st, const Tile *tiles, int64_t ntiles,
-                             int64_t ndiag, int G) {
+                             hipStream_t st, const Tile *tiles, int64_t ntiles, int64_t ndiag,
+                             int G) {
   const int64_t nt = (S.n + AT - 1) / AT;
   const int64_t nslot = tiles ? ntiles : nt * (nt + 1) / 2;
   if (nslot == 0) return hipSuccess;
-  return kind == 0 ? grad_mm_launch<PM, 0>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st,
-                                           tiles, nslot, ndiag, G)
-                   : grad_mm_launch<PM, 1>(S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st,
-                                           tiles, nslot, ndiag, G);
+  return kind == 0 ? grad_mm_launch<PM, 0>(S, B, ZS, tab, A, ld, sA, alpha, gpart, st, tiles,
+                                           nslot, ndiag, G)
+                   : grad_mm_launch<PM, 1>(S, B, ZS, tab, A, ld, sA, alpha, gpart, st, tiles,
+                                           nslot, ndiag, G);
 }
 
 // Whether the per-tile staging of the MFMA kernels fits the 160 KB of LDS
@@ -817,13 +830,12 @@ bool mm_lds_ok(int PM, int B, int kind, bool grad) {
 
 hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                           const double *A, int64_t ld, double sA, const double *alpha,
-                          double *gpart, double *trpart, hipStream_t st, const Tile *tiles,
-                          int64_t ntiles, int G, int64_t ndiag) {
+                          double *gpart, hipStream_t st, const Tile *tiles, int64_t ntiles, int G,
+                          int64_t ndiag) {
   switch (PM) {
 #define ACE_CASE(P) \
   case P:           \
-    return grad_mm_pm<P>(kind, S, B, ZS, tab, A, ld, sA, alpha, gpart, trpart, st, tiles, ntiles, \
-                         ndiag, G);
+    return grad_mm_pm<P>(kind, S, B, ZS, tab, A, ld, sA, alpha, gpart, st, tiles, ntiles, ndiag, G);
     ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
     ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
 #undef ACE_CASE

@@ -1,0 +1,233 @@
+// ace_predict.cpp -- products with the resident inverse of a model: A^-1 V
+// (ace_model_apply_inverse) and device-resident posterior prediction
+// (ace_model_predict / ace_model_predict_marginal).
+//
+// The reference's predict path (R/kernel_SE_R6.R:75-97) builds K_xX and
+// K_xx (or their n x n2 x B "elements" cubes) on the host, ships the stored
+// invKmatn, and pred_cpp / pred_marginal_cpp (src/pred_cpp.cpp:8-126) form
+// tmp = K_xX invK_XX with a full GEMM and the full n2 x n2 matrix
+// K_xx - tmp K_xX^T, of which only the diagonal (and, for ATE/ATT/ATU,
+// three quadratic forms) is used.  Here:
+//   * the inverse is the one the last para_update left in HBM (Q6: the
+//     theta_{T-1} inverse with kernels at the caller's theta_T), read from
+//     the swept matrix's lower triangle (-A^-1) by k_symm -- never copied,
+//     never sent to the host;
+//   * K_xX (the marginal slice sum for predict_marginal) is assembled on the
+//     device, test points in chunks, and T' = A^-1 K_xX^T (n x chunk) is one
+//     MFMA product per chunk;
+//   * only diag(K_xx) is formed (r2 = 0: launch_kdiag), and the ATE/ATT/ATU
+//     quadratic forms use Km_xx (n2 x n2) and three n-vectors;
+//   * sharded models: each rank multiplies by the inverse entries it stores
+//     and the per-test-point sums are all-reduced (2 n2 + 3 doubles), never
+//     the n x n2 products.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "../../include/ace_hip.h"
+
+#include "ace_common.h"
+#include "ace_internal.h"
+#include "ace_model.h"
+
+using namespace ace;
+
+namespace {
+
+// test points per chunk: K_xX and T' are n x 8192 each (4.3 GB at n = 65536)
+constexpr int64_t NXC = 8192;
+
+// out (n x k, ld n) = A^-1 V, summed over the simulated ranks; on an RCCL
+// rank the caller all-reduces (the partial holds this rank's entries only).
+void symm_resident(ace_model *m, const double *V, int64_t ldv, bool vt, int64_t k, double *out,
+                   DBuf &tmp) {
+  ace_ctx *ctx = m->ctx;
+  hipStream_t st = ctx->stream;
+  const int64_t n = m->n;
+  if (!m->shard) {  // -A^-1 is stored: scale -1
+    ck(ctx, launch_symm(m->sw.A.d(), m->naug, n, 1, 0, V, ldv, vt, k, -1.0, out, n, st), "symm");
+    return;
+  }
+  const int G = shard_world(m->shard);
+  for (int j = 0; j < shard_nlocal(m->shard); ++j) {
+    double *dst = out;
+    if (j > 0) {
+      alloc(ctx, tmp, (size_t)(n * k) * sizeof(double), "alloc symm partial");
+      dst = tmp.d();
+    }
+    ck(ctx, launch_symm(shard_A0(m->shard, j), m->naug, n, G, shard_rank_of(m->shard, j), V, ldv,
+                        vt, k, -1.0, dst, n, st),
+       "symm");
+    if (j > 0) ck(ctx, launch_add(tmp.d(), out, n * k, st), "sim all-reduce");
+  }
+}
+
+void require_inverse(ace_model *m) {
+  arg(m->ctx, m->has_data, "ace_model_set_data() not called");
+  arg(m->ctx, m->has_inverse, "no resident inverse: call ace_model_para_update() first");
+}
+
+// Shared body of ace_model_predict (marginal = false) and
+// ace_model_predict_marginal (marginal = true).
+void predict_impl(ace_model *m, const double *theta, int64_t nx, const double *X2,
+                  const double *Zt, bool marginal, const double *Z_x, int ate, double mean_y,
+                  double std_y, double std_Z, double *map, double *ci, double *var, double *avg) {
+  ace_ctx *ctx = m->ctx;
+  hipStream_t st = ctx->stream;
+  const Shape &s = m->s;
+  const int64_t n = m->n;
+  const int B = s.B;
+  const int b0 = marginal && B > 1 ? 1 : 0;  // src/pred_cpp.cpp:55-67
+  const int b1 = marginal ? (B > 1 ? B : 1) : B;
+  const double mu = theta[1];
+  // test side and theta tables (kernels at the caller's theta, Q6)
+  std::vector<double> tab = make_tab(theta, s, false);
+  DBuf dtab, dw, dKc, dT, dad, dkd, dtmp, dW3, dS3, dU3, dKmxx, dq3, dvt, ddot;
+  upload(ctx, dtab, tab.data(), tab.size(), "upload tables");
+  const TabView tv = tab_view(dtab, s);
+  SideBufs test;
+  upload_side(ctx, test, s, X2, Zt, nx, nx);
+  const PairSide train = m->shard ? shard_train_side(m->shard) : m->side.view(n);
+  // w = y - mu: a = tmp (y - mu) with tmp^T = T' below (src/pred_cpp.cpp:20, 70)
+  alloc(ctx, dw, (size_t)n * sizeof(double), "alloc w");
+  ck(ctx, launch_center(m->shard ? shard_train_y(m->shard) : m->y.d(), n, mu, dw.d(), st),
+     "center y");
+  const int64_t chunk = std::min<int64_t>(NXC, nx);
+  alloc(ctx, dKc, (size_t)(chunk * n) * sizeof(double), "alloc K_xX");
+  alloc(ctx, dT, (size_t)(chunk * n) * sizeof(double), "alloc T");
+  alloc(ctx, dad, (size_t)(2 * nx) * sizeof(double), "alloc sums");  // [a | d]
+  alloc(ctx, dkd, (size_t)nx * sizeof(double), "alloc diag");
+  std::vector<double> zx;
+  if (ate) {  // weights 1, Z_x, (Z_x == 0) (src/pred_cpp.cpp:89-106)
+    zx.assign(Z_x, Z_x + nx);
+    std::vector<double> W3((size_t)(3 * nx));
+    for (int64_t r = 0; r < nx; ++r) {
+      W3[(size_t)r] = 1.0;
+      W3[(size_t)(nx + r)] = zx[(size_t)r];
+      W3[(size_t)(2 * nx + r)] = (zx[(size_t)r] == 0) ? 1.0 : 0.0;
+    }
+    upload(ctx, dW3, W3.data(), W3.size(), "upload weights");
+    alloc(ctx, dS3, (size_t)(3 * n) * sizeof(double), "alloc s");
+    alloc(ctx, dU3, (size_t)(3 * n) * sizeof(double), "alloc u");
+    alloc(ctx, dvt, (size_t)n * sizeof(double), "alloc gemv");
+    ck(ctx, launch_fill(dS3.d(), 3 * n, 0.0, st), "zero");
+    ck(ctx, launch_fill(dU3.d(), 3 * n, 0.0, st), "zero");
+  }
+  for (int64_t c0 = 0; c0 < nx; c0 += chunk) {
+    const int64_t nc = std::min<int64_t>(chunk, nx - c0);
+    PairSide tc = test.view(nc);
+    tc.X += c0 * s.PM;
+    tc.Z += c0 * s.ZS;
+    tc.LZ += c0 * s.ZS;
+    // K_xX rows c0 .. c0 + nc (kernmat_*_cpp(X2, X, Z2, Z): test side first)
+    ck(ctx, launch_assembly(2, s.kind, s.PM, tc, train, 0, B, s.ZS, tv, 0.0, dKc.d(), nc, nullptr,
+                            st, nullptr, 0, 1, 0, b0, b1),
+       "cross assembly");
+    // T' = A^-1 K_xX^T (n x nc): the transpose of tmp = K_xX invK_XX
+    symm_resident(m, dKc.d(), nc, true, nc, dT.d(), dtmp);
+    ck(ctx, launch_pred_cols(dT.d(), n, dKc.d(), nc, n, nc, dw.d(), dad.d() + c0, dad.d() + nx + c0,
+                             st),
+       "pred sums");
+    if (ate)
+      for (int j = 0; j < 3; ++j) {
+        const double *wj = dW3.d() + j * nx + c0;
+        // s_j += K_xX^T w_j, u_j += T' w_j = A^-1 K_xX^T w_j
+        ck(ctx, launch_gemv_t(dKc.d(), nc, nc, n, wj, dvt.d(), st), "gemv_t");
+        ck(ctx, launch_add(dvt.d(), dS3.d() + j * n, n, st), "add");
+        ck(ctx, launch_gemv(dT.d(), n, n, nc, wj, dvt.d(), st), "gemv");
+        ck(ctx, launch_add(dvt.d(), dU3.d() + j * n, n, st), "add");
+      }
+  }
+  ck(ctx, launch_kdiag(s.kind, test.view(nx), s.ZS, tv, b0, b1, dkd.d(), st), "kernel diagonal");
+  std::vector<double> q3(3, 0.0), dots(3, 0.0);
+  if (ate) {
+    // w_j^T Km_xx w_j with the full marginal test kernel (kernmat_*_symmetric_cpp(X2, dZ2))
+    alloc(ctx, dKmxx, (size_t)(nx * nx) * sizeof(double), "alloc K_xx");
+    ck(ctx, launch_assembly(1, s.kind, s.PM, test.view(nx), test.view(nx), 0, B, s.ZS, tv, 0.0,
+                            dKmxx.d(), nx, nullptr, st, nullptr, 0, 1, 0, b0, b1),
+       "symmetric assembly");
+    alloc(ctx, dq3, (size_t)(3 * nx + 3) * sizeof(double), "alloc quad");
+    ck(ctx, launch_quad3(dKmxx.d(), nx, nx, dW3.d(), dq3.d(), st), "quad3");
+    // s_j . u_j  (the rank's share of s_j^T A^-1 s_j)
+    alloc(ctx, ddot, 3 * sizeof(double), "alloc dots");
+    for (int j = 0; j < 3; ++j)
+      ck(ctx, launch_gemv_t(dS3.d() + j * n, n, n, 1, dU3.d() + j * n, ddot.d() + j, st), "dot");
+    if (m->shard) shard_allreduce_sum(m->shard, ddot.d(), 3);
+    download(ctx, q3.data(), dq3.d(), 3, "download quad");
+    download(ctx, dots.data(), ddot.d(), 3, "download dots");
+  }
+  if (m->shard) shard_allreduce_sum(m->shard, dad.d(), 2 * nx);
+  std::vector<double> ad((size_t)(2 * nx)), kd((size_t)nx);
+  download(ctx, ad.data(), dad.d(), ad.size(), "download sums");
+  download(ctx, kd.data(), dkd.d(), kd.size(), "download diag");
+  sync(ctx);
+  if (!marginal) {
+    finish_pred(nx, ad.data(), kd.data(), ad.data() + nx, theta[0], mu, mean_y, std_y, map, ci,
+                var);
+    return;
+  }
+  std::vector<double> post(3);
+  for (int j = 0; j < 3; ++j) post[(size_t)j] = q3[(size_t)j] - dots[(size_t)j];
+  finish_marginal(nx, ad.data(), kd.data(), ad.data() + nx, std_y, std_Z,
+                  ate ? zx.data() : nullptr, ate ? post.data() : nullptr, map, ci, var, avg);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ace_model_apply_inverse(ace_model *m, int64_t k, const double *V, double *out) {
+  if (!m) return ACE_ERR_ARG;
+  ace_ctx *ctx = m->ctx;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, k >= 1 && V && out, "bad shape / null argument");
+  require_inverse(m);
+  const int64_t n = m->n;
+  DBuf dV, dout, dtmp;
+  upload(ctx, dV, V, (size_t)(n * k), "upload V");
+  alloc(ctx, dout, (size_t)(n * k) * sizeof(double), "alloc out");
+  symm_resident(m, dV.d(), n, false, k, dout.d(), dtmp);
+  if (m->shard) shard_allreduce_sum(m->shard, dout.d(), n * k);
+  download(ctx, out, dout.d(), (size_t)(n * k), "download out");
+  sync(ctx);
+  return ACE_OK;
+  ACE_CATCH
+}
+
+int ace_model_predict(ace_model *m, const double *theta, int64_t nx, const double *X2,
+                      const double *Z2, double mean_y, double std_y, double *map, double *ci,
+                      double *var) {
+  if (!m) return ACE_ERR_ARG;
+  ace_ctx *ctx = m->ctx;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, nx >= 1 && theta && map && ci && var && (m->s.p == 0 || X2) && (m->s.B == 1 || Z2),
+      "bad shape / null argument");
+  require_inverse(m);
+  predict_impl(m, theta, nx, X2, Z2, false, nullptr, 0, mean_y, std_y, 1.0, map, ci, var, nullptr);
+  return ACE_OK;
+  ACE_CATCH
+}
+
+int ace_model_predict_marginal(ace_model *m, const double *theta, int64_t nx, const double *X2,
+                               const double *dZ2, const double *Z_x, double std_y, double std_Z,
+                               int calculate_ate, double *map, double *ci, double *var,
+                               double *avg) {
+  if (!m) return ACE_ERR_ARG;
+  ace_ctx *ctx = m->ctx;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, nx >= 1 && theta && map && ci && var && (m->s.p == 0 || X2) && (m->s.B == 1 || dZ2),
+      "bad shape / null argument");
+  arg(ctx, !calculate_ate || (Z_x && avg), "calculate_ate needs Z_x and avg");
+  require_inverse(m);
+  predict_impl(m, theta, nx, X2, dZ2, true, Z_x, calculate_ate, 0.0, std_y, std_Z, map, ci, var,
+               avg);
+  return ACE_OK;
+  ACE_CATCH
+}
+
+}  // extern "C"

@@ -105,7 +105,7 @@ struct RankState {
   DBuf tupd, tasm, tgrad;  // device tile lists
   int64_t nupd = 0, nasm = 0, ngrad = 0, ndiag = 0;
   std::vector<Tile> hupd;  // host copy (flop accounting)
-  DBuf y, tab, alpha, scal, gpart, trpart, red, sums, augvec;
+  DBuf y, tab, alpha, scal, gpart, gwork, red, sums, augvec;
   SideBufs side;
 };
 
@@ -119,6 +119,7 @@ struct ShardModel {
   bool sim = true;
   ncclComm_t comm = nullptr;
   std::vector<std::unique_ptr<RankState>> ranks;  // 1 (RCCL) or G (simulated)
+  DBuf vote;                                       // shard_any: one double
   std::vector<hipEvent_t> ev;                      // lookahead events
   // timing of local rank 0 (update launches, assembly, gradient)
   std::vector<hipEvent_t> ev_upd;
@@ -339,7 +340,10 @@ ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int
   for (int j = 0; j < nlocal; ++j) {
     std::unique_ptr<RankState> R(new RankState());
     R->r = m->sim ? j : rank;
-    const int64_t nloc = ncols_local(naug, world, R->r);
+    // every rank allocates the largest local width (rank 0's), so that the
+    // local arrays are equal-sized all-gather operands (shard_get_inverse);
+    // the extra block column of the smaller ranks is never touched otherwise
+    const int64_t nloc = ncols_local(naug, world, 0);
     alloc(ctx, R->A[0], (size_t)(naug * nloc) * sizeof(double), "alloc local A");
     ck(ctx, hipMemsetAsync(R->A[0].p, 0, R->A[0].bytes, ctx->stream), "memset A");
     for (int b = 0; b < 2; ++b) {
@@ -371,9 +375,10 @@ ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int
     alloc(ctx, R->tab, (size_t)(2 * s.B * s.PM + s.B) * sizeof(double), "alloc tab");
     alloc(ctx, R->alpha, (size_t)npad * sizeof(double), "alloc alpha");
     alloc(ctx, R->scal, 16 * sizeof(double), "alloc scal");
-    alloc(ctx, R->gpart, (size_t)(std::max<int64_t>(R->ngrad, 1) * ncol) * sizeof(double),
+    const int ldg = grad_part_cols(s.PM, s.B);
+    alloc(ctx, R->gpart, (size_t)(std::max<int64_t>(R->ngrad, 1) * ldg) * sizeof(double),
           "alloc gpart");
-    alloc(ctx, R->trpart, (size_t)std::max<int64_t>(R->ngrad, 1) * sizeof(double), "alloc trpart");
+    alloc(ctx, R->gwork, (size_t)tile_sums_work(ldg) * sizeof(double), "alloc tile sums");
     alloc(ctx, R->red, (size_t)(ncol + 1 + npad) * sizeof(double), "alloc reduction");
     alloc(ctx, R->sums, 8 * sizeof(double), "alloc sums");
     alloc(ctx, R->augvec, (size_t)(2 * npad + 8) * sizeof(double), "alloc aug vector");
@@ -461,14 +466,12 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
     const Tile *tg = (const Tile *)R.tgrad.p;
     if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_grad[0], st), "event");
     ck(ctx, launch_grad(s.kind, s.PM, ps, s.B, s.ZS, tv, R.A[which].d(), naug, -1.0, R.alpha.d(),
-                        nullptr, R.gpart.d(), R.trpart.d(), st, tg, R.ngrad, m->G, R.ndiag),
+                        nullptr, R.gpart.d(), st, tg, R.ngrad, m->G, R.ndiag),
        "grad");
     if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_grad[1], st), "event");
-    ck(ctx, hipMemsetAsync(R.red.p, 0, R.red.bytes, st), "memset reduction");
-    if (R.ngrad > 0) {
-      ck(ctx, launch_colsum(R.gpart.d(), R.ngrad, ncol, R.red.d(), st), "colsum");
-      ck(ctx, launch_colsum(R.trpart.d(), R.ngrad, 1, R.red.d() + ncol, st), "colsum");
-    }
+    // a rank without gradient tiles contributes zeros (tile sums over none)
+    ck(ctx, launch_tile_sums(R.gpart.d(), R.ngrad, ncol + 1, R.gwork.d(), R.red.d(), st),
+       "tile sums");
   }
   allreduce(*m, 1, ncol + 1, st);
   // RMSE residual ybar - Kfull alpha = sig alpha (k_final_sums): no Kfull pass
@@ -494,37 +497,31 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
   sync(ctx);
 }
 
-// Full symmetric inverse (n x n) of the resident A[0] on every rank: own
-// lower columns into a zeroed buffer, all-reduce, mirror.
+// Full symmetric inverse (n x n) of the resident A[0] on every rank.  The
+// ranks' local arrays (equal-sized, see shard_create) are gathered into one
+// naug x (G * nloc) buffer, slot r = rank r's local columns -- an RCCL
+// all-gather, or device copies in the simulated group -- and the mirror
+// kernel reads global column c from slot (c / NB) % G at local column
+// lcol(c).  One gathered copy per process, no sums.
 void shard_get_inverse(ShardModel *m, double *inv) {
   ace_ctx *ctx = m->ctx;
   hipStream_t st = ctx->stream;
   const int64_t n = m->n, naug = m->naug;
-  DBuf out;
-  std::vector<DBuf> fulls(m->ranks.size());
-  for (size_t j = 0; j < m->ranks.size(); ++j) {
-    RankState &R = *m->ranks[j];
-    alloc(ctx, fulls[j], (size_t)(naug * naug) * sizeof(double), "alloc inverse");
-    ck(ctx, hipMemsetAsync(fulls[j].p, 0, fulls[j].bytes, st), "memset");
-    const int64_t nblk = (naug + NB - 1) / NB;
-    for (int64_t b = R.r; b < nblk; b += m->G) {
-      const int64_t c0 = b * NB, w = std::min<int64_t>(NB, naug - c0);
-      ck(ctx, hipMemcpy2DAsync(fulls[j].d() + c0 * naug, naug * sizeof(double),
-                               R.A[0].d() + lcol(c0, m->G) * naug, naug * sizeof(double),
-                               naug * sizeof(double), (size_t)w, hipMemcpyDeviceToDevice, st),
-         "copy columns");
-    }
-  }
+  const int64_t slot = naug * ncols_local(naug, m->G, 0);  // doubles per rank
+  DBuf gath, out;
+  alloc(ctx, gath, (size_t)(slot * m->G) * sizeof(double), "alloc gathered inverse");
   if (m->sim) {
-    for (size_t j = 1; j < fulls.size(); ++j)
-      ck(ctx, launch_add(fulls[j].d(), fulls[0].d(), naug * naug, st), "sum");
+    for (auto &R : m->ranks)
+      ck(ctx, hipMemcpyAsync(gath.d() + (size_t)R->r * slot, R->A[0].p, (size_t)slot * sizeof(double),
+                             hipMemcpyDeviceToDevice, st),
+         "gather local columns");
   } else {
-    nck(ctx, rccl().AllReduce(fulls[0].p, fulls[0].p, (size_t)(naug * naug), ncclDouble, ncclSum,
-                              m->comm, st),
-        "ncclAllReduce");
+    nck(ctx, rccl().AllGather(m->ranks[0]->A[0].p, gath.p, (size_t)slot, ncclDouble, m->comm, st),
+        "ncclAllGather (inverse)");
   }
   alloc(ctx, out, (size_t)(n * n) * sizeof(double), "alloc inverse");
-  ck(ctx, launch_sym_from_lower(fulls[0].d(), naug, n, -1.0, out.d(), n, st), "symmetrize");
+  ck(ctx, launch_sym_from_cyclic(gath.d(), naug, n, m->G, slot, -1.0, out.d(), n, st),
+     "symmetrize");
   download(ctx, inv, out.d(), (size_t)(n * n), "download inverse");
   sync(ctx);
 }
@@ -550,6 +547,40 @@ void shard_collect_timing(ShardModel *m, double *t_ms, int64_t *t_launch, double
   const double B = m->s.B, p = m->s.p;
   t_work[1] += pairs * B * (3 * p + 3);
   t_work[2] += pairs * (4 * B * p + 2 * p) + (m->s.kind == ACE_KERNEL_MATERN32 ? pairs * B * p : 0);
+}
+
+// Collective OR of a per-rank flag (the interrupt poll of ace_model_para_update):
+// with RCCL every rank must take the same branch, or the ranks that stop
+// leave the others blocked in the next sweep's collectives.  Simulated
+// groups share the process's poll, so the local value is already common.
+int shard_any(ShardModel *m, int local) {
+  if (m->sim) return local;
+  ace_ctx *ctx = m->ctx;
+  hipStream_t st = ctx->stream;
+  alloc(ctx, m->vote, sizeof(double), "alloc vote");
+  double v = local ? 1.0 : 0.0;
+  ck(ctx, hipMemcpyAsync(m->vote.p, &v, sizeof(double), hipMemcpyHostToDevice, st), "vote up");
+  nck(ctx, rccl().AllReduce(m->vote.p, m->vote.p, 1, ncclDouble, ncclMax, m->comm, st),
+      "ncclAllReduce (interrupt vote)");
+  ck(ctx, hipMemcpyAsync(&v, m->vote.p, sizeof(double), hipMemcpyDeviceToHost, st), "vote down");
+  sync(ctx);
+  return v != 0.0;
+}
+
+// ---- access for the resident-inverse products (ace_predict.cpp) --------------
+int shard_nlocal(const ShardModel *m) { return (int)m->ranks.size(); }
+PairSide shard_train_side(const ShardModel *m) { return m->ranks[0]->side.view(m->n); }
+const double *shard_train_y(const ShardModel *m) { return m->ranks[0]->y.d(); }
+const double *shard_A0(const ShardModel *m, int j) { return m->ranks[(size_t)j]->A[0].d(); }
+int shard_rank_of(const ShardModel *m, int j) { return m->ranks[(size_t)j]->r; }
+
+// Sum over ranks of `count` doubles (in place, device).  Simulated groups
+// sum their local partials themselves, so only RCCL has work to do.
+void shard_allreduce_sum(ShardModel *m, double *buf, int64_t count) {
+  if (m->sim || count <= 0) return;
+  nck(m->ctx, rccl().AllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, m->comm,
+                               m->ctx->stream),
+      "ncclAllReduce");
 }
 
 int shard_world(const ShardModel *m) { return m->G; }

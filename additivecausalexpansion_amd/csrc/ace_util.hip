@@ -177,6 +177,52 @@ hipError_t launch_colsum(const double *in, int64_t nrows, int ncols, double *out
   return hipGetLastError();
 }
 
+// Sums of the tile-major gradient partials (one row of ncols per tile).
+// Pass 1: block (g, ch) sums columns 64 g .. 64 g + 63 over tile chunk ch;
+// lane = column, so each wave reads one contiguous 512-B run of a tile row;
+// the 4 waves interleave tiles and meet in LDS.  Pass 2: the chunk partials.
+// Fixed summation order: bit-identical run to run.
+constexpr int TS_CHUNKS = 128;
+
+__global__ __launch_bounds__(256) void k_tile_sums1(const double *__restrict__ part,
+                                                    int64_t ntiles, int ncols,
+                                                    double *__restrict__ work) {
+  __shared__ double sh[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  const int64_t per = (ntiles + TS_CHUNKS - 1) / TS_CHUNKS;
+  const int64_t t0 = (int64_t)blockIdx.y * per;
+  const int64_t t1 = t0 + per < ntiles ? t0 + per : ntiles;
+  double s = 0.0;
+  if (col < ncols)
+    for (int64_t t = t0 + wv; t < t1; t += 4) s += part[t * ncols + col];
+  sh[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && col < ncols)
+    work[(int64_t)blockIdx.y * ncols + col] = (sh[0][lane] + sh[1][lane]) + (sh[2][lane] + sh[3][lane]);
+}
+
+__global__ __launch_bounds__(256) void k_tile_sums2(const double *__restrict__ work, int ncols,
+                                                    double *__restrict__ out) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= ncols) return;
+  double s = 0.0;
+  for (int ch = 0; ch < TS_CHUNKS; ++ch) s += work[(int64_t)ch * ncols + col];
+  out[col] = s;
+}
+
+int64_t tile_sums_work(int ncols) { return (int64_t)TS_CHUNKS * ncols; }
+
+hipError_t launch_tile_sums(const double *part, int64_t ntiles, int ncols, double *work,
+                            double *out, hipStream_t st) {
+  if (ncols <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_tile_sums1, dim3((unsigned)((ncols + 63) / 64), TS_CHUNKS), dim3(256), 0,
+                     st, part, ntiles, ncols, work);
+  hipLaunchKernelGGL(k_tile_sums2, dim3((unsigned)((ncols + 255) / 256)), dim3(256), 0, st, work,
+                     ncols, out);
+  return hipGetLastError();
+}
+
 // s = Kfull alpha (explicit, the ABI path) or null: then the fused model's
 // identity ybar - Kfull alpha = sig alpha is used -- A = Kfull + sig I is the
 // matrix the sweep inverted and alpha = A^-1 ybar, so the residual of
@@ -323,10 +369,15 @@ hipError_t launch_gemm_nn(int64_t m, int64_t n, int64_t k, const double *A, int6
 
 // ---------------------------------------------------------------- copies
 // out (full n x n) = scale * sym(A lower); tile-transposed through LDS.
+// G > 1: A is block-cyclic column storage (launch_sym_from_cyclic).
+__device__ __forceinline__ int64_t cyc_col(int64_t c, int64_t ld, int G, int64_t slot) {
+  return G == 1 ? c * ld : ((c / NB) % G) * slot + lcol(c, G) * ld;
+}
+
 __global__ __launch_bounds__(256) void k_sym_from_lower(const double *__restrict__ A,
                                                         int64_t ld, int64_t n, double scale,
                                                         double *__restrict__ out,
-                                                        int64_t ldo) {
+                                                        int64_t ldo, int G, int64_t slot) {
   __shared__ double t[64][65];
   const int64_t I = blockIdx.y, J = blockIdx.x;
   const int tid = threadIdx.x;
@@ -335,7 +386,7 @@ __global__ __launch_bounds__(256) void k_sym_from_lower(const double *__restrict
       const int a = e & 63, b = e >> 6;
       const int64_t r = I * 64 + a, c = J * 64 + b;
       if (r < n && c < n) {
-        const double v = (r >= c) ? A[r + c * ld] : A[c + r * ld];
+        const double v = (r >= c) ? A[r + cyc_col(c, ld, G, slot)] : A[c + cyc_col(r, ld, G, slot)];
         out[r + c * ldo] = scale * v;
       }
     }
@@ -344,7 +395,7 @@ __global__ __launch_bounds__(256) void k_sym_from_lower(const double *__restrict
     for (int e = tid; e < 4096; e += 256) {
       const int b = e & 63, a = e >> 6;  // b: row of A (= c), a: col of A (= r)
       const int64_t c = J * 64 + b, r = I * 64 + a;
-      t[a][b] = (r < n && c < n) ? A[c + r * ld] : 0.0;
+      t[a][b] = (r < n && c < n) ? A[c + cyc_col(r, ld, G, slot)] : 0.0;
     }
     __syncthreads();
     for (int e = tid; e < 4096; e += 256) {
@@ -359,7 +410,16 @@ hipError_t launch_sym_from_lower(const double *A, int64_t ld, int64_t n, double 
                                  double *out, int64_t ldo, hipStream_t st) {
   const unsigned nt = (unsigned)((n + 63) / 64);
   hipLaunchKernelGGL(k_sym_from_lower, dim3(nt, nt), dim3(256), 0, st, A, ld, n, scale, out,
-                     ldo);
+                     ldo, 1, (int64_t)0);
+  return hipGetLastError();
+}
+
+hipError_t launch_sym_from_cyclic(const double *A, int64_t ld, int64_t n, int G,
+                                  int64_t slot_elems, double scale, double *out, int64_t ldo,
+                                  hipStream_t st) {
+  const unsigned nt = (unsigned)((n + 63) / 64);
+  hipLaunchKernelGGL(k_sym_from_lower, dim3(nt, nt), dim3(256), 0, st, A, ld, n, scale, out,
+                     ldo, G, slot_elems);
   return hipGetLastError();
 }
 

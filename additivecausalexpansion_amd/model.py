@@ -91,6 +91,48 @@ class DeviceModel:
         check(lib().ace_model_get_inverse(self.handle, ptr(out)), self.ctx.handle)
         return out
 
+    def apply_inverse(self, V):
+        """ace_model_apply_inverse: A^-1 V with the resident inverse (V n x k)."""
+        Vf = np.asfortranarray(np.asarray(V, dtype=np.float64).reshape(self.n, -1))
+        out = np.empty_like(Vf, order="F")
+        check(lib().ace_model_apply_inverse(self.handle, Vf.shape[1], ptr(Vf), ptr(out)),
+              self.ctx.handle)
+        return out if np.ndim(V) == 2 else out.ravel()
+
+    def predict(self, theta, X2, Z2, mean_y, std_y):
+        """ace_model_predict: pred_cpp with the resident inverse (Q6), kernels at theta."""
+        th = np.ascontiguousarray(np.ravel(theta), dtype=np.float64)
+        X2f = fmat(X2)
+        nx = X2f.shape[0]
+        Z2f = np.asfortranarray(np.asarray(Z2, dtype=np.float64).reshape(nx, -1))
+        mp, var = np.empty(nx), np.empty(nx)
+        ci = np.empty((nx, 2), order="F")
+        check(lib().ace_model_predict(self.handle, ptr(th), nx, ptr(X2f), ptr(Z2f), float(mean_y),
+                                      float(std_y), ptr(mp), ptr(ci), ptr(var)), self.ctx.handle)
+        return {"map": mp, "ci": ci, "var": var}
+
+    def predict_marginal(self, theta, X2, dZ2, Z_x, std_y, std_Z, calculate_ate):
+        """ace_model_predict_marginal: pred_marginal_cpp with the resident inverse."""
+        th = np.ascontiguousarray(np.ravel(theta), dtype=np.float64)
+        X2f = fmat(X2)
+        nx = X2f.shape[0]
+        dZf = np.asfortranarray(np.asarray(dZ2, dtype=np.float64).reshape(nx, -1))
+        zx = (np.ascontiguousarray(np.ravel(Z_x), dtype=np.float64)
+              if calculate_ate else None)
+        mp, var, avg = np.empty(nx), np.empty(nx), np.empty(12)
+        ci = np.empty((nx, 2), order="F")
+        check(lib().ace_model_predict_marginal(self.handle, ptr(th), nx, ptr(X2f), ptr(dZf),
+                                               ptr(zx), float(std_y),
+                                               float(np.ravel([std_Z])[0]),
+                                               1 if calculate_ate else 0, ptr(mp), ptr(ci),
+                                               ptr(var), ptr(avg)), self.ctx.handle)
+        out = {"map": mp, "ci": ci, "var": var}
+        if calculate_ate:
+            for j, key in enumerate(("ate", "att", "atu")):
+                a = avg[4 * j:4 * j + 4]
+                out[key] = {"map": a[0], "ci": np.array([a[1], a[2]]), "var": a[3]}
+        return out
+
     def profile(self, enable):
         check(lib().ace_model_profile(self.handle, 1 if enable else 0), self.ctx.handle)
 
@@ -238,8 +280,17 @@ class _KernelClass:
         self._mark_kernel(X, Z)
         return model.train_stats(self.parameters)
 
+    def _resident(self, y, X, Z):
+        """The device model holds this fit's inverse (invKmatn never replaced
+        from outside) and was built on the same training data."""
+        return (self._inv_from_model and self._model is not None and
+                self._data_id == (id(y), id(X), id(Z)))
+
     def predict(self, y, X, Z, X2, Z2, mean_y, std_y):
-        """R/kernel_SE_R6.R:75-83"""
+        """R/kernel_SE_R6.R:75-83.  With the fit's device model the inverse
+        stays in HBM (ace_model_predict); otherwise the pred_cpp ABI."""
+        if self._resident(y, X, Z):
+            return self._model.predict(self.parameters, X2, Z2, mean_y, std_y)
         K_xX = self.kernel_mat(X2, X, Z2, Z)["full"]
         f = (native.kernmat_SE_symmetric_cpp if self.kernel == "SE"
              else native.kernmat_Matern32_symmetric_cpp)
@@ -248,7 +299,10 @@ class _KernelClass:
                                K_xx, mean_y, std_y, ctx=self.ctx)
 
     def predict_marginal(self, y, X, Z, X2, Z2, dZ2, mean_y, std_y, std_Z, calculate_ate):
-        """R/kernel_SE_R6.R:84-97"""
+        """R/kernel_SE_R6.R:84-97 (device-resident like predict)."""
+        if self._resident(y, X, Z):
+            return self._model.predict_marginal(self.parameters, X2, dZ2, Z2, std_y, std_Z,
+                                                calculate_ate)
         Km_xX = self.kernel_mat(X2, X, dZ2, Z)["elements"]
         f = (native.kernmat_SE_symmetric_cpp if self.kernel == "SE"
              else native.kernmat_Matern32_symmetric_cpp)

@@ -30,9 +30,13 @@ def _theta(parameters):
     return np.ascontiguousarray(np.ravel(parameters), dtype=np.float64)
 
 
-def _check_theta(theta, B, p):
-    if theta.shape[0] < 2 + B * (p + 1) - 1:
-        raise AceError("parameters too short for B and p")
+def _check_theta(theta, B, p, grad=False):
+    """The kernel reads theta up to P - 2 (P = 2 + B (p + 1)), so the kernmat_*
+    routines accept P - 1 entries like the reference's; the gradient also
+    reads the last, gradient-indexed length scale (Q1) and needs all P."""
+    need = 2 + B * (p + 1) - (0 if grad else 1)
+    if theta.shape[0] < need:
+        raise AceError(f"parameters too short for B={B} and p={p}: {theta.shape[0]} < {need}")
 
 
 # ---------------------------------------------------------------- kernels
@@ -108,6 +112,7 @@ def _grad(kind, y, X, Z, Kfull, K, invKmatn, eigenval, parameters, stats, B, std
         raise AceError("B != ncol(Z) + 1")
     yv = np.ascontiguousarray(np.ravel(y), dtype=np.float64)
     th = _theta(parameters)
+    _check_theta(th, B, p, grad=True)
     Kf = fmat(Kfull)
     Kc = fmat(K) if K is not None else None
     inv = fmat(invKmatn)

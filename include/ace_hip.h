@@ -64,7 +64,10 @@ const char *ace_last_error(const ace_ctx *ctx);
  * its row loops, src/kernel_SE_cpp.cpp): poll(user) is called between
  * iterations of ace_model_train and before every ace_model_para_update; a
  * non-zero return stops the call with ACE_ERR_INTERRUPTED (the R shim maps
- * it to R's interrupt).  poll == NULL removes it. */
+ * it to R's interrupt).  poll == NULL removes it.  On a model sharded over
+ * RCCL the ranks' poll results are OR-ed by a one-double all-reduce before
+ * every para_update (ranks without a poll vote 0), so all ranks stop before
+ * the same evaluation and none is left inside a collective. */
 int ace_set_interrupt_poll(ace_ctx *ctx, int (*poll)(void *user), void *user);
 
 /* ------------------------------------------------ Rcpp-export equivalents */
@@ -195,6 +198,31 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad,
 int ace_model_train_stats(ace_model *m, const double *theta, double *stats);
 /* Copies the resident training inverse (n x n) to the host. */
 int ace_model_get_inverse(ace_model *m, double *inv);
+/* out (n x k) = A^-1 V with the resident inverse of the last para_update,
+ * V and out column-major n x k on the host.  The inverse never leaves HBM
+ * (sharded: each rank multiplies by the entries it stores, one all-reduce of
+ * n x k).  ACE_ERR_ARG before the first para_update. */
+int ace_model_apply_inverse(ace_model *m, int64_t k, const double *V, double *out);
+
+/* Device-resident predict (R/kernel_SE_R6.R:75-83 -> pred_cpp,
+ * src/pred_cpp.cpp:8-34): kernels at `theta` (P, the caller's current
+ * parameters), inverse = the resident one of the last para_update (Q6: the
+ * R6 invKmatn).  X2 nx x p, Z2 nx x (B-1) column-major (the test basis).
+ * map (nx), ci (nx x 2), var (nx) as pred_cpp's list.  K_xX is assembled
+ * on the device, only diag(K_xx) is formed; nothing n x n crosses PCIe. */
+int ace_model_predict(ace_model *m, const double *theta, int64_t nx, const double *X2,
+                      const double *Z2, double mean_y, double std_y, double *map, double *ci,
+                      double *var);
+/* Device-resident predict_marginal (R/kernel_SE_R6.R:84-97 ->
+ * pred_marginal_cpp, src/pred_cpp.cpp:37-126): the marginal kernels are the
+ * slice sums b >= 1 (slice 0 if B == 1) of the cross / test kernels built
+ * with dZ2 (nx x (B-1), the basis derivative at the test treatments).
+ * Z_x (nx) is the treatment column the reference receives as Z2; it is read
+ * only when calculate_ate != 0.  avg (12) as ace_pred_marginal. */
+int ace_model_predict_marginal(ace_model *m, const double *theta, int64_t nx, const double *X2,
+                               const double *dZ2, const double *Z_x, double std_y, double std_Z,
+                               int calculate_ate, double *map, double *ci, double *var,
+                               double *avg);
 /* Per-kernel device timing for the roofline report: when enabled, HIP
  * events bracket every launch of the dense update kernel (`which` = 0),
  * the assembly kernel (1) and the gradient kernel (2) on the model's
@@ -239,10 +267,11 @@ int ace_model_train(ace_model *m, int optimizer, double learn_rate,
  * A is distributed by NB = 256-wide column blocks, block-cyclic over the
  * `world` ranks (block j on rank j % world), one process per GPU.  Each
  * sweep step broadcasts the pivot block's column panel from its owner and
- * all-gathers the panel's row pieces (RCCL over xGMI); assembly, update,
- * gradient and Kfull*alpha work only on the rank's own columns; one
- * all-reduce per evaluation combines alpha, the gradient partial sums and
- * Kfull*alpha.  Every rank returns identical grad / stats.
+ * all-gathers the panel's row pieces (RCCL over xGMI); assembly, update and
+ * gradient work only on the rank's own columns; one all-reduce per
+ * evaluation combines the swept [y; 1] rows (alpha, mu) and a second one the
+ * gradient partial sums (the RMSE residual is sig * alpha, so no Kfull*alpha
+ * pass exists).  Every rank returns identical grad / stats.
  *
  * Bootstrap: rank 0 calls ace_comm_unique_id() and sends the 128 bytes to
  * every rank out of band (MPI, torch.distributed, a file); each rank then

@@ -265,9 +265,14 @@ List ace_model_fit(SEXP model, int optimizer, double learn_rate, double momentum
                    double beta2, bool norm_clip, double clip_at, int maxiter, double tol,
                    NumericVector parameters) {
   XPtr<ace_model, PreserveStorage, ace_model_destroy, true> m(model);
-  NumericVector st(2);
+  if (maxiter < 1) Rcpp::stop("ace: maxiter must be >= 1");
+  // the R loop's matrix(0, 2, maxiter + 2) (R/main_ace.R:213): the library
+  // writes all 2 x (maxiter + 2) entries
+  NumericMatrix st(2, maxiter + 2);
   int iters = 0, converged = 0;
   ok(ace_model_train(m.get(), optimizer, learn_rate, momentum, beta1, beta2, norm_clip ? 1 : 0,
                      clip_at, maxiter, tol, parameters.begin(), st.begin(), &iters, &converged));
-  return List::create(_["stats"] = st, _["iterations"] = iters, _["converged"] = converged != 0);
+  // stats[, 3:(iter + 2)] as ace.train returns it (R/main_ace.R:235)
+  NumericMatrix out = st(_, Range(2, iters + 1));
+  return List::create(_["stats"] = out, _["iterations"] = iters, _["converged"] = converged != 0);
 }

@@ -1,0 +1,177 @@
+"""GPU parity tests of the device-resident prediction path
+(ace_model_predict / ace_model_predict_marginal / ace_model_apply_inverse):
+the resident inverse of the last para_update (Q6: theta_{T-1}) with kernels
+at the caller's theta_T, against the oracle's pred_cpp / pred_marginal_cpp
+(src/pred_cpp.cpp:8-126) fed the oracle's own kernels and inverse.
+
+Tolerances (north star 1e-6 relative fp64): map / ci relative 1e-6; the
+variance is |K_xx - tmp K_xX^T (+ e^sigma)|, a difference of terms up to
+cond x larger than the result under Q6's theta mix, so it is held to 1e-6
+of the cancelled terms std_y^2 (|K_xx,rr| + q_r).
+"""
+import numpy as np
+import pytest
+from test_gpu import close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def A():
+    import additivecausalexpansion_amd as pkg
+    pkg.default_context()
+    return pkg
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import ace_oracle
+    return ace_oracle
+
+
+def _fit_state(O, kernel, n, p, B, seed, sharded=False, world=1, A=None, mix=True):
+    """A model whose resident inverse is at theta_{T-1} = th, and theta_T:
+    th + 0.02 (mix, Q6), or th itself (then the marginal posterior
+    covariance is positive semidefinite and ATE/ATT/ATU's square roots exist,
+    which the Q6 mix does not guarantee -- the reference then returns NaN)."""
+    from additivecausalexpansion_amd.synthetic import make_problem
+    y, X, Z, th, sy = make_problem(n, p, B, seed=seed)
+    m = A.DeviceModel(kernel, n, p, B, world=world, sharded=sharded)
+    m.set_data(y, X, Z, sy)
+    th_prev = th.copy()
+    m.para_update(2, th_prev)             # resident inverse at theta_{T-1}
+    th_now = th + 0.02 if mix else th.copy()  # kernels at theta_T (Q6)
+    th_now[1] = 0.13
+    inv = O.invkernel_cpp(O.KERNELS[kernel][0](X, Z, th)["full"], th[0])["inv"]
+    return m, y, X, Z, th_now, sy, inv
+
+
+def _test_points(p, B, nx, seed):
+    from additivecausalexpansion_amd.synthetic import make_problem
+    _, X2, Z2, _, _ = make_problem(nx, p, B, seed=seed)
+    return X2, Z2
+
+
+def _var_terms(O, kernel, X2, Z2, th, sy, inv, K_xX, extra):
+    kxx = np.diag(O.KERNELS[kernel][0](X2, Z2, th)["full"])
+    q = np.abs(np.sum((K_xX @ inv) * K_xX, axis=1))
+    return sy ** 2 * (np.abs(kxx) + q + extra)
+
+
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+@pytest.mark.parametrize("n,p,B,nx", [(300, 3, 5, 70), (700, 20, 10, 257), (130, 1, 1, 9)])
+def test_device_predict_matches_oracle(A, O, kernel, n, p, B, nx):
+    m, y, X, Z, th, sy, inv = _fit_state(O, kernel, n, p, B, seed=n, A=A)
+    X2, Z2 = _test_points(p, B, nx, seed=n + 1)
+    sym, cross = O.KERNELS[kernel][0], O.KERNELS[kernel][1]
+    K_xX = cross(X2, X, Z2, Z, th)["full"]
+    ref = O.pred_cpp(y, th[0], th[1], inv, K_xX, sym(X2, Z2, th)["full"], 0.3, 1.7)
+    got = m.predict(th, X2, Z2, 0.3, 1.7)
+    close(got["map"], ref["map"])
+    close(got["ci"], ref["ci"], 1e-6, 1e-8)
+    terms = _var_terms(O, kernel, X2, Z2, th, 1.7, inv, K_xX, np.exp(th[0]))
+    assert np.all(np.abs(got["var"] - ref["var"]) <= 1e-6 * terms)
+
+
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+@pytest.mark.parametrize("B", [1, 2, 6])
+def test_device_predict_marginal_ate_matches_oracle(A, O, kernel, B):
+    n, p, nx = 400, 3, 150
+    m, y, X, Z, th, sy, inv = _fit_state(O, kernel, n, p, B, seed=5 + B, A=A, mix=False)
+    X2, Z2 = _test_points(p, B, nx, seed=77)
+    dZ2 = np.asfortranarray(Z2 * 0.7 + 0.1)  # a stand-in derivative basis
+    zx = (np.arange(nx) % 3 == 0).astype(float)
+    sym, cross = O.KERNELS[kernel][0], O.KERNELS[kernel][1]
+    Km_xX = cross(X2, X, dZ2, Z, th)["elements"]
+    Km_xx = sym(X2, dZ2, th)["elements"]
+    ref = O.pred_marginal_cpp(y, zx, th[0], th[1], inv, Km_xX, Km_xx, 0.3, 1.7, 0.8, True)
+    got = m.predict_marginal(th, X2, dZ2, zx, 1.7, 0.8, True)
+    close(got["map"], ref["map"])
+    sl = slice(1, B) if B > 1 else slice(0, 1)
+    KmX = Km_xX[:, :, sl].sum(axis=2)
+    kxx = np.diag(Km_xx[:, :, sl].sum(axis=2))
+    q = np.abs(np.sum((KmX @ inv) * KmX, axis=1))
+    terms = (1.7 / 0.8) ** 2 * (np.abs(kxx) + q)
+    assert np.all(np.abs(got["var"] - ref["var"]) <= 1e-6 * terms)
+    for k in ("ate", "att", "atu"):
+        close(got[k]["map"], ref[k]["map"])
+        close(got[k]["var"], ref[k]["var"], 1e-6, 1e-10)
+        close(got[k]["ci"], ref[k]["ci"], 1e-6, 1e-8)
+    plain = m.predict_marginal(th, X2, dZ2, zx, 1.7, 0.8, False)
+    assert "ate" not in plain and np.array_equal(plain["map"], got["map"])
+
+
+def test_device_predict_chunks_and_padding(A, O):
+    """nx above one 8192-point chunk plus a ragged tail, n not a multiple of
+    the 128-row product tile."""
+    kernel, n, p, B, nx = "SE", 333, 2, 3, 8192 + 77
+    m, y, X, Z, th, sy, inv = _fit_state(O, kernel, n, p, B, seed=3, A=A)
+    X2, Z2 = _test_points(p, B, nx, seed=4)
+    K_xX = O.KERNELS[kernel][1](X2, X, Z2, Z, th)["full"]
+    tmp = K_xX @ inv  # src/pred_cpp.cpp:19-28 without the nx x nx K_xx
+    mp = 0.5 + 1.5 * (tmp @ (y - th[1]) + th[1])
+    # diag(K_xx): r2 = 0, slice 0 exp(lam_0) plus z^2 exp(lam_b) (SE, z != 0)
+    kxx = np.exp(th[2]) + sum(Z2[:, b - 1] ** 2 * np.exp(th[2 + b]) for b in range(1, B))
+    q = np.sum(tmp * K_xX, axis=1)
+    var = (1.5 * np.sqrt(np.abs(kxx - q + np.exp(th[0])))) ** 2
+    got = m.predict(th, X2, Z2, 0.5, 1.5)
+    close(got["map"], mp)
+    assert np.all(np.abs(got["var"] - var) <= 1e-6 * 1.5 ** 2 * (np.abs(kxx) + np.abs(q) + 1))
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_sharded_predict_matches_single(A, O, world):
+    """Sharded models multiply by the inverse entries each rank stores and
+    all-reduce the per-point sums: same result as one GPU."""
+    kernel, n, p, B, nx = "Matern32", 1100, 4, 5, 300
+    single, y, X, Z, th, sy, inv = _fit_state(O, kernel, n, p, B, seed=21, A=A, mix=False)
+    sh, *_ = _fit_state(O, kernel, n, p, B, seed=21, sharded=True, world=world, A=A, mix=False)
+    X2, Z2 = _test_points(p, B, nx, seed=22)
+    a, b = single.predict(th, X2, Z2, 0.1, 1.3), sh.predict(th, X2, Z2, 0.1, 1.3)
+    # the sharded sweep's operand order differs: inverses agree to ~1e-10 of
+    # their scale (test_shard_gpu), the predictions to 1e-9 of theirs
+    close(b["map"], a["map"], 1e-8, 1e-9)
+    close(b["var"], a["var"], 1e-7, 1e-9)
+    zx = (np.arange(nx) % 2).astype(float)
+    a = single.predict_marginal(th, X2, Z2, zx, 1.3, 0.9, True)
+    b = sh.predict_marginal(th, X2, Z2, zx, 1.3, 0.9, True)
+    close(b["map"], a["map"], 1e-8, 1e-9)
+    for k in ("ate", "att", "atu"):
+        close(b[k]["var"], a[k]["var"], 1e-7, 1e-12)
+    V = np.random.default_rng(0).normal(size=(n, 5))
+    close(sh.apply_inverse(V), single.apply_inverse(V), 1e-8, 1e-9)
+
+
+def test_sharded_rccl_world1_predict(A, O):
+    kernel, n, p, B, nx = "SE", 700, 3, 4, 120
+    single, y, X, Z, th, sy, inv = _fit_state(O, kernel, n, p, B, seed=8, A=A)
+    from additivecausalexpansion_amd.synthetic import make_problem
+    y, X, Z, th0, sy = make_problem(n, p, B, seed=8)
+    sh = A.DeviceModel(kernel, n, p, B, world=1, rank=0, unique_id=A.comm_unique_id(),
+                       sharded=True)
+    sh.set_data(y, X, Z, sy)
+    sh.para_update(2, th0.copy())
+    X2, Z2 = _test_points(p, B, nx, seed=9)
+    close(sh.predict(th, X2, Z2, 0.0, 1.0)["map"], single.predict(th, X2, Z2, 0.0, 1.0)["map"],
+          1e-8, 1e-9)
+    V = np.random.default_rng(1).normal(size=(n, 3))
+    close(sh.apply_inverse(V), single.apply_inverse(V), 1e-8, 1e-9)
+
+
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+def test_apply_inverse_matches_oracle(A, O, kernel):
+    n, p, B = 513, 3, 4
+    m, y, X, Z, th, sy, inv = _fit_state(O, kernel, n, p, B, seed=2, A=A)
+    V = np.random.default_rng(5).normal(size=(n, 70))
+    close(m.apply_inverse(V), inv @ V, 1e-9, 1e-9)
+    v = np.random.default_rng(6).normal(size=n)
+    close(m.apply_inverse(v), inv @ v, 1e-9, 1e-9)
+
+
+def test_predict_before_para_update_raises(A):
+    m = A.DeviceModel("SE", 100, 2, 3)
+    from additivecausalexpansion_amd.synthetic import make_problem
+    y, X, Z, th, sy = make_problem(100, 2, 3, seed=1)
+    m.set_data(y, X, Z, sy)
+    with pytest.raises(A.AceError, match="ARG"):
+        m.predict(th, X[:5], Z[:5], 0.0, 1.0)
