@@ -46,6 +46,29 @@ SIGNATURES = {
                                          ctypes.c_double, _D, _D, _D, ctypes.c_double,
                                          ctypes.c_double, ctypes.c_double, ctypes.c_int, _D, _D,
                                          _D, _D]),
+    "ace_dmat_upload": (ctypes.c_int, [_vp, _I64, _I64, _I64, _D, ctypes.POINTER(_vp)]),
+    "ace_dmat_dims": (ctypes.c_int, [_vp, ctypes.POINTER(_I64), ctypes.POINTER(_I64),
+                                     ctypes.POINTER(_I64)]),
+    "ace_dmat_read": (ctypes.c_int, [_vp, _I64, _I64, _D]),
+    "ace_dmat_materialized": (ctypes.c_int, [_vp]),
+    "ace_dmat_free": (None, [_vp]),
+    "ace_kernmat_sym_dev": (ctypes.c_int, [_vp, ctypes.c_int, _I64, ctypes.c_int, ctypes.c_int,
+                                           _D, _D, _D, ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
+    "ace_kernmat_cross_dev": (ctypes.c_int, [_vp, ctypes.c_int, _I64, _I64, ctypes.c_int,
+                                             ctypes.c_int, _D, _D, _D, _D, _D,
+                                             ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
+    "ace_invkernel_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_double, _D, ctypes.POINTER(_vp)]),
+    "ace_mu_solution_dev": (ctypes.c_int, [_vp, _I64, _D, _vp, _D]),
+    "ace_stats_dev": (ctypes.c_int, [_vp, _I64, _D, _vp, _vp, _D, ctypes.c_double,
+                                     ctypes.c_double, _D]),
+    "ace_grad_dev": (ctypes.c_int, [_vp, ctypes.c_int, _I64, ctypes.c_int, ctypes.c_int, _D, _D,
+                                    _D, _vp, _vp, _vp, _D, _D, _D, ctypes.c_double, _D]),
+    "ace_pred_dev": (ctypes.c_int, [_vp, _I64, _I64, _D, ctypes.c_double, ctypes.c_double, _vp,
+                                    _vp, _vp, ctypes.c_double, ctypes.c_double, _D, _D, _D]),
+    "ace_pred_marginal_dev": (ctypes.c_int, [_vp, _I64, _I64, _D, _D, ctypes.c_double,
+                                             ctypes.c_double, _vp, _vp, _vp, ctypes.c_double,
+                                             ctypes.c_double, ctypes.c_double, ctypes.c_int, _D,
+                                             _D, _D, _D]),
     "ace_nesterov": (ctypes.c_int, [_I64, ctypes.c_double, ctypes.c_double, _D, _D, _D]),
     "ace_nadam": (ctypes.c_int, [_I64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                  ctypes.c_double, ctypes.c_double, _D, _D, _D, _D]),
@@ -113,7 +136,12 @@ def lib():
                                "(there is no CPU fallback)")
             L = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
-                f = getattr(L, name)
+                # an older library built for an A/B run may lack newer entry
+                # points: they stay unbound (calling one raises AttributeError);
+                # tests/test_abi_cpu.py checks the in-tree library exports all
+                f = getattr(L, name, None)
+                if f is None:
+                    continue
                 f.restype = res
                 f.argtypes = args
             _lib = L

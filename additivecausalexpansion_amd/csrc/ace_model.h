@@ -1,6 +1,8 @@
 // ace_model.h -- the device-resident model shared by the C ABI (ace_api.cpp)
 // and the resident-inverse products / prediction (ace_predict.cpp).
 #pragma once
+#include <functional>
+
 #include "ace_common.h"
 #include "ace_internal.h"
 
@@ -97,3 +99,23 @@ struct ace_model {
   ShardModel *shard = nullptr;  // block-column-sharded model (ace_shard.cpp)
 };
 
+
+// Operands of the device prediction pipeline (pred_pipeline, ace_predict.cpp).
+struct PredOps {
+  ace_ctx *ctx = nullptr;
+  int64_t n = 0;            // training points
+  const double *w = nullptr;  // y - mu on the device (n)
+  // out (n x k, ld n) = A^-1 V^T for V = K_xX rows (k x n, ld ldv): this
+  // rank's share when sharded (summed by allreduce)
+  std::function<void(const double *V, int64_t ldv, int64_t k, double *out, DBuf &tmp)> symm;
+  std::function<void(double *buf, int64_t count)> allreduce;  // empty: single process
+  // K_xX rows c0 .. c0 + nc (marginal slice sum for predict_marginal): a
+  // device pointer with leading dimension *ld, possibly built in scratch
+  std::function<const double *(int64_t c0, int64_t nc, int64_t *ld, DBuf &scratch)> cross;
+  std::function<void(double *dst)> kdiag;  // diag(K_xx) (nx)
+  // K_xx (nx x nx) for the ATE / ATT / ATU forms; scratch holds nx * nx
+  std::function<const double *(int64_t *ld, DBuf &scratch)> kxx;
+};
+void pred_pipeline(const PredOps &op, int64_t nx, bool marginal, const double *Z_x, int ate,
+                   double sigma, double mu, double mean_y, double std_y, double std_Z,
+                   double *map, double *ci, double *var, double *avg);

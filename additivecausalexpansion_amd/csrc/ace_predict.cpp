@@ -69,33 +69,19 @@ void require_inverse(ace_model *m) {
   arg(m->ctx, m->has_inverse, "no resident inverse: call ace_model_para_update() first");
 }
 
-// Shared body of ace_model_predict (marginal = false) and
-// ace_model_predict_marginal (marginal = true).
-void predict_impl(ace_model *m, const double *theta, int64_t nx, const double *X2,
-                  const double *Zt, bool marginal, const double *Z_x, int ate, double mean_y,
-                  double std_y, double std_Z, double *map, double *ci, double *var, double *avg) {
-  ace_ctx *ctx = m->ctx;
+}  // namespace
+
+// The device prediction pipeline (pred_cpp / pred_marginal_cpp semantics)
+// over abstract operands -- the device model's resident inverse here, and the
+// device-matrix handles of the R6-faithful path in ace_dmat.cpp.
+void pred_pipeline(const PredOps &op, int64_t nx, bool marginal, const double *Z_x, int ate,
+                   double sigma, double mu, double mean_y, double std_y, double std_Z,
+                   double *map, double *ci, double *var, double *avg) {
+  ace_ctx *ctx = op.ctx;
   hipStream_t st = ctx->stream;
-  const Shape &s = m->s;
-  const int64_t n = m->n;
-  const int B = s.B;
-  const int b0 = marginal && B > 1 ? 1 : 0;  // src/pred_cpp.cpp:55-67
-  const int b1 = marginal ? (B > 1 ? B : 1) : B;
-  const double mu = theta[1];
-  // test side and theta tables (kernels at the caller's theta, Q6)
-  std::vector<double> tab = make_tab(theta, s, false);
-  DBuf dtab, dw, dKc, dT, dad, dkd, dtmp, dW3, dS3, dU3, dKmxx, dq3, dvt, ddot;
-  upload(ctx, dtab, tab.data(), tab.size(), "upload tables");
-  const TabView tv = tab_view(dtab, s);
-  SideBufs test;
-  upload_side(ctx, test, s, X2, Zt, nx, nx);
-  const PairSide train = m->shard ? shard_train_side(m->shard) : m->side.view(n);
-  // w = y - mu: a = tmp (y - mu) with tmp^T = T' below (src/pred_cpp.cpp:20, 70)
-  alloc(ctx, dw, (size_t)n * sizeof(double), "alloc w");
-  ck(ctx, launch_center(m->shard ? shard_train_y(m->shard) : m->y.d(), n, mu, dw.d(), st),
-     "center y");
+  const int64_t n = op.n;
+  DBuf dKc, dT, dad, dkd, dtmp, dW3, dS3, dU3, dKmxx, dq3, dvt, ddot;
   const int64_t chunk = std::min<int64_t>(NXC, nx);
-  alloc(ctx, dKc, (size_t)(chunk * n) * sizeof(double), "alloc K_xX");
   alloc(ctx, dT, (size_t)(chunk * n) * sizeof(double), "alloc T");
   alloc(ctx, dad, (size_t)(2 * nx) * sizeof(double), "alloc sums");  // [a | d]
   alloc(ctx, dkd, (size_t)nx * sizeof(double), "alloc diag");
@@ -117,61 +103,113 @@ void predict_impl(ace_model *m, const double *theta, int64_t nx, const double *X
   }
   for (int64_t c0 = 0; c0 < nx; c0 += chunk) {
     const int64_t nc = std::min<int64_t>(chunk, nx - c0);
-    PairSide tc = test.view(nc);
-    tc.X += c0 * s.PM;
-    tc.Z += c0 * s.ZS;
-    tc.LZ += c0 * s.ZS;
-    // K_xX rows c0 .. c0 + nc (kernmat_*_cpp(X2, X, Z2, Z): test side first)
-    ck(ctx, launch_assembly(2, s.kind, s.PM, tc, train, 0, B, s.ZS, tv, 0.0, dKc.d(), nc, nullptr,
-                            st, nullptr, 0, 1, 0, b0, b1),
-       "cross assembly");
+    int64_t ldk = 0;
+    const double *Kc = op.cross(c0, nc, &ldk, dKc);  // K_xX rows c0 .. c0 + nc
     // T' = A^-1 K_xX^T (n x nc): the transpose of tmp = K_xX invK_XX
-    symm_resident(m, dKc.d(), nc, true, nc, dT.d(), dtmp);
-    ck(ctx, launch_pred_cols(dT.d(), n, dKc.d(), nc, n, nc, dw.d(), dad.d() + c0, dad.d() + nx + c0,
-                             st),
+    op.symm(Kc, ldk, nc, dT.d(), dtmp);
+    ck(ctx, launch_pred_cols(dT.d(), n, Kc, ldk, n, nc, op.w, dad.d() + c0, dad.d() + nx + c0, st),
        "pred sums");
     if (ate)
       for (int j = 0; j < 3; ++j) {
         const double *wj = dW3.d() + j * nx + c0;
         // s_j += K_xX^T w_j, u_j += T' w_j = A^-1 K_xX^T w_j
-        ck(ctx, launch_gemv_t(dKc.d(), nc, nc, n, wj, dvt.d(), st), "gemv_t");
+        ck(ctx, launch_gemv_t(Kc, ldk, nc, n, wj, dvt.d(), st), "gemv_t");
         ck(ctx, launch_add(dvt.d(), dS3.d() + j * n, n, st), "add");
         ck(ctx, launch_gemv(dT.d(), n, n, nc, wj, dvt.d(), st), "gemv");
         ck(ctx, launch_add(dvt.d(), dU3.d() + j * n, n, st), "add");
       }
   }
-  ck(ctx, launch_kdiag(s.kind, test.view(nx), s.ZS, tv, b0, b1, dkd.d(), st), "kernel diagonal");
+  op.kdiag(dkd.d());
   std::vector<double> q3(3, 0.0), dots(3, 0.0);
   if (ate) {
-    // w_j^T Km_xx w_j with the full marginal test kernel (kernmat_*_symmetric_cpp(X2, dZ2))
-    alloc(ctx, dKmxx, (size_t)(nx * nx) * sizeof(double), "alloc K_xx");
-    ck(ctx, launch_assembly(1, s.kind, s.PM, test.view(nx), test.view(nx), 0, B, s.ZS, tv, 0.0,
-                            dKmxx.d(), nx, nullptr, st, nullptr, 0, 1, 0, b0, b1),
-       "symmetric assembly");
+    // w_j^T Km_xx w_j with the full marginal test kernel
+    int64_t ldx = 0;
+    const double *Kxx = op.kxx(&ldx, dKmxx);
     alloc(ctx, dq3, (size_t)(3 * nx + 3) * sizeof(double), "alloc quad");
-    ck(ctx, launch_quad3(dKmxx.d(), nx, nx, dW3.d(), dq3.d(), st), "quad3");
+    ck(ctx, launch_quad3(Kxx, ldx, nx, dW3.d(), dq3.d(), st), "quad3");
     // s_j . u_j  (the rank's share of s_j^T A^-1 s_j)
     alloc(ctx, ddot, 3 * sizeof(double), "alloc dots");
     for (int j = 0; j < 3; ++j)
       ck(ctx, launch_gemv_t(dS3.d() + j * n, n, n, 1, dU3.d() + j * n, ddot.d() + j, st), "dot");
-    if (m->shard) shard_allreduce_sum(m->shard, ddot.d(), 3);
+    if (op.allreduce) op.allreduce(ddot.d(), 3);
     download(ctx, q3.data(), dq3.d(), 3, "download quad");
     download(ctx, dots.data(), ddot.d(), 3, "download dots");
   }
-  if (m->shard) shard_allreduce_sum(m->shard, dad.d(), 2 * nx);
+  if (op.allreduce) op.allreduce(dad.d(), 2 * nx);
   std::vector<double> ad((size_t)(2 * nx)), kd((size_t)nx);
   download(ctx, ad.data(), dad.d(), ad.size(), "download sums");
   download(ctx, kd.data(), dkd.d(), kd.size(), "download diag");
   sync(ctx);
   if (!marginal) {
-    finish_pred(nx, ad.data(), kd.data(), ad.data() + nx, theta[0], mu, mean_y, std_y, map, ci,
-                var);
+    finish_pred(nx, ad.data(), kd.data(), ad.data() + nx, sigma, mu, mean_y, std_y, map, ci, var);
     return;
   }
   std::vector<double> post(3);
   for (int j = 0; j < 3; ++j) post[(size_t)j] = q3[(size_t)j] - dots[(size_t)j];
   finish_marginal(nx, ad.data(), kd.data(), ad.data() + nx, std_y, std_Z,
                   ate ? zx.data() : nullptr, ate ? post.data() : nullptr, map, ci, var, avg);
+}
+
+namespace {
+
+// ace_model_predict (marginal = false) / ace_model_predict_marginal: the
+// model's resident inverse, K_xX assembled from the resident training side.
+void predict_impl(ace_model *m, const double *theta, int64_t nx, const double *X2,
+                  const double *Zt, bool marginal, const double *Z_x, int ate, double mean_y,
+                  double std_y, double std_Z, double *map, double *ci, double *var, double *avg) {
+  ace_ctx *ctx = m->ctx;
+  hipStream_t st = ctx->stream;
+  const Shape &s = m->s;
+  const int64_t n = m->n;
+  const int B = s.B;
+  const int b0 = marginal && B > 1 ? 1 : 0;  // src/pred_cpp.cpp:55-67
+  const int b1 = marginal ? (B > 1 ? B : 1) : B;
+  const double mu = theta[1];
+  // kernels at the caller's theta (Q6)
+  std::vector<double> tab = make_tab(theta, s, false);
+  DBuf dtab, dw;
+  upload(ctx, dtab, tab.data(), tab.size(), "upload tables");
+  const TabView tv = tab_view(dtab, s);
+  SideBufs test;
+  upload_side(ctx, test, s, X2, Zt, nx, nx);
+  const PairSide train = m->shard ? shard_train_side(m->shard) : m->side.view(n);
+  // w = y - mu: a = tmp (y - mu) with tmp^T = T' (src/pred_cpp.cpp:20, 70)
+  alloc(ctx, dw, (size_t)n * sizeof(double), "alloc w");
+  ck(ctx, launch_center(m->shard ? shard_train_y(m->shard) : m->y.d(), n, mu, dw.d(), st),
+     "center y");
+  PredOps op;
+  op.ctx = ctx;
+  op.n = n;
+  op.w = dw.d();
+  op.symm = [&](const double *V, int64_t ldv, int64_t k, double *out, DBuf &tmp) {
+    symm_resident(m, V, ldv, true, k, out, tmp);
+  };
+  if (m->shard) op.allreduce = [&](double *b, int64_t c) { shard_allreduce_sum(m->shard, b, c); };
+  op.cross = [&](int64_t c0, int64_t nc, int64_t *ld, DBuf &scratch) -> const double * {
+    alloc(ctx, scratch, (size_t)(nc * n) * sizeof(double), "alloc K_xX");
+    PairSide tc = test.view(nc);
+    tc.X += c0 * s.PM;
+    tc.Z += c0 * s.ZS;
+    tc.LZ += c0 * s.ZS;
+    // kernmat_*_cpp(X2, X, Z2, Z): test side first
+    ck(ctx, launch_assembly(2, s.kind, s.PM, tc, train, 0, B, s.ZS, tv, 0.0, scratch.d(), nc,
+                            nullptr, st, nullptr, 0, 1, 0, b0, b1),
+       "cross assembly");
+    *ld = nc;
+    return scratch.d();
+  };
+  op.kdiag = [&](double *dst) {
+    ck(ctx, launch_kdiag(s.kind, test.view(nx), s.ZS, tv, b0, b1, dst, st), "kernel diagonal");
+  };
+  op.kxx = [&](int64_t *ld, DBuf &scratch) -> const double * {
+    alloc(ctx, scratch, (size_t)(nx * nx) * sizeof(double), "alloc K_xx");
+    ck(ctx, launch_assembly(1, s.kind, s.PM, test.view(nx), test.view(nx), 0, B, s.ZS, tv, 0.0,
+                            scratch.d(), nx, nullptr, st, nullptr, 0, 1, 0, b0, b1),
+       "symmetric assembly");
+    *ld = nx;
+    return scratch.d();
+  };
+  pred_pipeline(op, nx, marginal, Z_x, ate, theta[0], mu, mean_y, std_y, std_Z, map, ci, var, avg);
 }
 
 }  // namespace

@@ -19,6 +19,70 @@ def _ctx(ctx):
     return (ctx or default_context()).handle
 
 
+# ---------------------------------------------------------------- device handles
+class DMat:
+    """An ace_dmat handle: a device-resident matrix / cube, or a virtual
+    `elements` cube (X, Z, theta recorded; values assembled only if read).
+    What the R shim wraps in an ALTREP vector: reading it (np.asarray, or
+    any numpy use) materialises it, passing it back to a *_cpp routine does
+    not (include/ace_hip.h "device-matrix handles")."""
+
+    def __init__(self, handle, ctx):
+        self.handle, self.ctx = handle, ctx
+        r, c, sl = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(lib().ace_dmat_dims(handle, ctypes.byref(r), ctypes.byref(c), ctypes.byref(sl)))
+        self.shape = (r.value, c.value) if sl.value == 1 else (r.value, c.value, sl.value)
+
+    @classmethod
+    def upload(cls, a, ctx=None):
+        a = np.asarray(a, dtype=np.float64)
+        dims = a.shape + (1,) * (3 - a.ndim)
+        af = np.asfortranarray(a)
+        h = ctypes.c_void_p()
+        check(lib().ace_dmat_upload(_ctx(ctx), dims[0], dims[1], dims[2], ptr(af),
+                                    ctypes.byref(h)), _ctx(ctx))
+        return cls(h, _ctx(ctx))
+
+    def read(self):
+        out = np.empty(self.shape, order="F")
+        check(lib().ace_dmat_read(self.handle, 0, out.size, ptr(out)), self.ctx)
+        return out
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.read()
+        return a if dtype is None else a.astype(dtype)
+
+    @property
+    def on_device(self):
+        return bool(lib().ace_dmat_materialized(self.handle) & 1)
+
+    @property
+    def read_to_host(self):
+        return bool(lib().ace_dmat_materialized(self.handle) & 2)
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                lib().ace_dmat_free(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+def _dmat(a, ctx, keep):
+    """A handle for a matrix argument: DMat as is, a host array uploaded (the
+    R shim does the same for a plain R matrix); `keep` holds temporaries."""
+    if isinstance(a, DMat):
+        return a.handle
+    d = DMat.upload(a, ctx)
+    keep.append(d)
+    return d.handle
+
+
+def _any_dev(*xs):
+    return any(isinstance(x, DMat) for x in xs)
+
+
 def _zmat(Z, n):
     Z = np.asarray(Z, dtype=np.float64)
     if Z.ndim == 1:
@@ -40,7 +104,7 @@ def _check_theta(theta, B, p, grad=False):
 
 
 # ---------------------------------------------------------------- kernels
-def _kernmat_cross(kind, X1, X2, Z1, Z2, parameters, ctx=None, elements=True):
+def _kernmat_cross(kind, X1, X2, Z1, Z2, parameters, ctx=None, elements=True, device=False):
     X1 = fmat(X1)
     X2 = fmat(X2)
     n1, n2, p = X1.shape[0], X2.shape[0], X2.shape[1]
@@ -49,6 +113,12 @@ def _kernmat_cross(kind, X1, X2, Z1, Z2, parameters, ctx=None, elements=True):
     B = Z1.shape[1] + 1
     th = _theta(parameters)
     _check_theta(th, B, p)
+    if device:
+        hf, he = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().ace_kernmat_cross_dev(_ctx(ctx), kind, n1, n2, p, B, ptr(X1), ptr(X2), ptr(Z1),
+                                          ptr(Z2), ptr(th), ctypes.byref(hf), ctypes.byref(he)),
+              _ctx(ctx))
+        return {"full": DMat(hf, _ctx(ctx)), "elements": DMat(he, _ctx(ctx))}
     full = np.empty((n1, n2), order="F")
     el = np.empty((n1, n2, B), order="F") if elements else None
     check(lib().ace_kernmat_cross(_ctx(ctx), kind, n1, n2, p, B, ptr(X1), ptr(X2), ptr(Z1),
@@ -56,13 +126,18 @@ def _kernmat_cross(kind, X1, X2, Z1, Z2, parameters, ctx=None, elements=True):
     return {"full": full, "elements": el}
 
 
-def _kernmat_sym(kind, X, Z, parameters, ctx=None, elements=True):
+def _kernmat_sym(kind, X, Z, parameters, ctx=None, elements=True, device=False):
     X = fmat(X)
     n, p = X.shape
     Z = _zmat(Z, n)
     B = Z.shape[1] + 1
     th = _theta(parameters)
     _check_theta(th, B, p)
+    if device:
+        hf, he = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().ace_kernmat_sym_dev(_ctx(ctx), kind, n, p, B, ptr(X), ptr(Z), ptr(th),
+                                        ctypes.byref(hf), ctypes.byref(he)), _ctx(ctx))
+        return {"full": DMat(hf, _ctx(ctx)), "elements": DMat(he, _ctx(ctx))}
     full = np.empty((n, n), order="F")
     el = np.empty((n, n, B), order="F") if elements else None
     check(lib().ace_kernmat_sym(_ctx(ctx), kind, n, p, B, ptr(X), ptr(Z), ptr(th), ptr(full),
@@ -70,29 +145,37 @@ def _kernmat_sym(kind, X, Z, parameters, ctx=None, elements=True):
     return {"full": full, "elements": el}
 
 
-def kernmat_SE_cpp(X1, X2, Z1, Z2, parameters, ctx=None):
+def kernmat_SE_cpp(X1, X2, Z1, Z2, parameters, ctx=None, device=False):
     """src/kernel_SE_cpp.cpp:9-64"""
-    return _kernmat_cross(KIND["SE"], X1, X2, Z1, Z2, parameters, ctx)
+    return _kernmat_cross(KIND["SE"], X1, X2, Z1, Z2, parameters, ctx, device=device)
 
 
-def kernmat_SE_symmetric_cpp(X, Z, parameters, ctx=None):
+def kernmat_SE_symmetric_cpp(X, Z, parameters, ctx=None, device=False):
     """src/kernel_SE_cpp.cpp:67-134"""
-    return _kernmat_sym(KIND["SE"], X, Z, parameters, ctx)
+    return _kernmat_sym(KIND["SE"], X, Z, parameters, ctx, device=device)
 
 
-def kernmat_Matern32_cpp(X1, X2, Z1, Z2, parameters, ctx=None):
+def kernmat_Matern32_cpp(X1, X2, Z1, Z2, parameters, ctx=None, device=False):
     """src/kernel_Matern_cpp.cpp:52-93"""
-    return _kernmat_cross(KIND["Matern32"], X1, X2, Z1, Z2, parameters, ctx)
+    return _kernmat_cross(KIND["Matern32"], X1, X2, Z1, Z2, parameters, ctx, device=device)
 
 
-def kernmat_Matern32_symmetric_cpp(X, Z, parameters, ctx=None):
+def kernmat_Matern32_symmetric_cpp(X, Z, parameters, ctx=None, device=False):
     """src/kernel_Matern_cpp.cpp:190-240"""
-    return _kernmat_sym(KIND["Matern32"], X, Z, parameters, ctx)
+    return _kernmat_sym(KIND["Matern32"], X, Z, parameters, ctx, device=device)
 
 
 def invkernel_cpp(pdmat, sigma, ctx=None):
     """src/kernel_SE_cpp.cpp:137-157.  `eigenval` holds the elimination
     pivots (sum(log(.)) == log det, the only use the reference makes of it)."""
+    sig = float(np.ravel([sigma])[0])
+    if _any_dev(pdmat):  # handle in, handle out: the inverse stays in HBM
+        n = pdmat.shape[0]
+        ev = np.empty(n)
+        h = ctypes.c_void_p()
+        check(lib().ace_invkernel_dev(_ctx(ctx), pdmat.handle, sig, ptr(ev), ctypes.byref(h)),
+              _ctx(ctx))
+        return {"eigenval": ev, "inv": DMat(h, _ctx(ctx))}
     K = fmat(pdmat)
     n = K.shape[0]
     if K.shape != (n, n):
@@ -113,16 +196,25 @@ def _grad(kind, y, X, Z, Kfull, K, invKmatn, eigenval, parameters, stats, B, std
     yv = np.ascontiguousarray(np.ravel(y), dtype=np.float64)
     th = _theta(parameters)
     _check_theta(th, B, p, grad=True)
-    Kf = fmat(Kfull)
-    Kc = fmat(K) if K is not None else None
-    inv = fmat(invKmatn)
+    dev = _any_dev(Kfull, K, invKmatn)
+    Kf = fmat(Kfull) if not dev else None
+    Kc = fmat(K) if (K is not None and not dev) else None
+    inv = fmat(invKmatn) if not dev else None
     ev = np.ascontiguousarray(np.ravel(eigenval), dtype=np.float64)
     if not (isinstance(stats, np.ndarray) and stats.dtype == np.float64 and stats.size >= 2):
         raise AceError("stats must be a float64 numpy array of length 2 (mutated in place)")
     st = np.ascontiguousarray(stats)
     g = np.empty(th.shape[0])
-    check(lib().ace_grad(_ctx(ctx), kind, n, p, B, ptr(yv), ptr(X), ptr(Z), ptr(Kf), ptr(Kc),
-                         ptr(inv), ptr(ev), ptr(th), ptr(st), float(std_y), ptr(g)), _ctx(ctx))
+    if dev:
+        keep = []
+        hK = _dmat(Kfull, ctx, keep)
+        hC = _dmat(K, ctx, keep) if K is not None else None
+        hI = _dmat(invKmatn, ctx, keep)
+        check(lib().ace_grad_dev(_ctx(ctx), kind, n, p, B, ptr(yv), ptr(X), ptr(Z), hK, hC, hI,
+                                 ptr(ev), ptr(th), ptr(st), float(std_y), ptr(g)), _ctx(ctx))
+    else:
+        check(lib().ace_grad(_ctx(ctx), kind, n, p, B, ptr(yv), ptr(X), ptr(Z), ptr(Kf), ptr(Kc),
+                             ptr(inv), ptr(ev), ptr(th), ptr(st), float(std_y), ptr(g)), _ctx(ctx))
     stats.flat[0:2] = st.flat[0:2]
     return g
 
@@ -145,6 +237,13 @@ def stats_cpp(y, Kmat, invKmatn, eigenval, mu, std_y=1.0, ctx=None):
     yv = np.ascontiguousarray(np.ravel(y), dtype=np.float64)
     n = yv.shape[0]
     out = np.empty(2)
+    if _any_dev(Kmat, invKmatn):
+        keep = []
+        check(lib().ace_stats_dev(_ctx(ctx), n, ptr(yv), _dmat(Kmat, ctx, keep),
+                                  _dmat(invKmatn, ctx, keep),
+                                  ptr(np.ascontiguousarray(np.ravel(eigenval), dtype=np.float64)),
+                                  float(np.ravel([mu])[0]), float(std_y), ptr(out)), _ctx(ctx))
+        return out
     check(lib().ace_stats(_ctx(ctx), n, ptr(yv), ptr(fmat(Kmat)), ptr(fmat(invKmatn)),
                           ptr(np.ascontiguousarray(np.ravel(eigenval), dtype=np.float64)),
                           float(np.ravel([mu])[0]), float(std_y), ptr(out)), _ctx(ctx))
@@ -155,6 +254,11 @@ def mu_solution_cpp(y, invKmat, ctx=None):
     """src/utilities_cpp.cpp:6-10"""
     yv = np.ascontiguousarray(np.ravel(y), dtype=np.float64)
     out = ctypes.c_double()
+    if _any_dev(invKmat):
+        check(lib().ace_mu_solution_dev(_ctx(ctx), yv.shape[0], ptr(yv), invKmat.handle,
+                                        ctypes.cast(ctypes.pointer(out),
+                                                    ctypes.POINTER(ctypes.c_double))), _ctx(ctx))
+        return out.value
     check(lib().ace_mu_solution(_ctx(ctx), yv.shape[0], ptr(yv), ptr(fmat(invKmat)),
                                 ctypes.cast(ctypes.pointer(out), ctypes.POINTER(ctypes.c_double))),
           _ctx(ctx))
@@ -164,6 +268,16 @@ def mu_solution_cpp(y, invKmat, ctx=None):
 def pred_cpp(y_X, sigma, mu, invK_XX, K_xX, K_xx, mean_y, std_y, ctx=None):
     """src/pred_cpp.cpp:8-34"""
     yv = np.ascontiguousarray(np.ravel(y_X), dtype=np.float64)
+    if _any_dev(invK_XX, K_xX, K_xx):
+        keep = []
+        nx, nX = K_xX.shape if isinstance(K_xX, DMat) else np.shape(K_xX)
+        mp, var = np.empty(nx), np.empty(nx)
+        ci = np.empty((nx, 2), order="F")
+        check(lib().ace_pred_dev(_ctx(ctx), nX, nx, ptr(yv), float(sigma), float(mu),
+                                 _dmat(invK_XX, ctx, keep), _dmat(K_xX, ctx, keep),
+                                 _dmat(K_xx, ctx, keep), float(mean_y), float(std_y), ptr(mp),
+                                 ptr(ci), ptr(var)), _ctx(ctx))
+        return {"map": mp, "ci": ci, "var": var}
     KxX = fmat(K_xX)
     nx, nX = KxX.shape
     mp = np.empty(nx)
@@ -179,19 +293,31 @@ def pred_marginal_cpp(y_X, Z_x, sigma, mu, invK_XX, K_xX, K_xx, mean_y, std_y, s
                       calculate_ate, ctx=None):
     """src/pred_cpp.cpp:37-126"""
     yv = np.ascontiguousarray(np.ravel(y_X), dtype=np.float64)
-    cX = fmat(K_xX)
-    cx = fmat(K_xx)
-    nx, nX, B = cX.shape
     zx = np.ascontiguousarray(np.ravel(Z_x), dtype=np.float64) if Z_x is not None else None
-    mp = np.empty(nx)
-    ci = np.empty((nx, 2), order="F")
-    var = np.empty(nx)
     avg = np.empty(12)
-    check(lib().ace_pred_marginal(_ctx(ctx), nX, nx, B, ptr(yv), ptr(zx), float(sigma),
-                                  float(mu), ptr(fmat(invK_XX)), ptr(cX), ptr(cx),
-                                  float(mean_y), float(std_y), float(np.ravel([std_Z])[0]),
-                                  1 if calculate_ate else 0, ptr(mp), ptr(ci), ptr(var),
-                                  ptr(avg)), _ctx(ctx))
+    if _any_dev(invK_XX, K_xX, K_xx):
+        keep = []
+        nx, nX = (K_xX.shape if isinstance(K_xX, DMat) else np.shape(K_xX))[:2]
+        mp, var = np.empty(nx), np.empty(nx)
+        ci = np.empty((nx, 2), order="F")
+        check(lib().ace_pred_marginal_dev(_ctx(ctx), nX, nx, ptr(yv), ptr(zx), float(sigma),
+                                          float(mu), _dmat(invK_XX, ctx, keep),
+                                          _dmat(K_xX, ctx, keep), _dmat(K_xx, ctx, keep),
+                                          float(mean_y), float(std_y),
+                                          float(np.ravel([std_Z])[0]), 1 if calculate_ate else 0,
+                                          ptr(mp), ptr(ci), ptr(var), ptr(avg)), _ctx(ctx))
+    else:
+        cX = fmat(K_xX)
+        cx = fmat(K_xx)
+        nx, nX, B = cX.shape
+        mp = np.empty(nx)
+        ci = np.empty((nx, 2), order="F")
+        var = np.empty(nx)
+        check(lib().ace_pred_marginal(_ctx(ctx), nX, nx, B, ptr(yv), ptr(zx), float(sigma),
+                                      float(mu), ptr(fmat(invK_XX)), ptr(cX), ptr(cx),
+                                      float(mean_y), float(std_y), float(np.ravel([std_Z])[0]),
+                                      1 if calculate_ate else 0, ptr(mp), ptr(ci), ptr(var),
+                                      ptr(avg)), _ctx(ctx))
     out = {"map": mp, "ci": ci, "var": var}
     if calculate_ate:
         for j, key in enumerate(("ate", "att", "atu")):

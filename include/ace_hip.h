@@ -135,6 +135,60 @@ int ace_pred_marginal(ace_ctx *ctx, int64_t nX, int64_t nx, int B,
                       double std_Z, int calculate_ate, double *map, double *ci,
                       double *var, double *avg);
 
+/* ------------------------------- device-matrix handles (unchanged R6 flow)
+ *
+ * The R6 kernel classes keep Kmat, Karray and invKmatn as R objects and
+ * pass them between the routines above on every para_update
+ * (R/kernel_SE_R6.R:26-50; predict: :75-97).  The *_dev variants keep
+ * those objects in HBM as ace_dmat handles; the R shim wraps a handle in an
+ * ALTREP double vector that is materialised only when R reads its values
+ * (INTEGRATION.md), so the unchanged R6 code moves no n x n matrix and no
+ * n x n x B cube.  Semantics, argument order and outputs are those of the
+ * host-buffer routine of the same name.
+ *   kernmat_*_dev: *full is a device n1 x n2 matrix; *elements (optional) is
+ *     VIRTUAL: X, Z and theta are recorded and slices (or pred_marginal's
+ *     slice sums) are assembled only when read or consumed.
+ *   invkernel_dev: *inv is the sweep's device result (never symmetrised or
+ *     copied unless read); eigenval (n, host) receives the pivots.
+ *   grad_dev / stats_dev: RMSE from the explicit residual ybar - Kfull alpha
+ *     (src/kernel_SE_cpp.cpp:238), like the host-buffer routines.
+ * Handles belong to the context that made them; ace_dmat_free releases one. */
+typedef struct ace_dmat ace_dmat;
+int ace_dmat_upload(ace_ctx *ctx, int64_t rows, int64_t cols, int64_t slices,
+                    const double *host, ace_dmat **out);
+int ace_dmat_dims(const ace_dmat *h, int64_t *rows, int64_t *cols, int64_t *slices);
+/* count doubles from column-major linear index offset (materialises a
+ * virtual cube / the symmetric inverse on the device on first read) */
+int ace_dmat_read(const ace_dmat *h, int64_t offset, int64_t count, double *out);
+/* bit 0: full values exist on the device; bit 1: values were read to the host */
+int ace_dmat_materialized(const ace_dmat *h);
+void ace_dmat_free(ace_dmat *h);
+int ace_kernmat_sym_dev(ace_ctx *ctx, int kind, int64_t n, int p, int B, const double *X,
+                        const double *Z, const double *theta, ace_dmat **full,
+                        ace_dmat **elements);
+int ace_kernmat_cross_dev(ace_ctx *ctx, int kind, int64_t n1, int64_t n2, int p, int B,
+                          const double *X1, const double *X2, const double *Z1, const double *Z2,
+                          const double *theta, ace_dmat **full, ace_dmat **elements);
+int ace_invkernel_dev(ace_ctx *ctx, const ace_dmat *K, double sigma, double *eigenval,
+                      ace_dmat **inv);
+int ace_mu_solution_dev(ace_ctx *ctx, int64_t n, const double *y, const ace_dmat *inv,
+                        double *out);
+int ace_stats_dev(ace_ctx *ctx, int64_t n, const double *y, const ace_dmat *Kmat,
+                  const ace_dmat *inv, const double *eigenval, double mu, double std_y,
+                  double *out);
+int ace_grad_dev(ace_ctx *ctx, int kind, int64_t n, int p, int B, const double *y,
+                 const double *X, const double *Z, const ace_dmat *Kfull, const ace_dmat *Kel,
+                 const ace_dmat *inv, const double *eigenval, const double *theta, double *stats,
+                 double std_y, double *grad);
+int ace_pred_dev(ace_ctx *ctx, int64_t nX, int64_t nx, const double *y_X, double sigma, double mu,
+                 const ace_dmat *invK_XX, const ace_dmat *K_xX, const ace_dmat *K_xx,
+                 double mean_y, double std_y, double *map, double *ci, double *var);
+int ace_pred_marginal_dev(ace_ctx *ctx, int64_t nX, int64_t nx, const double *y_X,
+                          const double *Z_x, double sigma, double mu, const ace_dmat *invK_XX,
+                          const ace_dmat *K_xX, const ace_dmat *K_xx, double mean_y, double std_y,
+                          double std_Z, int calculate_ate, double *map, double *ci, double *var,
+                          double *avg);
+
 /* ---------------------------------------------- host-only (no GPU, no ctx) */
 
 /* Nesterov_cpp / Nadam_cpp / Adam_cpp (src/optimizer_cpp.cpp:8-63).  All

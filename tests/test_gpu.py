@@ -232,8 +232,8 @@ def test_model_para_update_matches_oracle(A, O, kernel, n, p, B):
     oracle's kernmat_sym -> invkernel -> grad chain, at iter 1 (mu first) and 2.
     Every case runs the MFMA-expansion pair kernels (both gradient workgroup
     shapes, diagonal and strictly lower tiles, per-slice and double-buffered
-    partials) except (200, 50, 32): its per-tile staging exceeds the LDS
-    budget and takes the all-VALU fallback."""
+    partials); (200, 50, 32) is the largest per-tile LDS staging (PM = 64,
+    B = 32: above 64 KB, one workgroup per CU)."""
     from additivecausalexpansion_amd.synthetic import make_problem
     y, X, Z, th, sy = make_problem(n, p, B, seed=7)
     m = A.DeviceModel(kernel, n, p, B)

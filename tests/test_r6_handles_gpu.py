@@ -1,0 +1,142 @@
+"""The unchanged R6 call sequence over device handles (ace_dmat, the objects
+the R shim wraps in ALTREP vectors): additivecausalexpansion_amd.r6 mirrors
+R/kernel_SE_R6.R / R/kernel_Matern32_R6.R line by line and calls the
+.Call surface exactly as the R code does -- kernmat_*_symmetric_cpp ->
+invkernel_cpp -> mu_solution_cpp -> grad_*_cpp -> Optim$update ->
+mu_solution_cpp, predict via kernmat + pred_cpp / pred_marginal_cpp.
+
+Checked against the oracle's golden README trajectory (tests/golden/traj_*),
+with the `elements` cube never built and no matrix read back to the host.
+Tolerances as tests/test_gpu.py::test_training_trajectory_matches_golden.
+"""
+import numpy as np
+import pytest
+from conftest import golden
+from test_gpu import close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def A():
+    import additivecausalexpansion_amd as pkg
+    pkg.default_context()
+    return pkg
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import ace_oracle
+    return ace_oracle
+
+
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+def test_r6_sequence_on_handles_matches_golden_trajectory(A, kernel):
+    from additivecausalexpansion_amd.r6 import R6KernelMatern32, R6KernelSE
+    d = golden(f"traj_{kernel}")
+    y, X, Bm = d["y"], np.asfortranarray(d["X"]), np.asfortranarray(d["basis"])
+    B = Bm.shape[1] + 1
+    sy, my = float(d["moments"][0, 1]), float(d["moments"][0, 0])
+    Kc = R6KernelSE if kernel == "SE" else R6KernelMatern32
+    k = Kc(2, B, d["theta0"], sy)
+    opt = A.set_optimizer("Nadam", k, 0.01, 0.0, 0.9, 0.999, True, 1.0)
+    for it in range(1, 21):
+        st = k.para_update(it, y, X, Bm, opt, verbose=False)
+        close(st, d["stats"][it - 1], 1e-6, 1e-9)
+        close(k.parameters, d["thetas"][it - 1], 1e-5, 1e-9)
+        # the R6 fields are device handles; the cube was never assembled and
+        # nothing was read back
+        assert isinstance(k.Karray, A.DMat) and not k.Karray.on_device
+        for h in (k.Kmat, k.Karray, k.invKmatn):
+            assert not h.read_to_host
+    # prediction with the golden theta_{T-1} inverse and theta_T kernels (Q6)
+    k.parameters = d["thetas"][18].copy()
+    k.para_update(20, y, X, Bm, A.set_optimizer("GD", k, 0.0, 0.0, 0.9, 0.999, False, 1.0),
+                  verbose=False)
+    k.parameters = d["thetas"][19].copy()
+    pr = k.predict(y, X, Bm, X, Bm, my, sy)
+    close(pr["map"], d["pred_map"], 1e-6, 1e-9)
+    sym = A.kernmat_SE_symmetric_cpp if kernel == "SE" else A.kernmat_Matern32_symmetric_cpp
+    kxx = np.diag(sym(X, Bm, d["thetas"][19])["full"])
+    terms = sy ** 2 * (2 * np.abs(kxx) + abs(np.exp(d["thetas"][19][0])))
+    assert np.all(np.abs(pr["var"] - d["pred_var"]) <= 1e-6 * terms)
+    assert not k.invKmatn.read_to_host
+    st = k.get_train_stats(y, X, Bm)
+    assert np.all(np.isfinite(st))
+
+
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+def test_r6_handles_match_host_matrices(A, O, kernel):
+    """The same R6 sequence with host matrices (the plain ABI) and with
+    handles; and predict_marginal with virtual cubes against the oracle."""
+    from additivecausalexpansion_amd.r6 import R6KernelMatern32, R6KernelSE
+    from additivecausalexpansion_amd.synthetic import make_problem
+    n, p, B = 420, 3, 5
+    y, X, Z, th, sy = make_problem(n, p, B, seed=31)
+    Kc = R6KernelSE if kernel == "SE" else R6KernelMatern32
+    runs = {}
+    for handles in (False, True):
+        k = Kc(p, B, th, sy, handles=handles)
+        opt = A.set_optimizer("Adam", k, 0.02, 0.0, 0.9, 0.999, True, 1.0)
+        sts = [k.para_update(it, y, X, Z, opt, verbose=False) for it in (1, 2, 3)]
+        runs[handles] = (np.array(sts), k.parameters.copy(), k)
+    # the two paths round differently (lower-stored vs symmetrised inverse);
+    # Adam divides by sqrt(v), so last-bit differences in small gradient
+    # components grow along the loop (see the golden trajectory test)
+    close(runs[True][0], runs[False][0], 1e-8, 1e-10)
+    close(runs[True][1], runs[False][1], 1e-7, 1e-10)
+    k = runs[True][2]
+    # predict_marginal over virtual cubes: the marginal slice sums are
+    # assembled directly, never the n2 x n x B cube
+    nx = 90
+    _, X2, Z2, _, _ = make_problem(nx, p, B, seed=32)
+    dZ2 = np.asfortranarray(Z2 * 0.5)
+    zx = (np.arange(nx) % 4 == 0).astype(float)
+    got = k.predict_marginal(y, X, Z, X2, zx, dZ2, 0.2, 1.1, 0.7, True)
+    kh = runs[False][2]  # the same state with host matrices (the plain ABI)
+    ref = kh.predict_marginal(y, X, Z, X2, zx, dZ2, 0.2, 1.1, 0.7, True)
+    close(got["map"], ref["map"], 1e-8, 1e-10)
+    close(got["var"], ref["var"], 1e-7, 1e-10)
+    for key in ("ate", "att", "atu"):
+        close(got[key]["map"], ref[key]["map"], 1e-8, 1e-12)
+
+
+def test_dmat_handles_read_and_mix(A, O):
+    """Reading a handle materialises it (virtual cube included) and equals the
+    oracle; handles and host arrays mix in one call (the shim uploads a plain
+    R matrix to a temporary handle)."""
+    from additivecausalexpansion_amd.synthetic import make_problem
+    n, p, B = 150, 2, 4
+    y, X, Z, th, sy = make_problem(n, p, B, seed=41)
+    ref = O.kernmat_Matern32_symmetric_cpp(X, Z, th)
+    Kl = A.kernmat_Matern32_symmetric_cpp(X, Z, th, device=True)
+    assert not Kl["elements"].on_device
+    close(np.asarray(Kl["full"]), ref["full"], 1e-12, 1e-12)
+    close(np.asarray(Kl["elements"]), ref["elements"], 1e-12, 1e-12)
+    assert Kl["elements"].on_device and Kl["elements"].read_to_host
+    lst = A.invkernel_cpp(Kl["full"], th[0])
+    iref = O.invkernel_cpp(ref["full"], th[0])
+    close(np.asarray(lst["inv"]), iref["inv"], 1e-9, 1e-9)
+    assert np.sum(np.log(lst["eigenval"])) == pytest.approx(np.sum(np.log(iref["eigenval"])),
+                                                            rel=1e-10)
+    st_h, st_r = np.zeros(2), np.zeros(2)
+    g_h = A.grad_Matern_cpp(y, X, Z, ref["full"], None, lst["inv"], lst["eigenval"], th, st_h, B,
+                            sy)
+    g_r = O.grad_Matern_cpp(y, X, Z, ref["full"], ref["elements"], iref["inv"],
+                            iref["eigenval"], th.copy(), st_r, B, sy)
+    close(g_h, g_r)
+    close(st_h, st_r)
+    assert A.mu_solution_cpp(y, lst["inv"]) == pytest.approx(
+        O.mu_solution_cpp(y, iref["inv"]), rel=1e-8)
+    close(A.stats_cpp(y, Kl["full"], lst["inv"], lst["eigenval"], 0.1, sy),
+          O.stats_cpp(y, ref["full"], iref["inv"], iref["eigenval"], 0.1, sy))
+    up = A.DMat.upload(ref["elements"])
+    assert up.shape == (n, n, B)
+    assert np.array_equal(np.asarray(up), ref["elements"])
+
+
+def test_dmat_not_positive_definite_gives_nan(A):
+    K = A.DMat.upload(-np.eye(10))
+    r = A.invkernel_cpp(K, -5.0)
+    assert np.all(np.isnan(np.asarray(r["inv"])))
+    assert np.any(r["eigenval"] <= 0)
