@@ -443,3 +443,24 @@ def test_update_tile_order_is_bitwise_neutral(A, tmp_path):
     assert np.array_equal(outs["0"], outs["4"]) and np.array_equal(outs["2"], outs["4"])
     mine = A.invkernel_cpp(K, th[0])["inv"]  # this process: default order
     assert np.array_equal(mine, outs["4"])
+
+
+def test_fused_chain_is_bitwise_neutral(A, tmp_path):
+    """The fused pivot-block chain (k_chain, ACE_CHAIN=1) performs the k_pivot
+    / k_panel arithmetic in the same order in one workgroup: the inverse is
+    bit-identical to the per-sub-block launches (the default)."""
+    import os
+    import subprocess
+    import sys
+    from additivecausalexpansion_amd.synthetic import make_problem
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = 1300
+    y, X, Z, th, _ = make_problem(n, 4, 5, seed=17)
+    K = A.kernmat_SE_symmetric_cpp(X, Z, th)["full"]
+    inp = str(tmp_path / "k.npz")
+    np.savez(inp, K=K, s=th[0])
+    out = str(tmp_path / "inv1.npy")
+    env = dict(os.environ, ACE_CHAIN="1")
+    subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
+                   env=env, check=True, timeout=100)
+    assert np.array_equal(A.invkernel_cpp(K, th[0])["inv"], np.load(out))
