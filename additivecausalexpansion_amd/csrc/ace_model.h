@@ -22,7 +22,7 @@ struct SweepWork {
     naug = npad + AUG;
     alloc(ctx, A, (size_t)(naug * naug) * sizeof(double), "alloc A");
     for (DBuf *b : {&P0, &P1, &W0, &W1}) alloc(ctx, *b, (size_t)(naug * NB) * sizeof(double), "alloc panel");
-    alloc(ctx, SW, (size_t)(SUB * SUB) * sizeof(double), "alloc SW");
+    alloc(ctx, SW, (size_t)SW_DOUBLES * sizeof(double), "alloc SW");
     alloc(ctx, S0, (size_t)(SUB * NB) * sizeof(double), "alloc S");
     alloc(ctx, S1, (size_t)(SUB * NB) * sizeof(double), "alloc S");
     alloc(ctx, piv, (size_t)npad * sizeof(double), "alloc piv");

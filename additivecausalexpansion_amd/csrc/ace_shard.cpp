@@ -351,7 +351,7 @@ ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int
       alloc(ctx, R->W[b], (size_t)(naug * NB) * sizeof(double), "alloc panel");
       alloc(ctx, R->S[b], (size_t)(SUB * NB) * sizeof(double), "alloc S");
     }
-    alloc(ctx, R->SW, (size_t)(SUB * SUB) * sizeof(double), "alloc SW");
+    alloc(ctx, R->SW, (size_t)SW_DOUBLES * sizeof(double), "alloc SW");
     alloc(ctx, R->piv, (size_t)npad * sizeof(double), "alloc piv");
     alloc(ctx, R->flag, 16, "alloc flag");
     alloc(ctx, R->low, (size_t)(naug * NB) * sizeof(double), "alloc exchange");

@@ -266,179 +266,114 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ W, int64_t l
   }
 }
 
-// ---------------------------------------------------------------- fused chain
-// The whole NB x NB pivot-block sweep of one panel in ONE workgroup: for each
-// of the NB / SUB sub-blocks s, the k_pivot sub-sweep (waves 0-3, register
-// resident; the other waves only join its barriers) followed by the k_panel
-// update of all NB pivot rows (every wave: 2 groups of 16 rows).  Same
-// arithmetic in the same order as the k_pivot / k_panel pair -- bit-identical
-// results -- but one launch per sweep step instead of 2 NB / SUB: the
-// latency-bound chain no longer waits for a free CU slot between its
-// sub-steps while the bulk update occupies the machine.
-// S0 holds sub-block 0's pivot rows (k_gather); S0 / S1 ping-pong the
-// snapshots (written by the waves owning sub-block s+1's rows, read by all
-// waves after the sub-step's closing barrier).
-constexpr int CH_THREADS = 512;  // 8 waves, <= 128 VGPRs: fits beside one update WG
-
-// Pivot sub-sweep of D_s (k_pivot's arithmetic) by all NW waves of the
-// chain workgroup, 64 / NW columns per wave (8 at 512 threads: half the
-// per-lane state of k_pivot's 16), into sSW.  Every element sees the same
-// operations in the same order as in k_pivot: bit-identical.
-template <int NW>
-__device__ __forceinline__ void chain_pivot(const double *__restrict__ S, int s, int64_t p0,
-                                            double *__restrict__ piv, int *__restrict__ flag,
-                                            double (*__restrict__ sSW)[PLD]) {
-  constexpr int CPW = SUB / NW;  // columns per wave
-  static_assert(CPW * NW == SUB && CPW % 2 == 0, "columns split evenly in pairs");
-  __shared__ __attribute__((aligned(16))) double colb[2][SUB];
-  __shared__ __attribute__((aligned(16))) double rowb[2][SUB];
-  __shared__ double pv[SUB];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  double v[CPW];
-#pragma unroll
-  for (int q = 0; q < CPW; ++q) v[q] = S[lane + (s * SUB + CPW * w + q) * SUB];
-#pragma unroll 1
-  for (int tw = 0; tw < NW; ++tw) {
-#pragma unroll
-    for (int tq = 0; tq < CPW; ++tq) {
-      const int t = CPW * tw + tq;
-      const int buf = tq & 1;
-      if (w == tw) colb[buf][lane] = v[tq];
-      if (lane == t) {
-#pragma unroll
-        for (int q = 0; q < CPW; q += 2)
-          *reinterpret_cast<double2 *>(&rowb[buf][CPW * w + q]) = double2{v[q], v[q + 1]};
-      }
-      __syncthreads();
-      const double d = rowb[buf][t];
-#if ACE_PIVOT_RCP
-      double rd = __builtin_amdgcn_rcp(d);
-      double re = fma(-d, rd, 1.0);
-      rd = fma(rd, re, rd);
-      re = fma(-d, rd, 1.0);
-      rd = fma(rd, re, rd);
-#else
-      const double rd = 1.0 / d;
-#endif
-      const double dit = colb[buf][lane];
-#pragma unroll
-      for (int q = 0; q < CPW; q += 2) {
-        const double2 rr = *reinterpret_cast<const double2 *>(&rowb[buf][CPW * w + q]);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int j = CPW * w + q + h;
-          const double dtj = h ? rr.y : rr.x;
-          double x;
-          if (lane == t) x = (j == t) ? -rd : dtj * rd;
-          else if (j == t) x = dit * rd;
-          else x = fma(-(dit * dtj), rd, v[q + h]);
-          v[q + h] = x;
-        }
-      }
-      if (tid == 0) pv[t] = d;
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < CPW; ++q) sSW[CPW * w + q][lane] = v[q];
-  __syncthreads();
-  if (tid < SUB) {
-    const double d = pv[tid];
-    piv[p0 + tid] = d;
-    if (!(d > 0.0) || !isfinite(d)) *flag = 1;
-  }
-}
-
-template <int NTH>
-__global__ __launch_bounds__(NTH, 4) void k_chain(double *__restrict__ W, int64_t ldp, int64_t k0,
-                                                  double *__restrict__ S0, double *__restrict__ S1,
-                                                  double *__restrict__ piv, int *__restrict__ flag) {
+// ---------------------------------------------------------------- split panel
+// k_panel's arithmetic with the column chunks spread over workgroups:
+// workgroup (g, cc) updates rows g (64) of the pivot block in chunk cc (64
+// columns) only -- (NB/SUB)^2 small workgroups instead of NB/SUB that each
+// walk every chunk.  Under the bulk update a chain workgroup runs on a CU it
+// shares with an update workgroup, so the chain's latency is its
+// per-workgroup work (profiles/r02_chain_ab.txt).  Phase 1 (Vn for the
+// rows) is recomputed by each workgroup of the row group, so its input
+// W[:, s] must not change during sub-step s:
+//   * sub-step s >= 1 reads it from X[s & 1], the copy of chunk s that the
+//     chunk-s workgroups of sub-step s-1 wrote beside W;
+//   * sub-step 0 reads W[:, 0] (the gathered panel) and writes its chunk 0
+//     (V) to V0 instead of W; sub-step 1 takes chunk 0's accumulator there.
+// X[0], X[1] and V0 are NB x SUB (row within the pivot block, column within
+// the chunk) after SW in the SW buffer.  Every element sees k_panel's
+// operations in k_panel's order: bit-identical.
+__global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int64_t ldp,
+                                                     int64_t k0, int s,
+                                                     const double *__restrict__ SW,
+                                                     const double *__restrict__ S,
+                                                     double *__restrict__ Snext,
+                                                     double *__restrict__ Xb) {
   CHAIN_PRIO();
-  constexpr int NW = NTH / 64;        // waves
-  constexpr int RG = NB / (16 * NW);  // 16-row groups per wave
-  static_assert(RG >= 1 && RG * 16 * NW == NB, "every pivot row owned by one wave");
   __shared__ double sSW[SUB][PLD];  // sSW[b][a] = SW(a, b)
   __shared__ double sSt[SUB][SLD];  // sSt[c][t] = S(t, 64 cc + c)
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lr = lane & 15, lk = lane >> 4;
   constexpr int NS = NB / SUB;
-#pragma unroll 1
-  for (int s = 0; s < NS; ++s) {
-    const double *S = (s & 1) ? S1 : S0;
-    double *Snext = (s & 1) ? S0 : S1;
-    chain_pivot<NW>(S, s, k0 + s * SUB, piv, flag, sSW);
-    // ---- panel update of the NB pivot rows (k_panel): the waves take the
-    // 16-row groups in RG rounds (one group's V fragments live at a time, so
-    // 512 threads stay within 128 VGPRs and fit next to one update WG)
-#pragma unroll 1
-    for (int g = 0; g < RG; ++g) {
-      const int ro = g * 16 * NW + 16 * w;  // first row of the group within the panel
-      const int rb = ro % SUB;              // its row within the 64-row sub-block
-      const bool pivrows = ro / SUB == s, nextrows = ro / SUB == s + 1;
-      const int64_t row = k0 + ro + lr;
-      d4 acc1[4];
-      if (pivrows) {
+  constexpr int64_t CH = (int64_t)NB * SUB;  // one chunk buffer
+  double *const V0 = Xb + 2 * CH;
+  const int g = blockIdx.x, cc = blockIdx.y;
+  const bool pivrows = g == s;
+  const bool nextrows = s + 1 < NS && g == s + 1;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int srow = 16 * w + lr;     // row within the row group (and Snext)
+  const int brow = g * SUB + srow;  // row within the pivot block
+  const int64_t row = k0 + brow;
+  d4 accs[4];
+  if (cc != s && !pivrows) {
+    const bool fromv = s == 1 && cc == 0;
+    const double *src = fromv ? V0 + brow : W + row + (int64_t)(cc * SUB) * ldp;
+    const int64_t lds = fromv ? NB : ldp;
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct)
+    for (int ctc = 0; ctc < 4; ++ctc)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc1[ct][j] = -sSW[16 * ct + lk + 4 * j][rb + lr];
-      } else {
+      for (int j = 0; j < 4; ++j) accs[ctc][j] = src[(int64_t)(16 * ctc + lk + 4 * j) * lds];
+  } else {
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc1[ct] = d4{0.0, 0.0, 0.0, 0.0};
-        double bw[SUB / 4];
+    for (int ctc = 0; ctc < 4; ++ctc) accs[ctc] = d4{0.0, 0.0, 0.0, 0.0};
+  }
+  for (int e = tid; e < SUB * SUB; e += 256) {
+    const int a = e & 63, b = e >> 6;
+    sSW[b][a] = SW[a + b * SUB];
+    if (cc != s) sSt[b][a] = S[a + (cc * SUB + b) * SUB];
+  }
+  __syncthreads();
+  d4 acc1[4];
+  if (pivrows) {
 #pragma unroll
-        for (int kk = 0; kk < SUB / 4; ++kk)
-          bw[kk] = W[row + (int64_t)(s * SUB + 4 * kk + lk) * ldp];
+    for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-        for (int kk = 0; kk < SUB / 4; ++kk) {
+      for (int j = 0; j < 4; ++j) acc1[ct][j] = -sSW[16 * ct + lk + 4 * j][16 * w + lr];
+  } else {
 #pragma unroll
-          for (int ct = 0; ct < 4; ++ct)
-            acc1[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(sSW[4 * kk + lk][16 * ct + lr], bw[kk],
-                                                            acc1[ct], 0, 0, 0);
-        }
-      }
+    for (int ct = 0; ct < 4; ++ct) acc1[ct] = d4{0.0, 0.0, 0.0, 0.0};
+    const double *src = s == 0 ? W + row : Xb + (int64_t)(s & 1) * CH + brow;
+    const int64_t lds = s == 0 ? ldp : NB;
+    double bw[SUB / 4];
+#pragma unroll
+    for (int kk = 0; kk < SUB / 4; ++kk) bw[kk] = src[(int64_t)(4 * kk + lk) * lds];
+#pragma unroll
+    for (int kk = 0; kk < SUB / 4; ++kk) {
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = s * SUB + 16 * ct + lk + 4 * j;
-          W[row + (int64_t)col * ldp] = -acc1[ct][j];
-          if (nextrows) Snext[(rb + lr) + col * SUB] = -acc1[ct][j];
-        }
-#pragma unroll 1
-      for (int cc = 0; cc < NS; ++cc) {
-        if (cc == s) continue;
-        // issue this chunk's accumulator loads before the staging barrier
-        d4 accs[4];
-#pragma unroll
-        for (int ctc = 0; ctc < 4; ++ctc)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            accs[ctc][j] = pivrows ? 0.0 : W[row + (int64_t)(cc * SUB + 16 * ctc + lk + 4 * j) * ldp];
-        __syncthreads();  // the previous chunk's sSt reads are done
-        for (int e = tid; e < SUB * SUB; e += NTH) {
-          const int t = e & 63, c = e >> 6;
-          sSt[c][t] = S[t + (cc * SUB + c) * SUB];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int ctc = 0; ctc < 4; ++ctc) {
-          d4 acc = accs[ctc];
-#pragma unroll
-          for (int kk = 0; kk < SUB / 4; ++kk)
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sSt[16 * ctc + lr][4 * kk + lk],
-                                                       acc1[kk >> 2][kk & 3], acc, 0, 0, 0);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int col = cc * SUB + 16 * ctc + lk + 4 * j;
-            W[row + (int64_t)col * ldp] = acc[j];
-            if (nextrows) Snext[(rb + lr) + col * SUB] = acc[j];
-          }
-        }
-      }
+        acc1[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(sSW[4 * kk + lk][16 * ct + lr], bw[kk],
+                                                        acc1[ct], 0, 0, 0);
     }
-    __syncthreads();  // Snext complete before the next sub-step's pivot reads it
+  }
+  if (cc == s) {
+    // acc1[ct][j] = Vn[row][16 ct + lk + 4 j]; chunk s = V = -Vn
+    double *dst = s == 0 ? V0 + brow : W + row + (int64_t)(s * SUB) * ldp;
+    const int64_t ldd = s == 0 ? NB : ldp;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = 16 * ct + lk + 4 * j;
+        dst[(int64_t)c * ldd] = -acc1[ct][j];
+        if (nextrows) Snext[srow + (s * SUB + c) * SUB] = -acc1[ct][j];
+      }
+    return;
+  }
+  // chunk s+1 is the next sub-step's phase-1 input: copy it to X[(s+1) & 1]
+  double *const xnext = cc == s + 1 ? Xb + (int64_t)((s + 1) & 1) * CH + brow : nullptr;
+#pragma unroll
+  for (int ctc = 0; ctc < 4; ++ctc) {
+    d4 acc = accs[ctc];
+#pragma unroll
+    for (int kk = 0; kk < SUB / 4; ++kk)
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sSt[16 * ctc + lr][4 * kk + lk],
+                                                 acc1[kk >> 2][kk & 3], acc, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 16 * ctc + lk + 4 * j;
+      const int col = cc * SUB + c;
+      W[row + (int64_t)col * ldp] = acc[j];
+      if (nextrows) Snext[srow + col * SUB] = acc[j];
+      if (xnext) xnext[(int64_t)c * NB] = acc[j];
+    }
   }
 }
 
@@ -912,15 +847,13 @@ __global__ __launch_bounds__(256) void k_unpack_panel(const double *__restrict__
 // Pivot block sweep (4 x 64-column sub-sweeps, pivots -> piv / flag) and the
 // panel GEMM for the rows rank r consumes.  W's pivot rows and S[0] must
 // hold the panel's pivot rows.
-// ACE_CHAIN=1 selects the fused single-workgroup k_chain (bit-identical; A/B
-// switch).  Measured slower than the per-sub-block k_pivot / k_panel
-// launches (775 vs 700 us per panel, profiles/r02_chain_ab.txt), so the
-// separate launches stay the default.
-static bool chain_fused() {
+// ACE_CHAIN=0 selects the row-group k_panel (A/B switch; k_panel_split is
+// the default and bit-identical).
+static bool panel_split() {
   static int v = -1;
   if (v < 0) {
     const char *e = getenv("ACE_CHAIN");
-    v = e ? (atoi(e) != 0) : 0;
+    v = e ? (atoi(e) != 0) : 1;
   }
   return v != 0;
 }
@@ -928,16 +861,16 @@ static bool chain_fused() {
 static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, double *SW,
                         double *const S[2], double *piv, int *flag, int G, int r,
                         hipStream_t st) {
-  if (chain_fused()) {
-    hipLaunchKernelGGL(k_chain<CH_THREADS>, dim3(1), dim3(CH_THREADS), 0, st, W, ld, k0, S[0], S[1],
-                       piv, flag);
-  } else {
-    for (int s = 0; s < NB / SUB; ++s) {
-      hipLaunchKernelGGL(k_pivot, dim3(1), dim3(256), 0, st, S[s & 1], s, SW, piv,
-                         k0 + (int64_t)s * SUB, flag);
+  const bool split = panel_split();
+  for (int s = 0; s < NB / SUB; ++s) {
+    hipLaunchKernelGGL(k_pivot, dim3(1), dim3(256), 0, st, S[s & 1], s, SW, piv,
+                       k0 + (int64_t)s * SUB, flag);
+    if (split)
+      hipLaunchKernelGGL(k_panel_split, dim3(NB / SUB, NB / SUB), dim3(256), 0, st, W, ld, k0, s,
+                         SW, S[s & 1], S[(s + 1) & 1], SW + SUB * SUB);
+    else
       hipLaunchKernelGGL(k_panel, dim3(NB / SUB), dim3(256), 0, st, W, ld, k0, s, SW, S[s & 1],
                          S[(s + 1) & 1], k0);
-    }
   }
   hipLaunchKernelGGL(k_panel_gemm, dim3((unsigned)(ld / SUB)), dim3(512), 0, st, W, Pn, ld, k0,
                      G, r);

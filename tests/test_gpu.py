@@ -445,10 +445,10 @@ def test_update_tile_order_is_bitwise_neutral(A, tmp_path):
     assert np.array_equal(mine, outs["4"])
 
 
-def test_fused_chain_is_bitwise_neutral(A, tmp_path):
-    """The fused pivot-block chain (k_chain, ACE_CHAIN=1) performs the k_pivot
-    / k_panel arithmetic in the same order in one workgroup: the inverse is
-    bit-identical to the per-sub-block launches (the default)."""
+def test_split_panel_is_bitwise_neutral(A, tmp_path):
+    """The column-split panel update (k_panel_split, default) performs
+    k_panel's arithmetic in k_panel's order over (NB/64)^2 workgroups: the
+    inverse is bit-identical to the row-group k_panel (ACE_CHAIN=0)."""
     import os
     import subprocess
     import sys
@@ -459,8 +459,8 @@ def test_fused_chain_is_bitwise_neutral(A, tmp_path):
     K = A.kernmat_SE_symmetric_cpp(X, Z, th)["full"]
     inp = str(tmp_path / "k.npz")
     np.savez(inp, K=K, s=th[0])
-    out = str(tmp_path / "inv1.npy")
-    env = dict(os.environ, ACE_CHAIN="1")
+    out = str(tmp_path / "inv0.npy")
+    env = dict(os.environ, ACE_CHAIN="0")
     subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
                    env=env, check=True, timeout=100)
     assert np.array_equal(A.invkernel_cpp(K, th[0])["inv"], np.load(out))
