@@ -111,16 +111,16 @@ hipError_t launch_tile_sums(const double *part, int64_t ntiles, int ncols, doubl
 int64_t tile_sums_work(int ncols);
 
 // ---- sweep -----------------------------------------------------------------
-// doubles of the SW buffer: SW (SUB x SUB), then k_panel_split's three
-// NB x SUB chunk buffers
-constexpr int64_t SW_DOUBLES = (int64_t)SUB * SUB + 3 * (int64_t)NB * SUB;
+// doubles of the SW buffer: SW[2] (SUB x SUB, ping-pong by sub-step), then
+// k_panel_split's three NB x SUB chunk buffers
+constexpr int64_t SW_DOUBLES = 2 * (int64_t)SUB * SUB + 3 * (int64_t)NB * SUB;
 struct SweepBufs {
   double *A;      // Naug x Naug, col-major, ld = Naug, lower triangle used
   int64_t ld;     // Naug
   int64_t npad;   // multiple of NB
   double *P[2];   // Naug x NB : -panel (negated copy), double-buffered by step
   double *W[2];   // Naug x NB : panel being swept, double-buffered by step
-  double *SW;     // SW_DOUBLES: SUB x SUB sub-pivot inverse + split-panel chunks
+  double *SW;     // SW_DOUBLES: 2 SUB x SUB sub-pivot inverses + split-panel chunks
   double *S[2];   // SUB x NB col-major: pivot rows before their sub-sweep (ping-pong)
   double *piv;    // npad pivots
   int *flag;      // set to 1 on a non-positive / non-finite pivot

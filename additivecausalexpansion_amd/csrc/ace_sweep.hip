@@ -100,38 +100,44 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
 // Sweeps the 64x64 sub-block s of the panel's pivot rows:
 //   d = D_tt; D_ij -= D_it D_tj / d; D_it /= d; D_tj /= d; D_tt = -1/d
 // -> SW = -D_s^-1 (exactly symmetric: every product is formed as a*b with
-// a = D_it = D_ti).  Layout: lane = row i, wave w keeps columns 16w..16w+15
-// in registers; per pivot the owning wave publishes column t and lane t of
-// every wave publishes its part of row t through double-buffered LDS
-// vectors, so there is one barrier per pivot.  D_s is read from the pivot-row
-// snapshot S (written by k_gather / the previous k_panel); every pivot d
-// (Cholesky diagonal squared) is recorded.
-__global__ __launch_bounds__(256) void k_pivot(const double *__restrict__ S, int s,
-                                               double *__restrict__ SW, double *__restrict__ piv,
-                                               int64_t p0, int *__restrict__ flag) {
-  CHAIN_PRIO();
-  __shared__ __attribute__((aligned(16))) double colb[2][SUB];
-  __shared__ __attribute__((aligned(16))) double rowb[2][SUB];
-  __shared__ double pv[SUB];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  double v[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) v[q] = S[lane + (s * SUB + 16 * w + q) * SUB];
+// a = D_it = D_ti).  Layout: lane = row i, wave w of NW keeps columns
+// CW w .. CW w + CW - 1 (CW = 64 / NW) in registers; per pivot the owning
+// wave publishes column t and lane t of every wave publishes its part of
+// row t through double-buffered LDS vectors, so there is one barrier per
+// pivot.  More waves = fewer dependent VALU operations per wave per pivot
+// (the chain's critical path); the arithmetic per element is the same for
+// every NW.  D_s is read from the pivot-row snapshot S (written by k_gather
+// / the previous panel update); every pivot d (Cholesky diagonal squared)
+// is recorded.
+template <int NW>
+struct PivotLds {
+  __attribute__((aligned(16))) double colb[2][SUB];
+  __attribute__((aligned(16))) double rowb[2][SUB];
+  double pv[SUB];
+};
+
+// the sub-sweep itself: v = this lane's row, columns CW w .. CW w + CW - 1
+template <int NW>
+__device__ __forceinline__ void pivot_sweep(double (&v)[SUB / NW], PivotLds<NW> &L, int tid) {
+  constexpr int CW = SUB / NW;
+  static_assert(CW % 2 == 0, "double2 row publishing");
+  const int lane = tid & 63, w = tid >> 6;
   // no global memory traffic inside the loop: every __syncthreads() is then
   // a bare s_barrier (a pending global store would add a vmcnt(0) wait)
-  for (int tw = 0; tw < 4; ++tw) {
+#pragma unroll 1
+  for (int tw = 0; tw < NW; ++tw) {
 #pragma unroll
-    for (int tq = 0; tq < 16; ++tq) {
-      const int t = 16 * tw + tq;
+    for (int tq = 0; tq < CW; ++tq) {
+      const int t = CW * tw + tq;
       const int buf = tq & 1;
-      if (w == tw) colb[buf][lane] = v[tq];
+      if (w == tw) L.colb[buf][lane] = v[tq];
       if (lane == t) {
 #pragma unroll
-        for (int q = 0; q < 16; q += 2)
-          *reinterpret_cast<double2 *>(&rowb[buf][16 * w + q]) = double2{v[q], v[q + 1]};
+        for (int q = 0; q < CW; q += 2)
+          *reinterpret_cast<double2 *>(&L.rowb[buf][CW * w + q]) = double2{v[q], v[q + 1]};
       }
       __syncthreads();
-      const double d = rowb[buf][t];
+      const double d = L.rowb[buf][t];
       // 1/d by v_rcp_f64 + two Newton steps (<= 1 ulp): five dependent fp64
       // operations on the chain's critical path instead of the eleven of
       // the IEEE division sequence
@@ -144,17 +150,17 @@ __global__ __launch_bounds__(256) void k_pivot(const double *__restrict__ S, int
 #else
       const double rd = 1.0 / d;
 #endif
-      const double dit = colb[buf][lane];
-      double rt[16];
+      const double dit = L.colb[buf][lane];
+      double rt[CW];
 #pragma unroll
-      for (int q = 0; q < 16; q += 2) {
-        const double2 x = *reinterpret_cast<const double2 *>(&rowb[buf][16 * w + q]);
+      for (int q = 0; q < CW; q += 2) {
+        const double2 x = *reinterpret_cast<const double2 *>(&L.rowb[buf][CW * w + q]);
         rt[q] = x.x;
         rt[q + 1] = x.y;
       }
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int j = 16 * w + q;
+      for (int q = 0; q < CW; ++q) {
+        const int j = CW * w + q;
         const double dtj = rt[q];
         double x;
         if (lane == t) x = (j == t) ? -rd : dtj * rd;
@@ -162,17 +168,68 @@ __global__ __launch_bounds__(256) void k_pivot(const double *__restrict__ S, int
         else x = fma(-(dit * dtj), rd, v[q]);
         v[q] = x;
       }
-      if (tid == 0) pv[t] = d;
+      if (tid == 0) L.pv[t] = d;
     }
   }
   __syncthreads();
+}
+
+// pivots (and the non-PD flag) and SW = -D^-1 out
+template <int NW>
+__device__ __forceinline__ void pivot_store(const double (&v)[SUB / NW], const PivotLds<NW> &L,
+                                            int tid, double *__restrict__ SW,
+                                            double *__restrict__ piv, int64_t p0,
+                                            int *__restrict__ flag) {
+  constexpr int CW = SUB / NW;
+  const int lane = tid & 63, w = tid >> 6;
   if (tid < SUB) {
-    const double d = pv[tid];
+    const double d = L.pv[tid];
     piv[p0 + tid] = d;
     if (!(d > 0.0) || !isfinite(d)) *flag = 1;
   }
 #pragma unroll
-  for (int q = 0; q < 16; ++q) SW[lane + (16 * w + q) * SUB] = v[q];
+  for (int q = 0; q < CW; ++q) SW[lane + (CW * w + q) * SUB] = v[q];
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_pivot(const double *__restrict__ S, int s,
+                                                   double *__restrict__ SW,
+                                                   double *__restrict__ piv, int64_t p0,
+                                                   int *__restrict__ flag) {
+  CHAIN_PRIO();
+  constexpr int CW = SUB / NW;
+  __shared__ PivotLds<NW> L;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double v[CW];
+#pragma unroll
+  for (int q = 0; q < CW; ++q) v[q] = S[lane + (s * SUB + CW * w + q) * SUB];
+  pivot_sweep<NW>(v, L, tid);
+  pivot_store<NW>(v, L, tid, SW, piv, p0, flag);
+}
+
+// waves of the pivot workgroup: 4, 8 or 16 (ACE_PIVOT_WAVES, A/B switch)
+static int pivot_waves() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_PIVOT_WAVES");
+    v = e ? atoi(e) : 4;
+    if (v != 4 && v != 8 && v != 16) v = 4;
+  }
+  return v;
+}
+
+static void launch_pivot(const double *S, int s, double *SW, double *piv, int64_t p0, int *flag,
+                         hipStream_t st) {
+  switch (pivot_waves()) {
+    case 16:
+      hipLaunchKernelGGL(k_pivot<16>, dim3(1), dim3(1024), 0, st, S, s, SW, piv, p0, flag);
+      break;
+    case 8:
+      hipLaunchKernelGGL(k_pivot<8>, dim3(1), dim3(512), 0, st, S, s, SW, piv, p0, flag);
+      break;
+    default:
+      hipLaunchKernelGGL(k_pivot<4>, dim3(1), dim3(256), 0, st, S, s, SW, piv, p0, flag);
+  }
 }
 
 // ---------------------------------------------------------------- panel
@@ -280,17 +337,25 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ W, int64_t l
 //   * sub-step 0 reads W[:, 0] (the gathered panel) and writes its chunk 0
 //     (V) to V0 instead of W; sub-step 1 takes chunk 0's accumulator there.
 // X[0], X[1] and V0 are NB x SUB (row within the pivot block, column within
-// the chunk) after SW in the SW buffer.  Every element sees k_panel's
-// operations in k_panel's order: bit-identical.
+// the chunk) after SW[0], SW[1] in the SW buffer.  The workgroup holding the
+// next diagonal block D_{s+1} (g = cc = s + 1) then runs the k_pivot
+// sub-sweep of sub-step s+1 on it (into SWn = the other SW buffer), which
+// saves one launch -- and its wait for a free CU slot under the bulk update
+// -- per sub-step.  Every element sees k_panel's / k_pivot's operations in
+// their order: bit-identical.
 __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int64_t ldp,
                                                      int64_t k0, int s,
                                                      const double *__restrict__ SW,
                                                      const double *__restrict__ S,
                                                      double *__restrict__ Snext,
-                                                     double *__restrict__ Xb) {
+                                                     double *__restrict__ Xb,
+                                                     double *__restrict__ SWn,
+                                                     double *__restrict__ piv,
+                                                     int *__restrict__ flag) {
   CHAIN_PRIO();
   __shared__ double sSW[SUB][PLD];  // sSW[b][a] = SW(a, b)
   __shared__ double sSt[SUB][SLD];  // sSt[c][t] = S(t, 64 cc + c)
+  __shared__ PivotLds<4> PL;
   constexpr int NS = NB / SUB;
   constexpr int64_t CH = (int64_t)NB * SUB;  // one chunk buffer
   double *const V0 = Xb + 2 * CH;
@@ -359,9 +424,10 @@ __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int
   }
   // chunk s+1 is the next sub-step's phase-1 input: copy it to X[(s+1) & 1]
   double *const xnext = cc == s + 1 ? Xb + (int64_t)((s + 1) & 1) * CH + brow : nullptr;
+  const bool fusepiv = nextrows && cc == s + 1;  // this workgroup holds D_{s+1}
 #pragma unroll
   for (int ctc = 0; ctc < 4; ++ctc) {
-    d4 acc = accs[ctc];
+    d4 &acc = accs[ctc];
 #pragma unroll
     for (int kk = 0; kk < SUB / 4; ++kk)
       acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sSt[16 * ctc + lr][4 * kk + lk],
@@ -375,6 +441,19 @@ __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int
       if (xnext) xnext[(int64_t)c * NB] = acc[j];
     }
   }
+  if (!fusepiv) return;
+  // D_{s+1}: accs[ctc][j] = D(srow, 16 ctc + lk + 4 j) -> lane = row layout
+  __syncthreads();  // every wave is done with sSW (phase 1)
+#pragma unroll
+  for (int ctc = 0; ctc < 4; ++ctc)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sSW[16 * ctc + lk + 4 * j][srow] = accs[ctc][j];
+  __syncthreads();
+  double v[SUB / 4];
+#pragma unroll
+  for (int q = 0; q < SUB / 4; ++q) v[q] = sSW[16 * w + q][lane];
+  pivot_sweep<4>(v, PL, tid);
+  pivot_store<4>(v, PL, tid, SWn, piv, k0 + (int64_t)(s + 1) * SUB, flag);
 }
 
 // ---------------------------------------------------------------- panel GEMM
@@ -862,15 +941,16 @@ static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, dou
                         double *const S[2], double *piv, int *flag, int G, int r,
                         hipStream_t st) {
   const bool split = panel_split();
+  double *const SWb[2] = {SW, SW + SUB * SUB};  // ping-pong by sub-step
   for (int s = 0; s < NB / SUB; ++s) {
-    hipLaunchKernelGGL(k_pivot, dim3(1), dim3(256), 0, st, S[s & 1], s, SW, piv,
-                       k0 + (int64_t)s * SUB, flag);
+    if (!split || s == 0) launch_pivot(S[s & 1], s, SWb[s & 1], piv, k0 + (int64_t)s * SUB, flag, st);
     if (split)
       hipLaunchKernelGGL(k_panel_split, dim3(NB / SUB, NB / SUB), dim3(256), 0, st, W, ld, k0, s,
-                         SW, S[s & 1], S[(s + 1) & 1], SW + SUB * SUB);
+                         SWb[s & 1], S[s & 1], S[(s + 1) & 1], SW + 2 * SUB * SUB,
+                         SWb[(s + 1) & 1], piv, flag);
     else
-      hipLaunchKernelGGL(k_panel, dim3(NB / SUB), dim3(256), 0, st, W, ld, k0, s, SW, S[s & 1],
-                         S[(s + 1) & 1], k0);
+      hipLaunchKernelGGL(k_panel, dim3(NB / SUB), dim3(256), 0, st, W, ld, k0, s, SWb[s & 1],
+                         S[s & 1], S[(s + 1) & 1], k0);
   }
   hipLaunchKernelGGL(k_panel_gemm, dim3((unsigned)(ld / SUB)), dim3(512), 0, st, W, Pn, ld, k0,
                      G, r);
@@ -952,7 +1032,13 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
   const int64_t naug = b.ld;
   const unsigned nT = (unsigned)(naug / UT);
   const int steps = (int)(b.npad / NB);
-  const bool two = sy && sy->side && sy->nev >= 2 * steps + 1;
+  // ACE_LOOKAHEAD=0: one stream, no lookahead (diagnostic: the chain
+  // kernels then run alone, uncontended)
+  static const int look = [] {
+    const char *e = getenv("ACE_LOOKAHEAD");
+    return e ? atoi(e) : 1;
+  }();
+  const bool two = look && sy && sy->side && sy->nev >= 2 * steps + 1;
   hipStream_t side = two ? sy->side : st;
   int used = 0;
   hipError_t e;
