@@ -449,7 +449,8 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   // the sweep inverted): no Kfull copy and no pass over it (k_final_sums)
   if (timed) ck(ctx, hipEventRecord(m->ev_grad[2 * ts], st), "event");
   ck(ctx, launch_grad(s.kind, s.PM, ps, s.B, s.ZS, tv, w.A.d(), w.naug, -1.0, m->alpha.d(),
-                      nullptr, m->gpart.d(), st),
+                      nullptr, m->gpart.d(), st, reinterpret_cast<const Tile *>(m->gtiles.p),
+                      m->ngdiag >= 0 ? m->ntiles : 0, 1, m->ngdiag),
      "grad");
   if (timed) ck(ctx, hipEventRecord(m->ev_grad[2 * ts + 1], st), "event");
   const int ldg = grad_part_cols(s.PM, s.B);
@@ -505,6 +506,21 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
     m->naug = m->sw.naug;
     m->ntiles = grad_ntiles(n);
     m->ntr = (n + AT - 1) / AT;
+    if (const int S = grad_order_block(); S > 0) {
+      // diagonal 64-tiles first, then the strictly lower ones dealt to the
+      // XCDs in S x S super-blocks (a launch's block b runs on XCD b % 8)
+      std::vector<Tile> lst, low;
+      for (int64_t I = 0; I < m->ntr; ++I) lst.push_back(Tile{(int)I, (int)I});
+      for (int64_t I = 1; I < m->ntr; ++I)
+        for (int64_t J = 0; J < I; ++J) low.push_back(Tile{(int)I, (int)J});
+      const std::vector<Tile> o = xcd_update_order(low, S);
+      lst.insert(lst.end(), o.begin(), o.end());
+      alloc(ctx, m->gtiles, lst.size() * sizeof(Tile), "alloc grad tiles");
+      ck(ctx, hipMemcpy(m->gtiles.p, lst.data(), lst.size() * sizeof(Tile), hipMemcpyHostToDevice),
+         "upload grad tiles");
+      m->ntiles = (int64_t)lst.size();
+      m->ngdiag = m->ntr;
+    }
     const Shape &s = m->s;
     alloc(ctx, m->y, (size_t)m->npad * sizeof(double), "alloc y");
     alloc(ctx, m->tab, (size_t)(2 * s.B * s.PM + s.B) * sizeof(double), "alloc tab");

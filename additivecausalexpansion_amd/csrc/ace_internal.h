@@ -104,6 +104,9 @@ hipError_t launch_grad(int kind, int PM, PairSide side, int B, int ZS,
                        const Tile *tiles = nullptr, int64_t ntiles = 0, int G = 1,
                        int64_t ndiag = -1);
 int64_t grad_ntiles(int64_t n);
+// super-block size of the fused model's XCD-dealt gradient tile order (0:
+// row-major grid); ACE_GRAD_ORDER=S overrides (A/B switch)
+int grad_order_block();
 // out[j] = sum_t part[t * ncols + j], j < ncols (deterministic order); work
 // needs tile_sums_work(ncols) doubles.
 hipError_t launch_tile_sums(const double *part, int64_t ntiles, int ncols, double *work,

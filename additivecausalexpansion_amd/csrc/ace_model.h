@@ -82,6 +82,8 @@ struct ace_model {
   bool has_inverse = false;  // a para_update has left a resident inverse
   SideBufs side;
   DBuf y, tab, alpha, scal, gpart, gwork, gsum, sums;
+  DBuf gtiles;          // gradient tile list (grad_tile_order), or none
+  int64_t ngdiag = -1;  // its leading diagonal tiles
   PinnedBuf hio;  // [theta tables | gsum | sums | scal | flag] host staging
   SweepWork sw;   // A = resident inverse of the last para_update
   SweepWork sw2;  // train_stats scratch (keeps sw's inverse, Q6)

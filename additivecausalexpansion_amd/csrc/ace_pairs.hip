@@ -10,6 +10,7 @@
 // operand (x_c, z_c, the per-b weight rows) is wave-uniform and is fetched
 // with scalar loads, and every store to the column-major matrix is one
 // contiguous 512-B segment per wave.  fp64 VALU bound.
+#include <algorithm>
 #include <cstdlib>
 
 #include "ace_internal.h"
@@ -709,6 +710,18 @@ static hipError_t grad_pm(int kind, PairSide S, int B, int ZS, TabView tab, cons
   }
 #undef ACE_G
   return hipGetLastError();
+}
+
+int grad_order_block() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_GRAD_ORDER");
+    // 4: gradient HBM reads 1.52 -> 1.21 GB per C2 evaluation against the
+    // 1.07 GB lower triangle (the per-tile X / Z staging stays in each XCD's
+    // L2), time-neutral (profiles/r02_grad_ab.txt)
+    v = e ? std::max(0, atoi(e)) : 4;
+  }
+  return v;
 }
 
 hipError_t launch_grad(int kind, int PM, PairSide S, int B, int ZS, TabView tab,

@@ -199,10 +199,10 @@ __host__ __device__ inline MmLayout mm_layout(int PM, int B, int KIND, bool grad
   off += 64 * (PM + 1);
   o.xi = off;
   if (grad && PM <= 32) off += 64 * (PM + 1);
-  o.z = off;
-  off += (B - 1) * 64;
+  o.z = off;  // row 0: slice 0's unit basis factors, rows 1..B-1: Z
+  off += B * 64;
   o.lz = off;
-  if (KIND == 0) off += (B - 1) * 64;
+  if (KIND == 0) off += B * 64;
   o.nc = off;
   off += NS * 64;
   o.nr = off;
@@ -238,8 +238,8 @@ __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS
   L.E = lds + o.etab;
   L.XJ = lds + o.xj;
   L.XI = lds + o.xi;
-  L.Z = lds + o.z;
-  L.LZ = lds + o.lz;
+  L.Z = lds + o.z + 64;  // slice b's row at L.Z + (b - 1) * 64, b = 0 included
+  L.LZ = lds + o.lz + 64;
   L.Nc = lds + o.nc;
   L.Nr = lds + o.nr;
   L.W = lds + o.w;
@@ -255,6 +255,10 @@ __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS
     const int bb = e >> 6, c = e & 63;
     L.Z[e] = S.Z[(C0 + c) * ZS + bb];
     if (KIND == 0) L.LZ[e] = S.LZ[(C0 + c) * ZS + bb];
+  }
+  if (tid < 64) {  // slice 0: z = 1, log|z| = 0 (products and sums exact)
+    L.Z[tid - 64] = 1.0;
+    if (KIND == 0) L.LZ[tid - 64] = 0.0;
   }
   if (tid < 32) L.E[tid] = kExp2Tab[tid];
   for (int e = tid; e < NS * PM; e += NT) L.W[e] = (e < B * PM) ? wk[e] : wlast[e - B * PM];
@@ -499,6 +503,10 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   if (tiles) {
     I = tiles[t].I;
     J = tiles[t].J;
+    if (I < 0) {  // padding of an XCD-dealt list: an all-zero partial row
+      for (int64_t e = threadIdx.x; e < ldg; e += NT) gpart[t * ldg + e] = 0.0;
+      return;
+    }
   } else if (DG) {
     I = J = blockIdx.x;
   } else {
@@ -573,9 +581,13 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   };
   // PS: one partial buffer per slice (the host checked L.red_slices == B)
   constexpr bool per_slice = PS;
+  // Slice 0 runs the basis-slice code with z = 1 and log|z| = 0 (an LDS row
+  // of ones / zeros; exact), so no per-pair code tests b: a lane's pairs are
+  // one straight-line block the scheduler can interleave (a b == 0 test made
+  // every pair its own basic block, running its dependent fp64 chain alone)
   for (int b = B - 1; b >= 0; --b) {
     double *red = L.Red + (per_slice ? b : (b & 1)) * PER;
-    double zr = 0.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
+    double zr = 1.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
     if (b > 0) {
       zr = S.Z[r * ZS + b - 1];
       if (KIND == 0) lzr = S.LZ[r * ZS + b - 1];
@@ -595,21 +607,23 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
         const int64_t c = C0 + cbase + cl;
         double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), 0.0);
         if (DG && c == r) r2 = 0.0;
-        double zc = 0.0, lzc = 0.0;
-        if (b > 0) {
-          zc = zcol[cl];
-          if (KIND == 0) lzc = lzcol[cl];
-        }
+        const double zc = zcol[cl];
+        const double lzc = KIND == 0 ? lzcol[cl] : 0.0;
         const bool rlo = DG && r < c;
         const double zlo = rlo ? zr : zc, zhi = rlo ? zc : zr;
         double kb, f = 1.0;
         if (KIND == 0) {
-          kb = kval_mm<0>(b, r2, lam, zlo, zhi, rlo ? lzr : lzc, rlo ? lzc : lzr, L.E);
+          // log|0| = -inf makes the exponential NaN: a select (not a branch)
+          // puts the reference's 0 there
+          const double kz = (sgn_mm(zlo) * sgn_mm(zhi)) *
+                            exp_tb(((lam - r2) + (rlo ? lzr : lzc)) + (rlo ? lzc : lzr), L.E);
+          kb = sel_f64(zlo == 0.0 || zhi == 0.0, 0.0, kz);
         } else {
           const double tt = sqrt_pk(r2);
           f = 1.0 + SQRT3 * tt;
           const double e = f * exp_tb(lam - SQRT3 * tt, L.E);
-          kb = (b == 0) ? e : (zlo == 0.0 ? 0.0 : (e * zlo) * zhi);
+          // z = 0 gives a zero product (of either sign: it only enters sums)
+          kb = (e * zlo) * zhi;
         }
         const double tk = tv[cb][v] * kb;
         gl += tk;
