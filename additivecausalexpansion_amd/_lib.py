@@ -107,7 +107,20 @@ SIGNATURES = {
                                                 ctypes.c_char_p, ctypes.POINTER(_vp)]),
     "ace_model_shard_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int),
                                             ctypes.POINTER(ctypes.c_int)]),
+    "ace_model_create_sharded_host": (ctypes.c_int, [_vp, ctypes.c_int, _I64, ctypes.c_int,
+                                                     ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                     ctypes.c_void_p, ctypes.POINTER(_vp)]),
 }
+
+# ace_comm_ops (include/ace_hip.h): host-callback collectives
+BCAST_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, _D, _I64, ctypes.c_int)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, _D, _D, _I64)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, _D, _I64, ctypes.c_int)
+
+
+class CommOps(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("broadcast", BCAST_FN),
+                ("allgather", ALLGATHER_FN), ("allreduce", ALLREDUCE_FN)]
 UNIQUE_ID_BYTES = 128
 
 STATUS = {0: "ACE_OK", 1: "ACE_ERR_ARG", 2: "ACE_ERR_HIP", 3: "ACE_ERR_OOM",

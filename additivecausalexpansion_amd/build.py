@@ -13,7 +13,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 SOURCES = ["csrc/ace_pairs.hip", "csrc/ace_pairs_mm.hip", "csrc/ace_sweep.hip", "csrc/ace_util.hip",
            "csrc/ace_symm.hip", "csrc/ace_api.cpp", "csrc/ace_host.cpp", "csrc/ace_shard.cpp",
-           "csrc/ace_predict.cpp", "csrc/ace_dmat.cpp"]
+           "csrc/ace_predict.cpp", "csrc/ace_dmat.cpp", "csrc/ace_train.hip"]
 HEADERS = ["csrc/ace_internal.h", "csrc/ace_common.h", "csrc/ace_model.h", "../include/ace_hip.h"]
 OUT = os.path.join(HERE, "libace_hip.so")
 OBJDIR = os.path.join(HERE, "build")

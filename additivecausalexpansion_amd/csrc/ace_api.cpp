@@ -402,20 +402,30 @@ int ace_pred_marginal(ace_ctx *ctx, int64_t nX, int64_t nx, int B, const double 
 
 namespace {
 
-void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu, bool timed) {
+// One evaluation on the stream.  theta_dev != nullptr: theta is a device
+// vector (the device-fused training loop) -- tables, exp(theta[0]) and
+// theta[1] are then read on the device and `theta` is not used.
+void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu, bool timed,
+                    const double *theta_dev = nullptr) {
   ace_ctx *ctx = m->ctx;
   hipStream_t st = ctx->stream;
   const Shape &s = m->s;
-  std::vector<double> tab = make_tab(theta, s);
-  // pinned staging, async on the stream: the previous evaluation's results
-  // were synchronised before this one started, so the region is free
-  double *h = m->hio.ensure(ctx, tab.size() + (size_t)(s.B * (s.PM + 1) + 1) + 4 + 5 + 1);
-  std::copy(tab.begin(), tab.end(), h);
-  ck(ctx, hipMemcpyAsync(m->tab.p, h, tab.size() * sizeof(double), hipMemcpyHostToDevice, st),
-     "upload tables");
-  const TabView tv = tab_view(m->tab, s);
+  TabView tv = tab_view(m->tab, s);
+  double sig = 0.0;
+  if (theta_dev) {
+    ck(ctx, launch_make_tab(theta_dev, s.B, s.p, s.PM, m->tab.d(), st), "tables");
+    tv.sig = m->tab.d() + 2 * s.B * s.PM + s.B;
+  } else {
+    std::vector<double> tab = make_tab(theta, s);
+    // pinned staging, async on the stream: the previous evaluation's results
+    // were synchronised before this one started, so the region is free
+    double *h = m->hio.ensure(ctx, tab.size() + (size_t)(s.B * (s.PM + 1) + 1) + 4 + 5 + 1);
+    std::copy(tab.begin(), tab.end(), h);
+    ck(ctx, hipMemcpyAsync(m->tab.p, h, tab.size() * sizeof(double), hipMemcpyHostToDevice, st),
+       "upload tables");
+    sig = std::exp(theta[0]);
+  }
   const PairSide ps = m->side.view(m->n);
-  const double sig = std::exp(theta[0]);
   ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, m->n, m->y.d(), st), "aug init");
   ck(ctx, hipMemsetAsync(w.flag.p, 0, sizeof(int), st), "memset flag");
   SweepSync sy = w.sync(ctx);
@@ -442,8 +452,8 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   tmg.used = &m->upd_used[ts];
   tmg.flops = m->upd_flops.data() + ts * (nset / 2);
   ck(ctx, run_sweep(w.bufs(), st, &sy, timed ? &tmg : nullptr), "sweep");
-  ck(ctx, launch_alpha_from_aug(w.A.d(), w.naug, w.npad, m->n, theta[1], use_mu, m->alpha.d(),
-                                m->scal.d(), st),
+  ck(ctx, launch_alpha_from_aug(w.A.d(), w.naug, w.npad, m->n, theta_dev ? 0.0 : theta[1], use_mu,
+                                m->alpha.d(), m->scal.d(), st, theta_dev ? theta_dev + 1 : nullptr),
      "alpha");
   // RMSE residual ybar - Kfull alpha = sig alpha (A = Kfull + sig I is what
   // the sweep inverted): no Kfull copy and no pass over it (k_final_sums)
@@ -457,7 +467,7 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   ck(ctx, launch_tile_sums(m->gpart.d(), m->ntiles, ldg, m->gwork.d(), m->gsum.d(), st),
      "tile sums");
   ck(ctx, launch_final_sums(m->y.d(), m->scal.d() + 4, m->alpha.d(), nullptr, sig, m->n,
-                            w.piv.d(), w.npad, m->sums.d(), st),
+                            w.piv.d(), w.npad, m->sums.d(), st, tv.sig),
      "final sums");
 }
 
@@ -485,6 +495,102 @@ void model_collect_timing(ace_model *m, int ts) {
   // from its tiles), pair kernels by their algorithmic flop formulas
   m->t_work[1] += pairs * B * (3 * p + 3);
   m->t_work[2] += pairs * (4 * B * p + 2 * p) + (m->s.kind == ACE_KERNEL_MATERN32 ? pairs * B * p : 0);
+}
+
+// Host syncs of the device-fused training loop: every ACE_TRAIN_SYNC
+// iterations (default 4).  Iterations enqueued after the one that converged
+// still run but change nothing (k_train_step checks the stop flag), so a fit
+// spends at most ACE_TRAIN_SYNC - 1 extra evaluations.
+int train_sync_every() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_TRAIN_SYNC");
+    v = e ? std::max(1, atoi(e)) : 4;
+  }
+  return v;
+}
+
+// ace_model_train of an unsharded model: theta, the optimizer moments and
+// the stats matrix live in HBM; each iteration is the evaluation pipeline
+// (tables from the device theta) + k_train_step, enqueued without a host
+// round trip.
+int train_device(ace_model *m, int optimizer, double learn_rate, double momentum, double beta1,
+                 double beta2, int norm_clip, double clip_at, int maxiter, double tol,
+                 double *theta, double *stats, int *iters, int *converged) {
+  ace_ctx *ctx = m->ctx;
+  ACE_TRY
+  ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+  arg(ctx, m->has_data, "ace_model_set_data() not called");
+  const Shape &s = m->s;
+  const int P = 2 + s.B * (s.p + 1);
+  hipStream_t st = ctx->stream;
+  DBuf dst, dhist, dctl;
+  std::vector<double> init((size_t)(4 * P), 0.0);
+  std::copy(theta, theta + P, init.begin());
+  upload(ctx, dst, init.data(), init.size(), "upload train state");
+  std::vector<double> hz((size_t)(2 * (maxiter + 2)), 0.0);
+  upload(ctx, dhist, hz.data(), hz.size(), "upload stats");
+  alloc(ctx, dctl, 4 * sizeof(int), "alloc train control");
+  ck(ctx, hipMemsetAsync(dctl.p, 0, 4 * sizeof(int), st), "memset control");
+  TrainCfg c;
+  c.optimizer = optimizer;
+  c.lr = learn_rate;
+  c.momentum = momentum;
+  c.beta1 = beta1;
+  c.beta2 = beta2;
+  c.clip = norm_clip;
+  c.clip_at = clip_at;
+  c.tol = tol;
+  c.P = P;
+  c.B = s.B;
+  c.p = s.p;
+  c.PM = s.PM;
+  c.kind = s.kind;
+  c.n = m->n;
+  c.std_y = m->std_y;
+  const int K = train_sync_every();
+  int ctl[4] = {0, 0, 0, 0};
+  bool interrupted = false;
+  for (int it = 1; it <= maxiter; ++it) {
+    if (ctx->poll && ctx->poll(ctx->poll_user)) {  // before iteration it, like para_update
+      interrupted = true;
+      break;
+    }
+    model_pipeline(m, m->sw, nullptr, it == 1 ? 1 : 0, false, dst.d());
+    ck(ctx, launch_train_step(c, it, m->gsum.d(), m->sums.d(), m->scal.d(), m->sw.flag.i(), dst.d(),
+                              dhist.d(), dctl.i(), st),
+       "train step");
+    if (it % K == 0 || it == maxiter) {
+      ck(ctx, hipMemcpyAsync(ctl, dctl.p, sizeof(ctl), hipMemcpyDeviceToHost, st), "download control");
+      sync(ctx);
+      if (ctl[1] != 0) break;
+    }
+  }
+  ck(ctx, hipMemcpyAsync(ctl, dctl.p, sizeof(ctl), hipMemcpyDeviceToHost, st), "download control");
+  download(ctx, theta, dst.d(), (size_t)P, "download theta");
+  download(ctx, stats, dhist.d(), (size_t)(2 * (maxiter + 2)), "download stats");
+  sync(ctx);
+  m->has_inverse = ctl[0] > 0;
+  const int it = ctl[0];
+  if (iters) *iters = it;
+  if (converged) *converged = 0;
+  if (interrupted) {
+    ctx->err = "interrupted";
+    return ACE_ERR_INTERRUPTED;
+  }
+  if (ctl[1] == 2) {
+    ctx->err = "Some gradients are not finite, NaN, or NA. Often this is due to too large "
+               "learning rates.";
+    return ACE_ERR_NONFINITE;
+  }
+  double fin[2];
+  const int rc = ace_model_train_stats(m, theta, fin);
+  if (rc != ACE_OK) return rc;
+  stats[2 * (it + 1)] = fin[0];
+  stats[2 * (it + 1) + 1] = fin[1];
+  if (converged) *converged = it < maxiter ? 1 : 0;
+  return ACE_OK;
+  ACE_CATCH
 }
 
 }  // namespace
@@ -523,7 +629,7 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
     }
     const Shape &s = m->s;
     alloc(ctx, m->y, (size_t)m->npad * sizeof(double), "alloc y");
-    alloc(ctx, m->tab, (size_t)(2 * s.B * s.PM + s.B) * sizeof(double), "alloc tab");
+    alloc(ctx, m->tab, (size_t)(2 * s.B * s.PM + s.B + 1) * sizeof(double), "alloc tab");
     alloc(ctx, m->alpha, (size_t)m->npad * sizeof(double), "alloc alpha");
     alloc(ctx, m->scal, 16 * sizeof(double), "alloc scal");
     const int ldg = grad_part_cols(s.PM, s.B);
@@ -764,6 +870,33 @@ int ace_model_create_sharded(ace_ctx *ctx, int kind, int64_t n, int p, int B, in
   return ACE_OK;
 }
 
+int ace_model_create_sharded_host(ace_ctx *ctx, int kind, int64_t n, int p, int B, int world,
+                                  int rank, const ace_comm_ops *ops, ace_model **out) {
+  if (!ctx || !out) return ACE_ERR_ARG;
+  *out = nullptr;
+  if (!ops || !ops->broadcast || !ops->allgather || !ops->allreduce) {
+    ctx->err = "ace_model_create_sharded_host: incomplete ace_comm_ops";
+    return ACE_ERR_ARG;
+  }
+  ace_model *m = new ace_model();
+  m->ctx = ctx;
+  try {
+    ck(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    m->s = check_shape(ctx, kind, p, B);
+    arg(ctx, n >= 2, "n must be >= 2");
+    arg(ctx, world >= 1 && world <= 64 && rank >= 0 && rank < world, "bad world / rank");
+    m->n = n;
+    m->npad = round_up(n, NB);
+    m->naug = m->npad + AUG;
+    m->shard = shard_create_host(ctx, m->s, n, world, rank, *ops);
+  } catch (const Fail &f) {
+    ace_model_destroy(m);
+    return f.code;
+  }
+  *out = m;
+  return ACE_OK;
+}
+
 int ace_model_shard_info(const ace_model *m, int *world, int *rank) {
   if (!m) return ACE_ERR_ARG;
   if (world) *world = m->shard ? shard_world(m->shard) : 1;
@@ -782,8 +915,12 @@ int ace_model_train(ace_model *m, int optimizer, double learn_rate, double momen
     return ACE_ERR_ARG;
   }
   const int P = 2 + m->s.B * (m->s.p + 1);
-  std::vector<double> g((size_t)P), mom1((size_t)P, 0.0), mom2((size_t)P, 0.0);
   for (int64_t j = 0; j < 2 * (int64_t)(maxiter + 2); ++j) stats[j] = 0.0;
+  if (!m->shard)
+    return train_device(m, optimizer, learn_rate, momentum, beta1, beta2, norm_clip, clip_at,
+                        maxiter, tol, theta, stats, iters, converged);
+  // sharded: the host loop (every rank runs the same iterations)
+  std::vector<double> g((size_t)P), mom1((size_t)P, 0.0), mom2((size_t)P, 0.0);
   int it = 0;
   for (it = 1; it <= maxiter; ++it) {
     double st[2], mu = 0.0;

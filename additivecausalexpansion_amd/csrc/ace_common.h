@@ -303,6 +303,9 @@ struct ShardModel;
 void shard_unique_id(unsigned char *id);  // throws std::runtime_error
 ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int rank,
                          const unsigned char *id);
+// host-callback collectives (ace_model_create_sharded_host)
+ShardModel *shard_create_host(ace_ctx *ctx, const Shape &s, int64_t n, int world, int rank,
+                              const ace_comm_ops &ops);
 void shard_destroy(ShardModel *m);
 void shard_set_data(ShardModel *m, const double *y, const double *X, const double *Z);
 void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool timed,

@@ -44,6 +44,9 @@ struct Tile {
 // lam[b] = theta[2+b].  Total 2*B*PM + B doubles.
 struct TabView {
   const double *wk, *wg, *lam;
+  // device exp(theta[0]) (the device-fused training loop's theta lives in
+  // HBM); null: the kernels' host `sig` argument
+  const double *sig = nullptr;
 };
 
 // Row-side / column-side operand of a pair kernel (row-major, padded).
@@ -199,20 +202,47 @@ hipError_t launch_alpha_from_vec(const double *vec, int64_t npad, int64_t n,
                                  double theta1, int use_mu_solution, double *alpha,
                                  double *scal, hipStream_t st);
 hipError_t launch_add(const double *x, double *y, int64_t count, hipStream_t st);
-// alpha = u - mu_eff * v, u/v read from A's AUG rows; mu_eff = theta1, or
-// 0.5*yK1/1K1 when use_mu_solution; writes scal[0..2] = {yKy, yK1, 1K1},
-// scal[3] = mu_solution, scal[4] = mu_eff.
+// alpha = u - mu_eff * v, u/v read from A's AUG rows; mu_eff = theta1 (or
+// *theta1p, a device scalar, when given), or 0.5*yK1/1K1 when
+// use_mu_solution; writes scal[0..2] = {yKy, yK1, 1K1}, scal[3] =
+// mu_solution, scal[4] = mu_eff.
 hipError_t launch_alpha_from_aug(const double *A, int64_t ld, int64_t npad,
                                  int64_t n, double theta1, int use_mu_solution,
-                                 double *alpha, double *scal, hipStream_t st);
+                                 double *alpha, double *scal, hipStream_t st,
+                                 const double *theta1p = nullptr);
 hipError_t launch_colsum(const double *in, int64_t nrows, int ncols,
                          double *out, hipStream_t st);
 // sums[0] = sum (ybar - s)^2, sums[1] = sum y*alpha, sums[2] = sum alpha,
 // sums[3] = sum log(piv[0..npiv)), with ybar = y - *mu (device scalar).
-// s == nullptr: ybar - s = sig * alpha (fused model, A = Kfull + sig I).
+// s == nullptr: ybar - s = sig * alpha (fused model, A = Kfull + sig I);
+// sigp (device scalar) replaces sig when given.
 hipError_t launch_final_sums(const double *y, const double *mu, const double *alpha,
                              const double *s, double sig, int64_t n, const double *piv,
-                             int64_t npiv, double *sums, hipStream_t st);
+                             int64_t npiv, double *sums, hipStream_t st,
+                             const double *sigp = nullptr);
+// ---- device-fused training loop (ace_train.hip) -----------------------------
+// theta tables of make_tab (ace_common.h) from a device theta, plus
+// tab[2 B PM + B] = exp(theta[0]) (TabView::sig)
+hipError_t launch_make_tab(const double *theta, int B, int p, int PM, double *tab,
+                           hipStream_t st);
+struct TrainCfg {
+  int optimizer;  // ace_optimizer
+  double lr, momentum, beta1, beta2;
+  int clip;
+  double clip_at, tol;
+  int P, B, p, PM, kind;
+  int64_t n;
+  double std_y;
+};
+// One iteration's host-side tail of ace_model_train on the device (one
+// workgroup): compose_grad + stats of para_update, norm clip, optimizer step,
+// the mu overwrite and the convergence test.  st = [theta | m1 | m2 | g]
+// (4 P), hist = the stats matrix (2 x (maxiter + 2)), ctl = {last iteration
+// done, stop: 0 running / 1 converged / 2 non-finite gradient}.  Once ctl[1]
+// is set, later launches change nothing.
+hipError_t launch_train_step(const TrainCfg &c, int it, const double *gsum, const double *sums,
+                             const double *scal, const int *flag, double *st, double *hist,
+                             int *ctl, hipStream_t stream);
 // y = M x for M (m x k, col-major ld) ; y = M^T x
 hipError_t launch_gemv(const double *M, int64_t ld, int64_t m, int64_t k,
                        const double *x, double *y, hipStream_t st);

@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void k_assembly(PairSide R, PairSide C, int64_
       }
     }
     if (MODE == 0) {
-      out[r + c * ld] = (r == c) ? kf + sig : kf;
+      out[r + c * ld] = (r == c) ? kf + (tab.sig ? *tab.sig : sig) : kf;
       if (cube) cube[r + c * ld] = kf;  // Kfull copy for the RMSE product (the sweep
                                         // overwrites out)
     } else {

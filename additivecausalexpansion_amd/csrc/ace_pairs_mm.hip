@@ -379,6 +379,7 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
                                                 const Tile *__restrict__ tiles, int G, int part,
                                                 int nt) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
+  const double sg = tab.sig ? *tab.sig : sig;  // exp(theta[0]) on the diagonal
   int64_t I, J;
   // part 1: the tiles of the first panel's columns (J < NB / AT, column by
   // column) -- what the sweep's first pivot chain needs; part 2: the rest
@@ -461,7 +462,7 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
     for (int v = 0; v < 4; ++v) {
       const int64_t c = C0 + 16 * cb + lk + 4 * v;
       if (r < n && c < n) {
-        out[r + c * ld] = (r == c) ? kf[cb][v] + sig : kf[cb][v];
+        out[r + c * ld] = (r == c) ? kf[cb][v] + sg : kf[cb][v];
         if (kcopy) kcopy[r + c * ld] = kf[cb][v];
       } else {
         out[r + c * ld] = (r == c) ? 1.0 : 0.0;  // identity padding

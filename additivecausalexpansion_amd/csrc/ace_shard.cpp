@@ -97,6 +97,41 @@ void nck(ace_ctx *ctx, ncclResult_t e, const char *what) {
   throw Fail{ACE_ERR_HIP};
 }
 
+// Host-callback collectives: stage through host buffers (the stream is
+// synchronised first; the copies back are synchronous too).
+void hck(ace_ctx *ctx, int rc, const char *what) {
+  if (rc == 0) return;
+  ctx->err = std::string(what) + ": host collective returned " + std::to_string(rc);
+  throw Fail{ACE_ERR_HIP};
+}
+
+void host_bcast(ace_ctx *ctx, const ace_comm_ops &o, double *dbuf, size_t count, int root,
+                hipStream_t st) {
+  std::vector<double> h(count);
+  ck(ctx, hipStreamSynchronize(st), "sync");
+  ck(ctx, hipMemcpy(h.data(), dbuf, count * sizeof(double), hipMemcpyDeviceToHost), "stage");
+  hck(ctx, o.broadcast(o.user, h.data(), (int64_t)count, root), "broadcast");
+  ck(ctx, hipMemcpy(dbuf, h.data(), count * sizeof(double), hipMemcpyHostToDevice), "unstage");
+}
+
+void host_allgather(ace_ctx *ctx, const ace_comm_ops &o, const double *dsend, double *drecv,
+                    size_t count, int world, hipStream_t st) {
+  std::vector<double> hs(count), hr(count * (size_t)world);
+  ck(ctx, hipStreamSynchronize(st), "sync");
+  ck(ctx, hipMemcpy(hs.data(), dsend, count * sizeof(double), hipMemcpyDeviceToHost), "stage");
+  hck(ctx, o.allgather(o.user, hs.data(), hr.data(), (int64_t)count), "allgather");
+  ck(ctx, hipMemcpy(drecv, hr.data(), hr.size() * sizeof(double), hipMemcpyHostToDevice), "unstage");
+}
+
+void host_allreduce(ace_ctx *ctx, const ace_comm_ops &o, double *dbuf, size_t count, int op,
+                    hipStream_t st) {
+  std::vector<double> h(count);
+  ck(ctx, hipStreamSynchronize(st), "sync");
+  ck(ctx, hipMemcpy(h.data(), dbuf, count * sizeof(double), hipMemcpyDeviceToHost), "stage");
+  hck(ctx, o.allreduce(o.user, h.data(), (int64_t)count, op), "allreduce");
+  ck(ctx, hipMemcpy(dbuf, h.data(), count * sizeof(double), hipMemcpyHostToDevice), "unstage");
+}
+
 // ------------------------------------------------------------------ rank
 struct RankState {
   int r = 0;
@@ -116,7 +151,9 @@ struct ShardModel {
   Shape s{};
   int64_t n = 0, npad = 0, naug = 0, ntr = 0;
   int G = 1, rank = 0;
-  bool sim = true;
+  bool sim = true;    // every rank simulated in this process (device copies)
+  bool host = false;  // host-callback collectives (ace_comm_ops)
+  ace_comm_ops ops{};
   ncclComm_t comm = nullptr;
   std::vector<std::unique_ptr<RankState>> ranks;  // 1 (RCCL) or G (simulated)
   DBuf vote;                                       // shard_any: one double
@@ -202,6 +239,12 @@ void exchange(ShardModel &m, int k, hipStream_t st) {
   const int slots = shard_row_slots(k, m.G);
   const size_t nrow = (size_t)slots * NB * NB;
   const int root = k % m.G;
+  if (m.host) {
+    RankState &R = *m.ranks[0];
+    host_bcast(ctx, m.ops, R.low.d(), nlow, root, st);
+    if (nrow > 0) host_allgather(ctx, m.ops, R.send.d(), R.recv.d(), nrow, m.G, st);
+    return;
+  }
   if (!m.sim) {
     RankState &R = *m.ranks[0];
     nck(ctx, rccl().GroupStart(), "ncclGroupStart");
@@ -232,6 +275,10 @@ void exchange(ShardModel &m, int k, hipStream_t st) {
 void allreduce(ShardModel &m, int which, int64_t count, hipStream_t st) {
   ace_ctx *ctx = m.ctx;
   auto buf = [&](RankState &R) { return which == 0 ? R.augvec.d() : R.red.d(); };
+  if (m.host) {
+    host_allreduce(ctx, m.ops, buf(*m.ranks[0]), (size_t)count, 0, st);
+    return;
+  }
   if (!m.sim) {
     double *b = buf(*m.ranks[0]);
     nck(ctx, rccl().AllReduce(b, b, (size_t)count, ncclDouble, ncclSum, m.comm, st),
@@ -252,16 +299,18 @@ void allreduce(ShardModel &m, int which, int64_t count, hipStream_t st) {
 void run_sweep_sharded(ShardModel &m, int which, bool timed) {
   ace_ctx *ctx = m.ctx;
   hipStream_t st = ctx->stream;
-  // the simulated group runs everything in order on one stream
-  hipStream_t side = m.sim ? st : ctx->side;
+  // the simulated and the host-callback groups run everything in order on
+  // one stream (their exchanges are synchronous)
+  const bool lookahead = !m.sim && !m.host;
+  hipStream_t side = lookahead ? ctx->side : st;
   const int steps = (int)(m.npad / NB);
   std::vector<ShardSweep> v;
   for (auto &R : m.ranks) v.push_back(sweep_view(m, *R, which));
   auto rec = [&](int idx, hipStream_t s) {
-    if (!m.sim) ck(ctx, hipEventRecord(m.ev[(size_t)idx], s), "event");
+    if (lookahead) ck(ctx, hipEventRecord(m.ev[(size_t)idx], s), "event");
   };
   auto wait = [&](hipStream_t s, int idx) {
-    if (!m.sim) ck(ctx, hipStreamWaitEvent(s, m.ev[(size_t)idx], 0), "event wait");
+    if (lookahead) ck(ctx, hipStreamWaitEvent(s, m.ev[(size_t)idx], 0), "event wait");
   };
   auto prepare = [&](int k, int buf) {  // panel k into buffer buf, on `side`
     for (auto &b : v) ck(ctx, shard_pack(b, k, side), "shard pack");
@@ -311,8 +360,9 @@ void shard_unique_id(unsigned char *id) {
   std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
 }
 
-ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int rank,
-                         const unsigned char *id) {
+namespace {
+ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world, int rank,
+                             const unsigned char *id, const ace_comm_ops *ops) {
   std::unique_ptr<ShardModel> m(new ShardModel());
   m->ctx = ctx;
   m->s = s;
@@ -322,9 +372,11 @@ ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int
   m->ntr = (n + AT - 1) / AT;
   m->G = world;
   m->rank = rank;
-  m->sim = id == nullptr;
+  m->host = ops != nullptr;
+  if (ops) m->ops = *ops;
+  m->sim = id == nullptr && !m->host;
   const int64_t naug = m->naug, npad = m->npad;
-  if (!m->sim) {
+  if (!m->sim && !m->host) {
     if (!rccl().ok) {
       ctx->err = rccl().err;
       throw Fail{ACE_ERR_HIP};
@@ -397,6 +449,17 @@ ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int
   }
   sync(ctx);
   return m.release();
+}
+}  // namespace
+
+ShardModel *shard_create(ace_ctx *ctx, const Shape &s, int64_t n, int world, int rank,
+                         const unsigned char *id) {
+  return shard_create_any(ctx, s, n, world, rank, id, nullptr);
+}
+
+ShardModel *shard_create_host(ace_ctx *ctx, const Shape &s, int64_t n, int world, int rank,
+                              const ace_comm_ops &ops) {
+  return shard_create_any(ctx, s, n, world, rank, nullptr, &ops);
 }
 
 void shard_destroy(ShardModel *m) { delete m; }
@@ -515,6 +578,8 @@ void shard_get_inverse(ShardModel *m, double *inv) {
       ck(ctx, hipMemcpyAsync(gath.d() + (size_t)R->r * slot, R->A[0].p, (size_t)slot * sizeof(double),
                              hipMemcpyDeviceToDevice, st),
          "gather local columns");
+  } else if (m->host) {
+    host_allgather(ctx, m->ops, m->ranks[0]->A[0].d(), gath.d(), (size_t)slot, m->G, st);
   } else {
     nck(ctx, rccl().AllGather(m->ranks[0]->A[0].p, gath.p, (size_t)slot, ncclDouble, m->comm, st),
         "ncclAllGather (inverse)");
@@ -557,6 +622,11 @@ int shard_any(ShardModel *m, int local) {
   if (m->sim) return local;
   ace_ctx *ctx = m->ctx;
   hipStream_t st = ctx->stream;
+  if (m->host) {
+    double v = local ? 1.0 : 0.0;
+    hck(ctx, m->ops.allreduce(m->ops.user, &v, 1, 1), "allreduce (interrupt vote)");
+    return v != 0.0;
+  }
   alloc(ctx, m->vote, sizeof(double), "alloc vote");
   double v = local ? 1.0 : 0.0;
   ck(ctx, hipMemcpyAsync(m->vote.p, &v, sizeof(double), hipMemcpyHostToDevice, st), "vote up");
@@ -578,6 +648,10 @@ int shard_rank_of(const ShardModel *m, int j) { return m->ranks[(size_t)j]->r; }
 // sum their local partials themselves, so only RCCL has work to do.
 void shard_allreduce_sum(ShardModel *m, double *buf, int64_t count) {
   if (m->sim || count <= 0) return;
+  if (m->host) {
+    host_allreduce(m->ctx, m->ops, buf, (size_t)count, 0, m->ctx->stream);
+    return;
+  }
   nck(m->ctx, rccl().AllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, m->comm,
                                m->ctx->stream),
       "ncclAllReduce");

@@ -130,12 +130,13 @@ hipError_t launch_add(const double *x, double *y, int64_t count, hipStream_t st)
 
 __global__ void k_alpha_from_aug(const double *__restrict__ A, int64_t ld, int64_t npad,
                                  int64_t n, double theta1, int use_mu,
-                                 double *__restrict__ alpha, double *__restrict__ scal) {
+                                 double *__restrict__ alpha, double *__restrict__ scal,
+                                 const double *__restrict__ theta1p) {
   const double yKy = -A[npad + npad * ld];
   const double yK1 = -A[(npad + 1) + npad * ld];
   const double oK1 = -A[(npad + 1) + (npad + 1) * ld];
   const double mu = 0.5 * yK1 / oK1;  // Q4 (src/utilities_cpp.cpp:9)
-  const double mu_eff = use_mu ? mu : theta1;
+  const double mu_eff = use_mu ? mu : (theta1p ? *theta1p : theta1);
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j < n) {
     const double u = A[npad + j * ld];
@@ -153,9 +154,9 @@ __global__ void k_alpha_from_aug(const double *__restrict__ A, int64_t ld, int64
 
 hipError_t launch_alpha_from_aug(const double *A, int64_t ld, int64_t npad, int64_t n,
                                  double theta1, int use_mu, double *alpha, double *scal,
-                                 hipStream_t st) {
+                                 hipStream_t st, const double *theta1p) {
   hipLaunchKernelGGL(k_alpha_from_aug, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A,
-                     ld, npad, n, theta1, use_mu, alpha, scal);
+                     ld, npad, n, theta1, use_mu, alpha, scal, theta1p);
   return hipGetLastError();
 }
 
@@ -232,9 +233,11 @@ __global__ __launch_bounds__(1024) void k_final_sums(const double *__restrict__ 
                                                     const double *__restrict__ alpha,
                                                     const double *__restrict__ s, double sig,
                                                     int64_t n, const double *__restrict__ piv,
-                                                    int64_t npiv, double *__restrict__ sums) {
+                                                    int64_t npiv, double *__restrict__ sums,
+                                                    const double *__restrict__ sigp) {
   __shared__ double sh[16];
   const double mu = *mup;
+  if (sigp) sig = *sigp;
   double e2 = 0.0, ya = 0.0, sa = 0.0, ld = 0.0;
   for (int64_t x = threadIdx.x; x < n; x += 1024) {
     const double ybar = y[x] - mu;
@@ -258,9 +261,9 @@ __global__ __launch_bounds__(1024) void k_final_sums(const double *__restrict__ 
 
 hipError_t launch_final_sums(const double *y, const double *mu, const double *alpha, const double *s,
                              double sig, int64_t n, const double *piv, int64_t npiv,
-                             double *sums, hipStream_t st) {
+                             double *sums, hipStream_t st, const double *sigp) {
   hipLaunchKernelGGL(k_final_sums, dim3(1), dim3(1024), 0, st, y, mu, alpha, s, sig, n, piv, npiv,
-                     sums);
+                     sums, sigp);
   return hipGetLastError();
 }
 

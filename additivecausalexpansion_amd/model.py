@@ -22,18 +22,27 @@ class DeviceModel:
     """ace_model handle: one fit's resident data and the last inverse."""
 
     def __init__(self, kind, n, p, B, ctx=None, world=1, rank=0, unique_id=None,
-                 sharded=False):
+                 sharded=False, host_comm=None):
         """sharded=False: one GPU (ace_model_create).  sharded=True: rank
         `rank` of a `world`-rank block-column-sharded model
         (ace_model_create_sharded): unique_id = the 128 bytes rank 0 got from
         comm_unique_id() (RCCL, one process per GPU), or None to simulate all
-        ranks in this process (validation mode)."""
+        ranks in this process (validation mode).  host_comm (a HostComm):
+        the collectives go through torch.distributed on host buffers
+        (ace_model_create_sharded_host; validation over gloo)."""
         self.ctx = ctx or default_context()
         self.kind, self.n, self.p, self.B = kind, n, p, B
         self.P = 2 + B * (p + 1)
         self.world, self.rank = (world, rank) if sharded else (1, 0)
         h = ctypes.c_void_p()
-        if sharded:
+        if sharded and host_comm is not None:
+            self._host_comm = host_comm  # keeps the callbacks alive
+            check(lib().ace_model_create_sharded_host(self.ctx.handle, KIND[kind], n, p, B,
+                                                      int(world), int(rank),
+                                                      ctypes.byref(host_comm.ops),
+                                                      ctypes.byref(h)),
+                  self.ctx.handle)
+        elif sharded:
             if unique_id is not None and len(unique_id) != UNIQUE_ID_BYTES:
                 raise ValueError("unique_id must be 128 bytes")
             check(lib().ace_model_create_sharded(self.ctx.handle, KIND[kind], n, p, B, int(world),

@@ -134,12 +134,17 @@ def cpu_baseline(cfg, timeout=240):
     """Rank 0 / N=1 only: the oracle leg in a subprocess (bounded)."""
     from additivecausalexpansion_amd.synthetic import CONFIGS
     n, p, B, kernel = CONFIGS[cfg]
+    import glob
+    fits = _newest_first_last(glob.glob(os.path.join(ROOT, "profiles", "r*_cpu_baseline.json")))
     cmd = [sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), "--n", str(n),
            "--p", str(p), "--B", str(B), "--kernel", kernel, "--sample-n", "1536"]
+    if fits:  # extrapolate with the measured exponents (oracle/cpu_scaling.py)
+        cmd += ["--fit", fits[-1]]
     try:
         out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, check=True)
         d = json.loads(out.stdout.strip().splitlines()[-1])
-        return {k: d[k] for k in ("value", "unit", "cores", "kind", "sample")}
+        return {k: d[k] for k in ("value", "unit", "cores", "kind", "sample", "measured_fit")
+                if k in d}
     except Exception as e:  # the baseline is reported, never required
         return {"value": None, "unit": "evals/s", "cores": None, "kind": "port",
                 "sample": f"failed: {type(e).__name__}: {e}"[:300]}
@@ -174,6 +179,7 @@ def make_step(kernel, p, B, theta, std_y, ctx, y, X, Z, model=None):
     def step():
         state["it"] += 1
         return k.para_update(state["it"], y, X, Z, opt, verbose=False)
+    step.kernel_object = k
     return step, model
 
 
@@ -189,6 +195,36 @@ def timed_steps(dist, step, steps, warmup, model, profile=True):
     _barrier_sync(dist)
     dt = time.perf_counter() - t0
     return _allreduce_max(dist, dt), stats
+
+
+def predict_leg(k, model, p, B, nx=4096, reps=3):
+    """Device prediction with the fit's resident inverse (Q6: the inverse of
+    the last para_update, kernels at the current theta): pred_cpp and
+    pred_marginal_cpp + ATE/ATT/ATU at nx test points against the n training
+    points (R/kernel_SE_R6.R:75-97, src/pred_cpp.cpp:8-126).  Each call
+    uploads X2 / Z2 (nx x (p + B - 1) doubles) and returns nx-long vectors
+    over PCIe; the n x nx cross kernel and the A^-1 products stay in HBM."""
+    import numpy as np
+    from additivecausalexpansion_amd.synthetic import make_problem
+    _, X2, Z2, _, _ = make_problem(nx, p, B, seed=77)
+    dZ2 = np.asfortranarray(0.5 * Z2)
+    zx = (np.arange(nx) % 3 == 0).astype(float)
+    out = {"nx": nx, "n_train": model.n, "reps": reps,
+           "note": "wall time per call incl. X2/Z2 upload and result download (small)"}
+    calls = {
+        "predict": lambda: model.predict(k.parameters, X2, Z2, 0.1, 1.3),
+        "predict_marginal_ate": lambda: model.predict_marginal(k.parameters, X2, dZ2, zx, 1.3,
+                                                               0.7, True),
+    }
+    for name, fn in calls.items():
+        fn()  # warm (kernel tables, scratch)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = fn()
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        out[name] = {"ms": ms, "points_per_s": nx / (ms * 1e-3),
+                     "finite": bool(np.all(np.isfinite(r["map"])) and np.all(np.isfinite(r["var"])))}
+    return out
 
 
 def run_sharded(dist, rank, world, ctx, steps, warmup, name=None):
@@ -271,6 +307,7 @@ def main():
     asm_ms, _, asm_work = model.kernel_time(1)
     grad_ms, _, grad_work = model.kernel_time(2)
     model.profile(False)
+    pred = predict_leg(step.kernel_object, model, p, B) if rank == 0 else None
 
     line = None
     if rank == 0:
@@ -321,6 +358,7 @@ def main():
                 "gradient": grad_work / (grad_ms * 1e-3) / 1e12 if grad_ms else None},
             "pair_kernels_hbm_gbs": pair_hbm_gbs(asm_ms / a.steps, grad_ms / a.steps),
             "last_stats": [float(stats[0]), float(stats[1])],
+            "predict": pred,
         }
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(a.config)

@@ -343,6 +343,26 @@ int ace_model_create_sharded(ace_ctx *ctx, int kind, int64_t n, int p, int B,
 /* world / rank of a model (1 / 0 for ace_model_create models) */
 int ace_model_shard_info(const ace_model *m, int *world, int *rank);
 
+/* Host-callback collectives: the same sharded model with every exchange
+ * (panel broadcast + all-gather per sweep step, the two all-reduces per
+ * evaluation, the interrupt vote, the inverse gather) routed through
+ * caller-supplied functions on HOST buffers -- the library stages device ->
+ * host, calls, and copies back.  One process per rank with its own ace_ctx
+ * (any devices, also one shared GPU); for validating the per-process
+ * packing / ownership logic over a CPU transport such as gloo (not a
+ * performance path: every step synchronises).  Callbacks return 0 on
+ * success; op of allreduce: 0 = sum, 1 = max.  allgather: recv holds
+ * world x count doubles, rank r's block at r * count. */
+typedef struct ace_comm_ops {
+  void *user;
+  int (*broadcast)(void *user, double *buf, int64_t count, int root);
+  int (*allgather)(void *user, const double *send, double *recv, int64_t count);
+  int (*allreduce)(void *user, double *buf, int64_t count, int op);
+} ace_comm_ops;
+int ace_model_create_sharded_host(ace_ctx *ctx, int kind, int64_t n, int p, int B,
+                                  int world, int rank, const ace_comm_ops *ops,
+                                  ace_model **out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,6 +7,10 @@ workload, and extrapolates to the full size:
     the reference): the literal C restatement oracle/ace_ref.c, scaled by n^2;
   * invkernel_cpp (eig_sym = LAPACK dsyevd, then V D^-1/2 (V D^-1/2)^T):
     numpy.linalg.eigh + matmul on all host BLAS threads, scaled by n^3.
+The extrapolation exponents come from the measured scaling fit committed in
+profiles/r*_cpu_baseline.json (oracle/cpu_scaling.py: full evaluations at
+n = 2048, 4096, 8192 on the GPU box's host) when one is present -- the pair
+loops grow faster than n^2 there (cube traffic) -- else n^2 / n^3.
 Prints one JSON line.  PARITY UNPINNED note: see oracle/ace_oracle.py.
 """
 from __future__ import annotations
@@ -31,7 +35,13 @@ def main():
     ap.add_argument("--p", type=int, default=20)
     ap.add_argument("--B", type=int, default=10)
     ap.add_argument("--kernel", default="Matern32")
+    ap.add_argument("--fit", default=None, help="measured scaling fit (JSON of cpu_scaling.py)")
     a = ap.parse_args()
+    e_pairs, e_inv, fit = 2.0, 3.0, None
+    if a.fit and os.path.exists(a.fit):
+        fit = json.load(open(a.fit))
+        e_pairs = fit["fit"]["pairs"]["exponent"]
+        e_inv = fit["fit"]["inverse_eigh"]["exponent"]
 
     import numpy as np
 
@@ -70,22 +80,34 @@ def main():
     L.ref_grad(kind, n, p, B, P(y), P(X), P(Kf), P(Ke), P(inv), float(np.sum(np.log(w))), P(th),
                P(st), sy, P(g))
     t_grad = time.perf_counter() - t0
-    s2 = (a.n / n) ** 2
-    s3 = (a.n / n) ** 3
+    s2 = (a.n / n) ** e_pairs
+    s3 = (a.n / n) ** e_inv
     t_full = (t_asm + t_grad) * s2 + t_inv * s3
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
     try:
         cpu = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":")[1].strip()
     except Exception:
         cpu = "unknown"
-    print(json.dumps({
+    out = {
         "value": 1.0 / t_full, "unit": "evals/s", "cores": threads, "kind": "port",
         "sample": (f"one {a.kernel} eval at n={n}, p={p}, B={B} (sample of n={a.n}): pair loops "
-                   f"{t_asm + t_grad:.2f} s single-thread x (n/{n})^2, eigh+inverse {t_inv:.2f} s "
-                   f"on {threads} BLAS threads x (n/{n})^3 -> {t_full:.1f} s per eval; "
-                   f"host CPU: {cpu}"),
+                   f"{t_asm + t_grad:.2f} s single-thread x (n/{n})^{e_pairs:.2f}, eigh+inverse "
+                   f"{t_inv:.2f} s on {threads} BLAS threads x (n/{n})^{e_inv:.2f} -> {t_full:.1f} s "
+                   f"per eval (exponents: " +
+                   (f"measured fit {os.path.basename(a.fit)}" if fit else "n^2 / n^3") +
+                   f"); host CPU: {cpu}"),
         "sample_seconds": {"assembly": t_asm, "inverse": t_inv, "gradient": t_grad},
-        "extrapolated_seconds_per_eval": t_full}))
+        "extrapolated_seconds_per_eval": t_full}
+    if fit:
+        out["measured_fit"] = {
+            "source": os.path.relpath(a.fit, os.path.dirname(HERE)),
+            "exponents": {k: v["exponent"] for k, v in fit["fit"].items()},
+            "points_seconds_per_eval": {str(q["n"]): q["eval_reference"]
+                                        for q in fit["points_c2_shape"]},
+            "c2_seconds_per_eval_reference": fit["c2_extrapolated"]["seconds_per_eval_reference"],
+            "c2_seconds_per_eval_best_cpu": fit["c2_extrapolated"]["seconds_per_eval_best_cpu"],
+            "c1_median_seconds": fit["c1_measured"]}
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":

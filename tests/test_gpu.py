@@ -347,21 +347,27 @@ def test_ace_train_and_predict_end_to_end(A):
 @pytest.mark.parametrize("optimizer,kernel", [("Nadam", "SE"), ("Adam", "Matern32"),
                                               ("NAG", "SE")])
 def test_native_training_loop_matches_python_loop(A, optimizer, kernel):
-    """ace_model_train (the R loop of R/main_ace.R:213-235 inside the library)
-    and the Python mirror of the same loop call the same native para_update
-    and optimizer routines, so their trajectories agree bit for bit, including
-    the stopping iteration and the final train stats."""
+    """ace_model_train (the R loop of R/main_ace.R:213-235 fused on the
+    device, tests/test_train_gpu.py) and the host-driven Python mirror of the
+    loop (native para_update + host optimizer) follow the same trajectory to
+    the training tolerances, with the same stopping iteration.  (The golden
+    trajectory check of the device loop is in tests/test_train_gpu.py.)"""
     from additivecausalexpansion_amd.synthetic import readme_data
     y, X, Z = readme_data(seed=9, n=250)
     kw = dict(kernel=kernel, basis="cubic", n_knots=2, optimizer=optimizer, maxiter=40,
               tol=1e-3, learning_rate=0.02, momentum=0.5, norm_clip=True, verbose=False)
     f_py = A.ace_train(y, X, Z, **kw)
     f_nat = A.ace_train(y, X, Z, native_loop=True, **kw)
-    assert np.array_equal(f_nat["train_stats"]["stats"], f_py["train_stats"]["stats"])
+    s_nat, s_py = f_nat["train_stats"]["stats"], f_py["train_stats"]["stats"]
+    assert s_nat.shape == s_py.shape
+    close(s_nat, s_py, 1e-6, 1e-9)
     assert f_nat["train_stats"]["convergence"] == f_py["train_stats"]["convergence"]
-    assert np.array_equal(f_nat["Kernel"].parameters, f_py["Kernel"].parameters)
+    # the two loops round their tables (device vs host exp) and the clip norm
+    # (block vs sequential sum) differently; 40 optimizer steps amplify that
+    # to a few 1e-5 of a parameter (NAG has no sqrt(v) normalisation)
+    close(f_nat["Kernel"].parameters, f_py["Kernel"].parameters, 1e-4, 1e-9)
     p_nat, p_py = A.predict_ace(f_nat), A.predict_ace(f_py)
-    assert np.array_equal(p_nat["map"], p_py["map"])
+    close(p_nat["map"], p_py["map"], 1e-5, 1e-6)
 
 
 def test_native_training_loop_nonfinite_stops(A):

@@ -1,0 +1,99 @@
+"""The sharded HIP path in several processes: each rank
+is its own process with its own ace_ctx (all on the box's one GPU), and the
+panel broadcast / all-gather of every sweep step plus the per-evaluation
+all-reduces go through gloo via host-callback collectives
+(ace_model_create_sharded_host).  Unlike the in-process simulated group this
+exercises the per-process packing, ownership masks, tile lists and the
+one-local-rank code paths of ace_shard.cpp -- everything RCCL runs, except
+the transport.  Checked against the single-GPU model and the oracle.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+from test_gpu import close
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def A():
+    import additivecausalexpansion_amd as pkg
+    pkg.default_context()
+    return pkg
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import ace_oracle
+    return ace_oracle
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_group(world, out, kind, n, p, B):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), LOCAL_RANK="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "hostcomm_worker.py"),
+                                       out, kind, str(n), str(p), str(B)], env=env))
+    rcs = []
+    for pr in procs:
+        try:
+            rcs.append(pr.wait(timeout=100))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert rcs == [0] * world, rcs
+    return dict(np.load(out))
+
+
+@pytest.mark.parametrize("world,kind,n,p,B", [(2, "SE", 700, 3, 4), (3, "Matern32", 900, 5, 5)])
+def test_sharded_processes_match_single_gpu_and_oracle(A, O, tmp_path, world, kind, n, p, B):
+    r = _run_group(world, str(tmp_path / "r.npz"), kind, n, p, B)
+    y, X, Z, sy = r["y"], r["X"], r["Z"], float(r["sy"][0])
+    # every rank returned the same gradient
+    for q in range(1, world):
+        assert np.array_equal(r["g2_all_ranks"][q], r["g2_all_ranks"][0])
+    # the single-GPU model on the same data and thetas
+    m = A.DeviceModel(kind, n, p, B)
+    m.set_data(y, X, Z, sy)
+    th1 = r["theta1"].copy()
+    th1[1] = 0.0  # para_update(1) overwrote theta[1] with mu: restart from the input
+    g1, st1, mu1 = m.para_update(1, th1)
+    close(th1, r["theta1"], 1e-8, 1e-12)
+    close(g1, r["g1"], 1e-8, 1e-9)
+    close(st1, r["st1"], 1e-8, 1e-9)
+    assert mu1 == pytest.approx(float(r["mu1"][0]), rel=1e-8)
+    g2, st2, _ = m.para_update(2, r["theta2"].copy())
+    close(g2, r["g2"], 1e-8, 1e-9)
+    close(st2, r["st2"], 1e-8, 1e-9)
+    # the sharded sweep forms W with the operands swapped:
+    # inverse entries agree to a few 1e-9 of the largest one
+    close(m.apply_inverse(r["V"]), r["AinvV"], 1e-7, 1e-8)
+    close(np.diag(m.inverse()), r["inv_diag"], 1e-7, 1e-8)
+    close(m.train_stats(r["theta2"]), r["train_stats"], 1e-8, 1e-9)
+    pr = m.predict(r["theta2"], r["X2"], r["Z2"], 0.3, 1.2)
+    close(pr["map"], r["pred_map"], 1e-8, 1e-10)
+    close(pr["var"], r["pred_var"], 1e-7, 1e-10)
+    # the oracle at theta2 (gradient and stats of para_update)
+    th2 = r["theta2"]
+    sym = O.kernmat_SE_symmetric_cpp if kind == "SE" else O.kernmat_Matern32_symmetric_cpp
+    grad = O.grad_SE_cpp if kind == "SE" else O.grad_Matern_cpp
+    K = sym(X, Z, th2)
+    inv = O.invkernel_cpp(K["full"], th2[0])
+    st = np.zeros(2)
+    g = grad(y, X, Z, K["full"], K["elements"], inv["inv"], inv["eigenval"], th2.copy(), st, B, sy)
+    close(r["g2"], g, 1e-6, 1e-9)
+    close(r["st2"], st, 1e-6, 1e-9)
