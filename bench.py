@@ -386,6 +386,10 @@ def main():
         timer.cancel()
         if line is not None:
             line["sharded"] = sh
+            # SURVEY §8d's weak-scaling efficiency of ONE sharded evaluation
+            # (the headline value above is N independent replicas)
+            line["sharded_evals_per_s"] = sh.get("evals_per_s")
+            line["sharded_weak_scaling_efficiency"] = sh.get("weak_scaling_efficiency")
     if line is not None:
         print(json.dumps(line), flush=True)
     if failed:  # peers may be stuck in a collective: no barrier
