@@ -132,7 +132,17 @@ struct SweepBufs {
   int *flag;      // set to 1 on a non-positive / non-finite pivot
   const Tile *order = nullptr;  // k_update tile order (xcd_update_order), or row-major
   int64_t norder = 0;
+  // lookahead cross update on k_update's 128-tiles (cross_update_tiles):
+  // device list of every step's cross tiles, host offsets (steps + 1); null:
+  // k_update_x on 64-tiles
+  const Tile *xtiles = nullptr;
+  const int64_t *xoff = nullptr;
 };
+// The lower 128-tiles with I or J in block k+1, for k = 0 .. steps-2,
+// concatenated (each step's list dealt to the XCDs like the bulk order);
+// off[k] .. off[k+1] is step k's range.  ACE_XUPD=0 selects k_update_x.
+bool cross_update_on_tiles();
+std::vector<Tile> cross_update_tiles(int64_t naug, int steps, std::vector<int64_t> &off);
 // k_update tile order: the tiles of `tl` grouped into S x S super-blocks of
 // 128-tiles that are dealt whole to the 8 XCDs; list index b runs on XCD
 // b % 8 (dispatch is round-robin).  Entries with I < 0 are padding.

@@ -8,7 +8,8 @@
 
 // Buffers of one Gauss-Jordan sweep and its lookahead events.
 struct SweepWork {
-  DBuf A, P0, P1, W0, W1, SW, S0, S1, piv, flag, order;
+  DBuf A, P0, P1, W0, W1, SW, S0, S1, piv, flag, order, xtiles;
+  std::vector<int64_t> xoff;
   std::vector<hipEvent_t> ev;
   int64_t n = 0, npad = 0, naug = 0, norder = 0;
   SweepWork() = default;
@@ -35,6 +36,14 @@ struct SweepWork {
          "upload tile order");
       norder = (int64_t)t.size();
     }
+    xoff.clear();
+    if (cross_update_on_tiles()) {
+      const std::vector<Tile> t = cross_update_tiles(naug, (int)(npad / NB), xoff);
+      alloc(ctx, xtiles, std::max<size_t>(t.size(), 1) * sizeof(Tile), "alloc cross tiles");
+      if (!t.empty())
+        ck(ctx, hipMemcpy(xtiles.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
+           "upload cross tiles");
+    }
     const size_t need = (size_t)(2 * (npad / NB) + 1);
     while (ev.size() < need) {
       hipEvent_t e;
@@ -58,6 +67,10 @@ struct SweepWork {
     b.flag = flag.i();
     b.order = norder ? reinterpret_cast<const Tile *>(order.p) : nullptr;
     b.norder = norder;
+    if (!xoff.empty()) {
+      b.xtiles = reinterpret_cast<const Tile *>(xtiles.p);
+      b.xoff = xoff.data();
+    }
     return b;
   }
   SweepSync sync(ace_ctx *ctx) {

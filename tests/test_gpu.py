@@ -451,6 +451,31 @@ def test_update_tile_order_is_bitwise_neutral(A, tmp_path):
     assert np.array_equal(mine, outs["4"])
 
 
+def test_cross_update_on_tiles_is_bitwise_neutral(A, tmp_path):
+    """The lookahead cross update on k_update's 128-tiles (ACE_XUPD=1) runs
+    the same MFMA chain per element as k_update_x's 64-tiles: the inverse
+    is bit-identical."""
+    import os
+    import subprocess
+    import sys
+    from additivecausalexpansion_amd.synthetic import make_problem
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = 1500
+    y, X, Z, th, _ = make_problem(n, 4, 5, seed=19)
+    K = A.kernmat_SE_symmetric_cpp(X, Z, th)["full"]
+    inp = str(tmp_path / "k.npz")
+    np.savez(inp, K=K, s=th[0])
+    outs = {}
+    for v in ("0", "1"):
+        out = str(tmp_path / f"inv{v}.npy")
+        env = dict(os.environ, ACE_XUPD=v)
+        subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
+                       env=env, check=True, timeout=100)
+        outs[v] = np.load(out)
+    assert np.array_equal(outs["0"], outs["1"])
+    assert np.array_equal(A.invkernel_cpp(K, th[0])["inv"], outs["0"])
+
+
 def test_split_panel_is_bitwise_neutral(A, tmp_path):
     """The column-split panel update (k_panel_split, default) performs
     k_panel's arithmetic in k_panel's order over (NB/64)^2 workgroups: the
