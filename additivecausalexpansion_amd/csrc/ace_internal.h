@@ -124,8 +124,8 @@ struct SweepBufs {
   double *A;      // Naug x Naug, col-major, ld = Naug, lower triangle used
   int64_t ld;     // Naug
   int64_t npad;   // multiple of NB
-  double *P[2];   // Naug x NB : -panel (negated copy), double-buffered by step
-  double *W[2];   // Naug x NB : panel being swept, double-buffered by step
+  double *P[4];   // Naug x NB : -panel (negated copy), slot k & 1 (k & 3 with pair steps)
+  double *W[4];   // Naug x NB : panel being swept, same slots; [2], [3] null unless pairs
   double *SW;     // SW_DOUBLES: 2 SUB x SUB sub-pivot inverses + split-panel chunks
   double *S[2];   // SUB x NB col-major: pivot rows before their sub-sweep (ping-pong)
   double *piv;    // npad pivots
@@ -137,7 +137,19 @@ struct SweepBufs {
   // k_update_x on 64-tiles
   const Tile *xtiles = nullptr;
   const int64_t *xoff = nullptr;
+  // two sweep steps per bulk launch (pair_steps()): every group's lookahead
+  // cross tiles (pair_cross_tiles), host offsets per group
+  const Tile *ptiles = nullptr;
+  const int64_t *poff = nullptr;
 };
+// Two sweep steps per bulk update launch (k_update_pair, K = 2 NB per tile;
+// default): ACE_PAIR=0 selects one step per launch (A/B switch).
+bool pair_steps();
+// Lower 128-tiles with I or J in the blocks of group g = steps 2g, 2g + 1,
+// for g = 1 .. ngroups-1 (dealt to the XCDs); off[g] .. off[g + 1] is group
+// g's range (off[0] = off[1] = 0).
+std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t> &off);
+double update_gemm_tiles_pair(int64_t naug, int64_t ka0, int kx0, int kx1);
 // The lower 128-tiles with I or J in block k+1, for k = 0 .. steps-2,
 // concatenated (each step's list dealt to the XCDs like the bulk order);
 // off[k] .. off[k+1] is step k's range.  ACE_XUPD=0 selects k_update_x.

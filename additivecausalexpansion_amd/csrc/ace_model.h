@@ -8,8 +8,8 @@
 
 // Buffers of one Gauss-Jordan sweep and its lookahead events.
 struct SweepWork {
-  DBuf A, P0, P1, W0, W1, SW, S0, S1, piv, flag, order, xtiles;
-  std::vector<int64_t> xoff;
+  DBuf A, P0, P1, W0, W1, P2, P3, W2, W3, SW, S0, S1, piv, flag, order, xtiles, ptiles;
+  std::vector<int64_t> xoff, poff;
   std::vector<hipEvent_t> ev;
   int64_t n = 0, npad = 0, naug = 0, norder = 0;
   SweepWork() = default;
@@ -36,6 +36,15 @@ struct SweepWork {
          "upload tile order");
       norder = (int64_t)t.size();
     }
+    poff.clear();
+    if (pair_steps() && cross_update_on_tiles() && npad / NB >= 2) {
+      for (DBuf *b : {&P2, &P3, &W2, &W3}) alloc(ctx, *b, (size_t)(naug * NB) * sizeof(double), "alloc panel");
+      const std::vector<Tile> t = pair_cross_tiles(naug, (int)(npad / NB), poff);
+      alloc(ctx, ptiles, std::max<size_t>(t.size(), 1) * sizeof(Tile), "alloc pair cross tiles");
+      if (!t.empty())
+        ck(ctx, hipMemcpy(ptiles.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
+           "upload pair cross tiles");
+    }
     xoff.clear();
     if (cross_update_on_tiles()) {
       const std::vector<Tile> t = cross_update_tiles(naug, (int)(npad / NB), xoff);
@@ -60,6 +69,14 @@ struct SweepWork {
     b.P[1] = P1.d();
     b.W[0] = W0.d();
     b.W[1] = W1.d();
+    b.P[2] = P2.p ? P2.d() : nullptr;
+    b.P[3] = P3.p ? P3.d() : nullptr;
+    b.W[2] = W2.p ? W2.d() : nullptr;
+    b.W[3] = W3.p ? W3.d() : nullptr;
+    if (!poff.empty()) {
+      b.ptiles = reinterpret_cast<const Tile *>(ptiles.p);
+      b.poff = poff.data();
+    }
     b.SW = SW.d();
     b.S[0] = S0.d();
     b.S[1] = S1.d();

@@ -719,6 +719,185 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
     }
 }
 
+// Two sweep steps per launch: A_IJ += W_a,I Pn_a,J^T + W_b,I Pn_b,J^T with
+// panels a (block [ka0, ka0 + NB)) and b = a + 1 (the next block), K = 2 NB
+// per tile -- every accumulator runs the same MFMA chain over the same k
+// order as two k_update launches (acc stored / reloaded in fp64 between
+// them), so the results are bit-identical, while the C tile is read and
+// written once per two steps.  Tiles of block b take W_b (k_update's copy);
+// tiles of block a take W_a (what step a left there) and then only panel b's
+// product; tiles with I or J in blocks [kx0, kx1) (the lookahead cross,
+// updated on the side stream) are skipped.  Single GPU only (G = 1).
+__global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
+    double *__restrict__ A, int64_t ld, const double *__restrict__ Ra,
+    const double *__restrict__ Ca, const double *__restrict__ Rb, const double *__restrict__ Cb,
+    int64_t ldp, int64_t ka0, int kx0, int kx1, const Tile *__restrict__ tiles) {
+  __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
+  __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
+  constexpr int KT = NB / UT;
+  int I, J;
+  if (tiles) {
+    const Tile tt = tiles[blockIdx.x];
+    I = tt.I;
+    J = tt.J;
+    if (I < 0) return;  // padding of the XCD order
+  } else {
+    const int t = blockIdx.x;
+    int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((i + 1) * (i + 2) / 2 <= t) ++i;
+    while (i * (i + 1) / 2 > t) --i;
+    I = i;
+    J = t - i * (i + 1) / 2;
+  }
+  if (kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT))) return;
+  const int64_t kb0 = ka0 + NB;
+  const int ta0 = (int)(ka0 / UT), tb0 = ta0 + KT;
+  const bool Ia = I >= ta0 && I < tb0, Ja = J >= ta0 && J < tb0;
+  const bool Ib = I >= tb0 && I < tb0 + KT, Jb = J >= tb0 && J < tb0 + KT;
+  const int64_t R0 = (int64_t)I * UT, C0 = (int64_t)J * UT;
+  const int tid = threadIdx.x;
+  const double *Wa = Ra, *Wb = Rb;  // single GPU: R = W
+
+  if (Ib || Jb) {  // block b holds W_b after the pair
+    if (Ib && !Jb) {
+      double *tileT = &sW[0][0][0];  // 64 x 65 scratch
+      for (int sa = 0; sa < 2; ++sa)
+        for (int sb = 0; sb < 2; ++sb) {
+          __syncthreads();
+          for (int e = tid; e < 4096; e += UTHREADS) {
+            const int c = e & 63, a = e >> 6;
+            tileT[a * 65 + c] = Wb[(C0 + 64 * sb + c) + (R0 - kb0 + 64 * sa + a) * ldp];
+          }
+          __syncthreads();
+          for (int e = tid; e < 4096; e += UTHREADS) {
+            const int a = e & 63, c = e >> 6;
+            A[(R0 + 64 * sa + a) + (C0 + 64 * sb + c) * ld] = tileT[a * 65 + c];
+          }
+        }
+    } else {
+      for (int e = tid; e < UT * UT; e += UTHREADS) {
+        const int a = e & (UT - 1), c = e >> 7;
+        A[(R0 + a) + (C0 + c) * ld] = Wb[(R0 + a) + (C0 - kb0 + c) * ldp];
+      }
+    }
+    return;
+  }
+  // block a (not b): the tile starts from W_a and gets panel b only
+  const bool from_w = Ia || Ja;
+  // W_a at (row r, column c) of such a tile: column block a (and the
+  // diagonal block) W_a[r, c - ka0]; row block a W_a[c, r - ka0] (transposed)
+  const int64_t wrs = Ja ? 1 : ldp, wcs = Ja ? ldp : 1;  // strides of r, c
+  const double *wab = Ja ? Wa - ka0 * ldp : Wa - ka0 * ldp;  // (r, c) -> wab[r wrs + c wcs]
+
+  const int lane = tid & 63, wv = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  if (R0 >= ld - AUG) {  // AUG row block: 16 live rows (as k_update)
+    d4 acc;
+    const int64_t r = R0 + lr;
+    const int64_t c = C0 + 16 * wv + lk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      acc[j] = from_w ? wab[r * wrs + (c + 4 * j) * wcs] : ld_a(&A[r + (c + 4 * j) * ld]);
+    for (int pnl = from_w ? 1 : 0; pnl < 2; ++pnl) {
+      const double *gr = (pnl ? Rb : Ra) + R0 + lr + (int64_t)lk * ldp;
+      const double *gc = (pnl ? Cb : Ca) + C0 + 16 * wv + lr + (int64_t)lk * ldp;
+      double an = gc[0], bn = gr[0];
+      for (int kk = 0; kk < NB / 4; ++kk) {
+        const double a = an, bb = bn;
+        if (kk + 1 < NB / 4) {
+          an = gc[(int64_t)(4 * (kk + 1)) * ldp];
+          bn = gr[(int64_t)(4 * (kk + 1)) * ldp];
+        }
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st_a(&A[r + (c + 4 * j) * ld], acc[j]);
+    return;
+  }
+  const int sk = tid >> 5, sm = (tid & 31) * 4;
+  const double *gWa = Ra + (R0 + sm) + (int64_t)sk * ldp;
+  const double *gPa = Ca + (C0 + sm) + (int64_t)sk * ldp;
+  const double *gWb = Rb + (R0 + sm) + (int64_t)sk * ldp;
+  const double *gPb = Cb + (C0 + sm) + (int64_t)sk * ldp;
+  double2 rw0, rw1, rp0, rp1;
+  {
+    const double *w = from_w ? gWb : gWa, *pp = from_w ? gPb : gPa;
+    rw0 = *reinterpret_cast<const double2 *>(w);
+    rw1 = *reinterpret_cast<const double2 *>(w + 2);
+    rp0 = *reinterpret_cast<const double2 *>(pp);
+    rp1 = *reinterpret_cast<const double2 *>(pp + 2);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the C-tile loads behind them
+  const int wr = wv & 1, wc = wv >> 1;
+  d4 acc[2][4];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 4; ++ri) {
+      const int64_t r = R0 + 64 * wr + 16 * ri + lr;
+      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+      if (from_w) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[ci][ri][j] = wab[r * wrs + (c + 4 * j) * wcs];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[ci][ri][j] = ld_a(&A[r + (c + 4 * j) * ld]);
+      }
+    }
+  *reinterpret_cast<double2 *>(&sW[0][sk][sm]) = rw0;
+  *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2]) = rw1;
+  *reinterpret_cast<double2 *>(&sP[0][sk][sm]) = rp0;
+  *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2]) = rp1;
+  __syncthreads();
+  // chunk ch of segment seg (0: panel a, 1: panel b) uses LDS buffer ch & 1
+  // (NCH is even, so the parity runs on across the two segments)
+  for (int seg = from_w ? 1 : 0; seg < 2; ++seg) {
+    const double *sw = seg ? gWb : gWa, *sp = seg ? gPb : gPa;
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int cur = ch & 1;
+      const bool more = ch + 1 < NCH || seg == 0;
+      if (more) {
+        const double *nw = ch + 1 < NCH ? sw + (int64_t)(ch + 1) * BK * ldp : gWb;
+        const double *np = ch + 1 < NCH ? sp + (int64_t)(ch + 1) * BK * ldp : gPb;
+        rw0 = *reinterpret_cast<const double2 *>(nw);
+        rw1 = *reinterpret_cast<const double2 *>(nw + 2);
+        rp0 = *reinterpret_cast<const double2 *>(np);
+        rp1 = *reinterpret_cast<const double2 *>(np + 2);
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        double a[2], b[4];
+#pragma unroll
+        for (int ci = 0; ci < 2; ++ci) a[ci] = sP[cur][4 * kk + lk][32 * wc + 16 * ci + lr];
+#pragma unroll
+        for (int ri = 0; ri < 4; ++ri) b[ri] = sW[cur][4 * kk + lk][64 * wr + 16 * ri + lr];
+#pragma unroll
+        for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+          for (int ri = 0; ri < 4; ++ri)
+            acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
+      }
+      if (more) {
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm]) = rw0;
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2]) = rw1;
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm]) = rp0;
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2]) = rp1;
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 4; ++ri) {
+      const int64_t r = R0 + 64 * wr + 16 * ri + lr;
+      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st_a(&A[r + (c + 4 * j) * ld], acc[ci][ri][j]);
+    }
+}
+
 // Lookahead update: only the tiles with I or J in block kx (the next panel).
 // About 2 n/128 tiles -- one workgroup per CU at 128 x 128 -- so it uses
 // 64 x 64 tiles (4 waves of 32 x 32) for 4x the workgroups; same math and
@@ -1021,6 +1200,55 @@ std::vector<Tile> cross_update_tiles(int64_t naug, int steps, std::vector<int64_
   return all;
 }
 
+bool pair_steps() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_PAIR");
+    // 1: 81.4 -> 79.5 ms per C2 evaluation (profiles/r02_chain_ab.txt)
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
+std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t> &off) {
+  const int64_t nT = naug / UT;
+  constexpr int KT = NB / UT;
+  const int ng = (steps + 1) / 2;
+  std::vector<Tile> all;
+  off.assign(2, 0);  // group 0 has no cross list
+  for (int g = 1; g < ng; ++g) {
+    const int64_t x0 = (int64_t)(2 * g) * KT, x1 = (int64_t)std::min(2 * g + 2, steps) * KT;
+    std::vector<Tile> t;
+    for (int64_t I = 0; I < nT; ++I)
+      for (int64_t J = 0; J <= I; ++J)
+        if ((I >= x0 && I < x1) || (J >= x0 && J < x1)) t.push_back(Tile{(int)I, (int)J});
+    const int S = update_order_block();
+    const std::vector<Tile> o = S > 0 ? xcd_update_order(t, S) : t;
+    all.insert(all.end(), o.begin(), o.end());
+    off.push_back((int64_t)all.size());
+  }
+  return all;
+}
+
+// GEMM tiles of one k_update_pair launch over every lower tile, in units of
+// one full tile x NB (a tile of the AUG row block computes 16 of 128 rows).
+double update_gemm_tiles_pair(int64_t naug, int64_t ka0, int kx0, int kx1) {
+  const int64_t nT = naug / UT;
+  constexpr int KT = NB / UT;
+  const int64_t ta0 = ka0 / UT, tb0 = ta0 + KT;
+  double cnt = 0.0;
+  for (int64_t I = 0; I < nT; ++I)
+    for (int64_t J = 0; J <= I; ++J) {
+      if (kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT)))
+        continue;
+      const bool Ia = I >= ta0 && I < tb0, Ja = J >= ta0 && J < tb0;
+      const bool Ib = I >= tb0 && I < tb0 + KT, Jb = J >= tb0 && J < tb0 + KT;
+      if (Ib || Jb) continue;
+      cnt += ((I == nT - 1) ? 16.0 / UT : 1.0) * ((Ia || Ja) ? 1.0 : 2.0);
+    }
+  return cnt;
+}
+
 std::vector<Tile> own_tiles(int64_t ntile, int T, int G, int r) {
   std::vector<Tile> t;
   for (int64_t I = 0; I < ntile; ++I)
@@ -1057,8 +1285,95 @@ std::vector<Tile> xcd_update_order(const std::vector<Tile> &tl, int S) {
 // bulk update of step k-1 is done, updates the cross of block k+1 with panel
 // k and then gathers and sweeps panel k+1 -- all of it under the main
 // stream's update k.  P/W are double-buffered by step parity.
+// Two sweep steps per bulk launch.  Group g = steps 2g, 2g + 1 (the last
+// group may be one step); panels in slots k & 3.
+//   side:  wait(bulk g-1 done) -> pair cross of group g+1's blocks with
+//          group g's panels (k_update_pair on its tile list) -> panel 2g+2
+//          -> cross of block 2g+3 with panel 2g+2 (k_update on 128-tiles)
+//          -> panel 2g+3 -> ready(g+1)
+//   main:  wait(ready g) -> k_update_pair (every tile outside group g+1's
+//          cross), or k_update for a last single step.
+// Every element sees the single-step schedule's MFMA chains in the same
+// order: bit-identical to it (tests/test_gpu.py).
+static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
+                                  const SweepTiming *tm) {
+  const int64_t naug = b.ld;
+  const unsigned nT = (unsigned)(naug / UT);
+  const int steps = (int)(b.npad / NB);
+  const int ng = (steps + 1) / 2;
+  const bool two = sy && sy->side && sy->nev >= 2 * steps + 1;
+  hipStream_t side = two ? sy->side : st;
+  auto zsize = [&](int g) { return std::min(2, steps - 2 * g); };
+  auto slot = [](int k) { return k & 3; };
+  hipError_t e;
+  auto produce = [&](int g) -> hipError_t {  // group g's panels, on `side`
+    const int k = 2 * g;
+    hipError_t r = panel_sweep(b, slot(k), (int64_t)k * NB, side);
+    if (r != hipSuccess || zsize(g) < 2) return r;
+    const int64_t x0 = b.xoff[k], nx = b.xoff[k + 1] - x0;  // cross of block k+1, panel k
+    hipLaunchKernelGGL(k_update, dim3((unsigned)nx), dim3(UTHREADS), 0, side, b.A, b.ld,
+                       b.W[slot(k)], b.P[slot(k)], b.W[slot(k)], b.ld, (int64_t)k * NB, -1,
+                       b.xtiles + x0, 1);
+    return panel_sweep(b, slot(k + 1), (int64_t)(k + 1) * NB, side);
+  };
+  int used = 0;
+  if (two) {
+    if (!sy->ready_recorded) {
+      e = hipEventRecord(sy->ev[2 * steps], st);  // inputs ready
+      if (e != hipSuccess) return e;
+    }
+    e = hipStreamWaitEvent(side, sy->ev[2 * steps], 0);
+    if (e != hipSuccess) return e;
+  }
+  e = produce(0);
+  if (e != hipSuccess) return e;
+  if (two && (e = hipEventRecord(sy->ev[0], side)) != hipSuccess) return e;
+  for (int g = 0; g < ng; ++g) {
+    const int k = 2 * g;
+    const int64_t ka0 = (int64_t)k * NB;
+    const bool more = g + 1 < ng;
+    if (two && (e = hipStreamWaitEvent(st, sy->ev[2 * g], 0)) != hipSuccess) return e;
+    if (more) {
+      if (two) {
+        if ((e = hipEventRecord(sy->ev[2 * g + 1], st)) != hipSuccess) return e;  // bulk g-1 done
+        if ((e = hipStreamWaitEvent(side, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
+      }
+      const int64_t p0 = b.poff[g + 1], np = b.poff[g + 2] - p0;
+      hipLaunchKernelGGL(k_update_pair, dim3((unsigned)np), dim3(UTHREADS), 0, side, b.A, b.ld,
+                         b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0,
+                         -1, -1, b.ptiles + p0);
+      if ((e = produce(g + 1)) != hipSuccess) return e;
+      if (two && (e = hipEventRecord(sy->ev[2 * (g + 1)], side)) != hipSuccess) return e;
+    }
+    const bool timed = tm && tm->ev && used + 2 <= tm->nev;
+    if (timed) (void)hipEventRecord(tm->ev[used], st);
+    const unsigned grid = b.order ? (unsigned)b.norder : nT * (nT + 1) / 2;
+    const int kx0 = more ? 2 * (g + 1) : -1, kx1 = more ? 2 * (g + 1) + zsize(g + 1) : -1;
+    if (zsize(g) == 2)
+      hipLaunchKernelGGL(k_update_pair, dim3(grid), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[slot(k)],
+                         b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0, kx0, kx1,
+                         b.order);
+    else
+      hipLaunchKernelGGL(k_update, dim3(grid), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[slot(k)],
+                         b.P[slot(k)], b.W[slot(k)], b.ld, ka0, -1, b.order, 1);
+    if (timed) {
+      (void)hipEventRecord(tm->ev[used + 1], st);
+      if (tm->flops)
+        tm->flops[used / 2] = (zsize(g) == 2 ? update_gemm_tiles_pair(naug, ka0, kx0, kx1)
+                                             : update_gemm_tiles(naug, ka0, -1, false)) *
+                              2.0 * UT * UT * NB;
+      used += 2;
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (tm && tm->used) *tm->used = used;
+  return hipSuccess;
+}
+
 hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
                      const SweepTiming *tm) {
+  if (pair_steps() && b.ptiles && b.xtiles && b.P[2] && b.npad / NB >= 2)
+    return run_sweep_pairs(b, st, sy, tm);
   const int64_t naug = b.ld;
   const unsigned nT = (unsigned)(naug / UT);
   const int steps = (int)(b.npad / NB);

@@ -476,6 +476,30 @@ def test_cross_update_on_tiles_is_bitwise_neutral(A, tmp_path):
     assert np.array_equal(A.invkernel_cpp(K, th[0])["inv"], outs["0"])
 
 
+@pytest.mark.parametrize("n", [1100, 1500])
+def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
+    """Two sweep steps per bulk launch (k_update_pair, ACE_PAIR=1) run every
+    element's MFMA chain over the same k order as one step per launch: the
+    inverse is bit-identical.  n = 1100: 5 steps (a last single step), 1500: 6."""
+    import os
+    import subprocess
+    import sys
+    from additivecausalexpansion_amd.synthetic import make_problem
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    y, X, Z, th, _ = make_problem(n, 4, 5, seed=23)
+    K = A.kernmat_SE_symmetric_cpp(X, Z, th)["full"]
+    inp = str(tmp_path / "k.npz")
+    np.savez(inp, K=K, s=th[0])
+    outs = {}
+    for v in ("0", "1"):
+        out = str(tmp_path / f"inv{v}.npy")
+        env = dict(os.environ, ACE_PAIR=v)
+        subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
+                       env=env, check=True, timeout=100)
+        outs[v] = np.load(out)
+    assert np.array_equal(outs["0"], outs["1"])
+
+
 def test_split_panel_is_bitwise_neutral(A, tmp_path):
     """The column-split panel update (k_panel_split, default) performs
     k_panel's arithmetic in k_panel's order over (NB/64)^2 workgroups: the
