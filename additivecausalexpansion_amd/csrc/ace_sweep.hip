@@ -45,57 +45,6 @@ typedef double d4 __attribute__((ext_vector_type(4)));
     if (ACE_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(ACE_CHAIN_PRIO); \
   } while (0)
 
-// ---------------------------------------------------------------- gather
-// P = -A[:, k] for every row; W = A[:, k] only on the pivot rows (k_panel
-// sweeps them; k_panel_gemm forms every other row of W from P).
-__global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, int64_t ld,
-                                                int64_t k0, double *__restrict__ P,
-                                                double *__restrict__ W, int64_t ldp,
-                                                double *__restrict__ S0) {
-  __shared__ double tile[64][65];
-  const int64_t i0 = (int64_t)blockIdx.x * 64;
-  const int j0 = blockIdx.y * 64;
-  const int64_t col0 = k0 + j0;
-  const int tid = threadIdx.x;
-  const bool all_lower = i0 >= col0 + 63;
-  const bool all_upper = i0 + 63 < col0;
-  const bool piv = i0 >= k0 && i0 < k0 + NB;  // pivot rows: W needed
-  if (all_lower) {
-    for (int e = tid; e < 4096; e += 256) {
-      const int a = e & 63, b = e >> 6;
-      const double v = A[(i0 + a) + (col0 + b) * ld];
-      P[(i0 + a) + (int64_t)(j0 + b) * ldp] = -v;
-      if (piv) W[(i0 + a) + (int64_t)(j0 + b) * ldp] = v;
-    }
-  } else if (all_upper) {
-    for (int e = tid; e < 4096; e += 256) {
-      const int b = e & 63, a = e >> 6;
-      tile[a][b] = A[(col0 + b) + (i0 + a) * ld];
-    }
-    __syncthreads();
-    for (int e = tid; e < 4096; e += 256) {
-      const int a = e & 63, b = e >> 6;
-      const double v = tile[a][b];
-      P[(i0 + a) + (int64_t)(j0 + b) * ldp] = -v;
-      if (piv) W[(i0 + a) + (int64_t)(j0 + b) * ldp] = v;
-    }
-  } else {
-    for (int e = tid; e < 4096; e += 256) {
-      const int a = e & 63, b = e >> 6;
-      const int64_t i = i0 + a, c = col0 + b;
-      const double v = (i >= c) ? A[i + c * ld] : A[c + i * ld];
-      P[i + (int64_t)(j0 + b) * ldp] = -v;
-      if (piv) W[i + (int64_t)(j0 + b) * ldp] = v;
-    }
-  }
-  if (i0 == k0) {  // pivot rows of sub-block 0: snapshot for k_pivot / k_panel
-    for (int e = tid; e < 4096; e += 256) {
-      const int a = e & 63, b = e >> 6;
-      S0[a + (int64_t)(j0 + b) * SUB] = W[(i0 + a) + (int64_t)(j0 + b) * ldp];
-    }
-  }
-}
-
 // ---------------------------------------------------------------- pivot
 // Sweeps the 64x64 sub-block s of the panel's pivot rows:
 //   d = D_tt; D_ij -= D_it D_tj / d; D_it /= d; D_tj /= d; D_tt = -1/d
@@ -229,6 +178,74 @@ static void launch_pivot(const double *S, int s, double *SW, double *piv, int64_
       break;
     default:
       hipLaunchKernelGGL(k_pivot<4>, dim3(1), dim3(256), 0, st, S, s, SW, piv, p0, flag);
+  }
+}
+
+// ---------------------------------------------------------------- gather
+// P = -A[:, k] for every row; W = A[:, k] only on the pivot rows (k_panel
+// sweeps them; k_panel_gemm forms every other row of W from P).
+// PIV: the workgroup of the pivot block's first 64 x 64 diagonal block
+// (sub-block 0) then runs k_pivot's sub-sweep of it (into SW0, piv, flag):
+// one chain launch less per panel.
+template <bool PIV>
+__global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, int64_t ld,
+                                                int64_t k0, double *__restrict__ P,
+                                                double *__restrict__ W, int64_t ldp,
+                                                double *__restrict__ S0, double *__restrict__ SW0,
+                                                double *__restrict__ pivs, int *__restrict__ flag) {
+  __shared__ double tile[64][65];
+  const int64_t i0 = (int64_t)blockIdx.x * 64;
+  const int j0 = blockIdx.y * 64;
+  const int64_t col0 = k0 + j0;
+  const int tid = threadIdx.x;
+  const bool all_lower = i0 >= col0 + 63;
+  const bool all_upper = i0 + 63 < col0;
+  const bool piv = i0 >= k0 && i0 < k0 + NB;  // pivot rows: W needed
+  if (all_lower) {
+    for (int e = tid; e < 4096; e += 256) {
+      const int a = e & 63, b = e >> 6;
+      const double v = A[(i0 + a) + (col0 + b) * ld];
+      P[(i0 + a) + (int64_t)(j0 + b) * ldp] = -v;
+      if (piv) W[(i0 + a) + (int64_t)(j0 + b) * ldp] = v;
+    }
+  } else if (all_upper) {
+    for (int e = tid; e < 4096; e += 256) {
+      const int b = e & 63, a = e >> 6;
+      tile[a][b] = A[(col0 + b) + (i0 + a) * ld];
+    }
+    __syncthreads();
+    for (int e = tid; e < 4096; e += 256) {
+      const int a = e & 63, b = e >> 6;
+      const double v = tile[a][b];
+      P[(i0 + a) + (int64_t)(j0 + b) * ldp] = -v;
+      if (piv) W[(i0 + a) + (int64_t)(j0 + b) * ldp] = v;
+    }
+  } else {
+    const bool diag0 = PIV && i0 == k0 && j0 == 0;  // D_0 itself
+    for (int e = tid; e < 4096; e += 256) {
+      const int a = e & 63, b = e >> 6;
+      const int64_t i = i0 + a, c = col0 + b;
+      const double v = (i >= c) ? A[i + c * ld] : A[c + i * ld];
+      P[i + (int64_t)(j0 + b) * ldp] = -v;
+      if (piv) W[i + (int64_t)(j0 + b) * ldp] = v;
+      if (diag0) tile[a][b] = v;
+    }
+  }
+  if (i0 == k0) {  // pivot rows of sub-block 0: snapshot for k_pivot / k_panel
+    for (int e = tid; e < 4096; e += 256) {
+      const int a = e & 63, b = e >> 6;
+      S0[a + (int64_t)(j0 + b) * SUB] = W[(i0 + a) + (int64_t)(j0 + b) * ldp];
+    }
+  }
+  if (PIV && i0 == k0 && j0 == 0) {
+    __shared__ PivotLds<4> L;
+    __syncthreads();
+    const int lane = tid & 63, w = tid >> 6;
+    double v[SUB / 4];
+#pragma unroll
+    for (int q = 0; q < SUB / 4; ++q) v[q] = tile[lane][16 * w + q];
+    pivot_sweep<4>(v, L, tid);
+    pivot_store<4>(v, L, tid, SW0, pivs, k0, flag);
   }
 }
 
@@ -1116,13 +1133,15 @@ static bool panel_split() {
   return v != 0;
 }
 
+// pivot0: sub-block 0 was already swept (by k_gather<true>)
 static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, double *SW,
                         double *const S[2], double *piv, int *flag, int G, int r,
-                        hipStream_t st) {
+                        hipStream_t st, bool pivot0 = false) {
   const bool split = panel_split();
   double *const SWb[2] = {SW, SW + SUB * SUB};  // ping-pong by sub-step
   for (int s = 0; s < NB / SUB; ++s) {
-    if (!split || s == 0) launch_pivot(S[s & 1], s, SWb[s & 1], piv, k0 + (int64_t)s * SUB, flag, st);
+    if (!split || (s == 0 && !pivot0))
+      launch_pivot(S[s & 1], s, SWb[s & 1], piv, k0 + (int64_t)s * SUB, flag, st);
     if (split)
       hipLaunchKernelGGL(k_panel_split, dim3(NB / SUB, NB / SUB), dim3(256), 0, st, W, ld, k0, s,
                          SWb[s & 1], S[s & 1], S[(s + 1) & 1], SW + 2 * SUB * SUB,
@@ -1135,13 +1154,33 @@ static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, dou
                      G, r);
 }
 
+// ACE_GATHER_PIV=1: sub-block 0's sweep inside k_gather's D_0 workgroup
+// instead of its own k_pivot launch (A/B switch, bit-identical).  Off: the
+// chain is no longer the critical path, and the fused kernel's 98 VGPRs in
+// all 1040 gather workgroups cost the bulk update more than the saved launch
+// (79.76 / 79.65 vs 79.53 / 79.51 ms per C2 evaluation, profiles/r02_chain_ab.txt).
+static bool gather_pivot() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_GATHER_PIV");
+    v = e ? (atoi(e) != 0) : 0;
+  }
+  return v != 0;
+}
+
 static hipError_t panel_sweep(const SweepBufs &b, int buf, int64_t k0, hipStream_t st) {
   const int64_t naug = b.ld;
-  hipLaunchKernelGGL(k_gather, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st, b.A, b.ld,
-                     k0, b.P[buf], b.W[buf], b.ld, b.S[0]);
+  // with the split panel, k_gather's D_0 workgroup sweeps sub-block 0 too
+  const bool gp = panel_split() && gather_pivot();
+  if (gp)
+    hipLaunchKernelGGL(k_gather<true>, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st, b.A,
+                       b.ld, k0, b.P[buf], b.W[buf], b.ld, b.S[0], b.SW, b.piv, b.flag);
+  else
+    hipLaunchKernelGGL(k_gather<false>, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st,
+                       b.A, b.ld, k0, b.P[buf], b.W[buf], b.ld, b.S[0], nullptr, nullptr, nullptr);
   // sweep the NB x NB pivot block in place, then every other panel row:
   // W_i = Pn_i W_kk
-  panel_chain(b.P[buf], b.W[buf], b.ld, k0, b.SW, b.S, b.piv, b.flag, 1, 0, st);
+  panel_chain(b.P[buf], b.W[buf], b.ld, k0, b.SW, b.S, b.piv, b.flag, 1, 0, st, gp);
   return hipGetLastError();
 }
 

@@ -500,6 +500,25 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     assert np.array_equal(outs["0"], outs["1"])
 
 
+def test_gather_pivot_is_bitwise_neutral(A, tmp_path):
+    """Sub-block 0's sweep inside k_gather (ACE_GATHER_PIV=1) and as its own
+    k_pivot launch (default) give the same inverse bit for bit."""
+    import os
+    import subprocess
+    import sys
+    from additivecausalexpansion_amd.synthetic import make_problem
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    y, X, Z, th, _ = make_problem(1300, 4, 5, seed=29)
+    K = A.kernmat_SE_symmetric_cpp(X, Z, th)["full"]
+    inp = str(tmp_path / "k.npz")
+    np.savez(inp, K=K, s=th[0])
+    out = str(tmp_path / "inv0.npy")
+    env = dict(os.environ, ACE_GATHER_PIV="1")
+    subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
+                   env=env, check=True, timeout=100)
+    assert np.array_equal(A.invkernel_cpp(K, th[0])["inv"], np.load(out))
+
+
 def test_split_panel_is_bitwise_neutral(A, tmp_path):
     """The column-split panel update (k_panel_split, default) performs
     k_panel's arithmetic in k_panel's order over (NB/64)^2 workgroups: the
