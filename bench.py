@@ -119,7 +119,7 @@ def pair_hbm_gbs(asm_ms, grad_ms):
     try:
         ks = json.load(open(files[-1]))["kernels"]
         a, g = ks["k_asm_mm"], ks["k_grad_mm"]
-        evals = ks["k_update"]["launches"] / (N1 // 256)  # 64 sweep steps per C2 eval
+        evals = g["launches"] / 2  # diagonal + strictly-lower gradient launch per eval
         asm_b = a["traffic"] * a["launches"] / evals  # the assembly is 2 launches per eval
         grad_b = g["traffic"] * g["launches"] / evals
     except (KeyError, ValueError, OSError, ZeroDivisionError):
@@ -311,7 +311,7 @@ def main():
 
     line = None
     if rank == 0:
-        traffic, traffic_src = pmc_traffic()
+        traffic, traffic_src = pmc_traffic("k_update_pair_bulk")
         evals = a.steps * world
         value = evals / dt_max
         achieved = upd_work / (upd_ms * 1e-3) / 1e12 if upd_ms > 0 else None
@@ -336,7 +336,8 @@ def main():
                 "parallelism": "single" if world == 1 else f"replicas x{world}",
             },
             "roofline": {
-                "kernel": "k_update (sweep SYRK/GEMM update, v_mfma_f64_16x16x4_f64)",
+                "kernel": ("k_update_pair (bulk sweep update, two Gauss-Jordan steps per launch, "
+                           "K = 512 per 128x128 tile, v_mfma_f64_16x16x4_f64)"),
                 "bound": "mfma",
                 "achieved": achieved,
                 "peak": FP64_MFMA_PEAK_TFLOPS,
