@@ -1204,7 +1204,10 @@ int update_order_block() {
   static int v = -1;
   if (v < 0) {
     const char *e = getenv("ACE_UPD_ORDER");
-    v = e ? std::max(0, atoi(e)) : 4;
+    // 2 with two steps per launch (K = 512 panels per tile): 78.7-78.9 ms
+    // per C2 evaluation against 79.1-79.2 at 4, 79.6-79.7 at 3, 81.1-81.2
+    // at 8, 79.1-79.5 at 1 and at 0 (row-major); profiles/r02_chain_ab.txt
+    v = e ? std::max(0, atoi(e)) : 2;
   }
   return v;
 }
