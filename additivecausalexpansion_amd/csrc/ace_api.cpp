@@ -54,6 +54,7 @@ int ace_create(int device, ace_ctx **out) {
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
     e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, hi);
   }
   if (e != hipSuccess) {
     g_create_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
@@ -69,6 +70,7 @@ void ace_destroy(ace_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  if (ctx->side2) (void)hipStreamDestroy(ctx->side2);
   delete ctx;
 }
 

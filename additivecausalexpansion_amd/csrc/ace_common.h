@@ -18,6 +18,7 @@ struct ace_ctx {
   int device = 0;
   hipStream_t stream = nullptr;  // main stream (every ABI call syncs it)
   hipStream_t side = nullptr;    // sweep lookahead: panel factorisation
+  hipStream_t side2 = nullptr;   // sweep lookahead: the second block's cross update
   int (*poll)(void *) = nullptr; // optional interrupt poll (ace_set_interrupt_poll)
   void *poll_user = nullptr;
   std::string err;

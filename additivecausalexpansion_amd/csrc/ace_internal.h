@@ -1,6 +1,7 @@
 // ace_internal.h -- shared declarations between the HIP kernels
 // (ace_kernels.hip, ace_sweep.hip) and the host orchestration (ace_api.cpp).
 #pragma once
+#include <functional>
 #include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -141,13 +142,16 @@ struct SweepBufs {
   // cross tiles (pair_cross_tiles), host offsets per group
   const Tile *ptiles = nullptr;
   const int64_t *poff = nullptr;
+  const Tile *gorder = nullptr;  // per-group bulk orders (tail_sort), glen each
+  int64_t glen = 0;
 };
 // Two sweep steps per bulk update launch (k_update_pair, K = 2 NB per tile;
 // default): ACE_PAIR=0 selects one step per launch (A/B switch).
 bool pair_steps();
-// Lower 128-tiles with I or J in the blocks of group g = steps 2g, 2g + 1,
-// for g = 1 .. ngroups-1 (dealt to the XCDs); off[g] .. off[g + 1] is group
-// g's range (off[0] = off[1] = 0).
+// Lookahead cross tiles of group g = steps 2g, 2g + 1, for g = 1 ..
+// ngroups-1 (each list dealt to the XCDs): [off[2g], off[2g+1]) the lower
+// 128-tiles with I or J in block 2g, [off[2g+1], off[2g+2]) those with I or
+// J in block 2g + 1 and not in block 2g (empty for a one-step group).
 std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t> &off);
 double update_gemm_tiles_pair(int64_t naug, int64_t ka0, int kx0, int kx1);
 // The lower 128-tiles with I or J in block k+1, for k = 0 .. steps-2,
@@ -158,7 +162,12 @@ std::vector<Tile> cross_update_tiles(int64_t naug, int steps, std::vector<int64_
 // k_update tile order: the tiles of `tl` grouped into S x S super-blocks of
 // 128-tiles that are dealt whole to the 8 XCDs; list index b runs on XCD
 // b % 8 (dispatch is round-robin).  Entries with I < 0 are padding.
-std::vector<Tile> xcd_update_order(const std::vector<Tile> &tl, int S);
+std::vector<Tile> xcd_update_order(const std::vector<Tile> &tl, int S,
+                                   const std::function<double(const Tile &)> &cost = nullptr);
+// per group of two steps, the bulk order with each XCD's cheap tiles last
+// (ACE_TAIL_SORT=1): ngroups lists of *len entries
+bool tail_sort();
+std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len);
 // own lower tiles of size T over [0, ntile*T) in row-major order (ace_shard.cpp)
 std::vector<Tile> own_tiles(int64_t ntile, int T, int G, int r);
 // super-block size S of that order (0: row-major grid); ACE_UPD_ORDER=S
@@ -168,6 +177,7 @@ int update_order_block();
 // stream updates the rest of step k.  `ev` needs 2*steps + 1 events.
 struct SweepSync {
   hipStream_t side;
+  hipStream_t side2 = nullptr;  // pair steps: the second block's cross (needs 4 steps + 4 events)
   hipEvent_t *ev;
   int nev;
   bool ready_recorded = false;  // caller already recorded ev[2 * steps] ("inputs ready")

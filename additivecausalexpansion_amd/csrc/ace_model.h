@@ -8,8 +8,9 @@
 
 // Buffers of one Gauss-Jordan sweep and its lookahead events.
 struct SweepWork {
-  DBuf A, P0, P1, W0, W1, P2, P3, W2, W3, SW, S0, S1, piv, flag, order, xtiles, ptiles;
+  DBuf A, P0, P1, W0, W1, P2, P3, W2, W3, SW, S0, S1, piv, flag, order, xtiles, ptiles, gorder;
   std::vector<int64_t> xoff, poff;
+  int64_t glen = 0;
   std::vector<hipEvent_t> ev;
   int64_t n = 0, npad = 0, naug = 0, norder = 0;
   SweepWork() = default;
@@ -44,6 +45,13 @@ struct SweepWork {
       if (!t.empty())
         ck(ctx, hipMemcpy(ptiles.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
            "upload pair cross tiles");
+      glen = 0;
+      if (tail_sort()) {
+        const std::vector<Tile> o = pair_bulk_orders(naug, (int)(npad / NB), &glen);
+        alloc(ctx, gorder, o.size() * sizeof(Tile), "alloc bulk orders");
+        ck(ctx, hipMemcpy(gorder.p, o.data(), o.size() * sizeof(Tile), hipMemcpyHostToDevice),
+           "upload bulk orders");
+      }
     }
     xoff.clear();
     if (cross_update_on_tiles()) {
@@ -53,7 +61,7 @@ struct SweepWork {
         ck(ctx, hipMemcpy(xtiles.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
            "upload cross tiles");
     }
-    const size_t need = (size_t)(2 * (npad / NB) + 1);
+    const size_t need = (size_t)(4 * (npad / NB) + 4);
     while (ev.size() < need) {
       hipEvent_t e;
       ck(ctx, hipEventCreateWithFlags(&e, ACE_SYNC_EVENT_FLAGS), "event");
@@ -77,6 +85,10 @@ struct SweepWork {
       b.ptiles = reinterpret_cast<const Tile *>(ptiles.p);
       b.poff = poff.data();
     }
+    if (glen > 0) {
+      b.gorder = reinterpret_cast<const Tile *>(gorder.p);
+      b.glen = glen;
+    }
     b.SW = SW.d();
     b.S[0] = S0.d();
     b.S[1] = S1.d();
@@ -93,6 +105,7 @@ struct SweepWork {
   SweepSync sync(ace_ctx *ctx) {
     SweepSync s;
     s.side = ctx->side;
+    s.side2 = ctx->side2;
     s.ev = ev.data();
     s.nev = (int)ev.size();
     return s;

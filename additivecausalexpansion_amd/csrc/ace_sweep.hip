@@ -24,6 +24,7 @@
 // y.alpha with no extra pass over the inverse.
 #include "ace_internal.h"
 
+#include <functional>
 #include <map>
 
 namespace ace {
@@ -1242,6 +1243,46 @@ std::vector<Tile> cross_update_tiles(int64_t naug, int steps, std::vector<int64_
   return all;
 }
 
+// ACE_TAIL_SORT=1 (default): per group, the bulk tile order with each XCD's
+// cheap tiles (copies, block a, the AUG row, skipped lookahead tiles) last;
+// -0.15 ms per C2 evaluation once the side chain is off the critical path
+// (profiles/r02_chain_ab.txt)
+bool tail_sort() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_TAIL_SORT");
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
+std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len) {
+  const int64_t nT = naug / UT;
+  constexpr int KT = NB / UT;
+  const int ng = (steps + 1) / 2;
+  const std::vector<Tile> base = own_tiles(nT, UT, 1, 0);
+  const int S = std::max(1, update_order_block());
+  std::vector<Tile> all;
+  *len = 0;
+  for (int g = 0; g < ng; ++g) {
+    const int64_t ta0 = (int64_t)2 * g * KT, tb0 = ta0 + KT;
+    const bool more = g + 1 < ng;
+    const int64_t x0 = more ? (int64_t)2 * (g + 1) * KT : -1;
+    const int64_t x1 = more ? (int64_t)std::min(2 * (g + 1) + 2, steps) * KT : -1;
+    auto cost = [&](const Tile &t) -> double {
+      const int64_t I = t.I, J = t.J;
+      if (more && ((I >= x0 && I < x1) || (J >= x0 && J < x1))) return 0.0;  // skipped
+      if ((I >= tb0 && I < tb0 + KT) || (J >= tb0 && J < tb0 + KT)) return 0.05;  // copy
+      const double rows = (I == nT - 1) ? 16.0 / UT : 1.0;
+      return rows * (((I >= ta0 && I < tb0) || (J >= ta0 && J < tb0)) ? 1.0 : 2.0);
+    };
+    const std::vector<Tile> o = xcd_update_order(base, S, cost);
+    *len = (int64_t)o.size();
+    all.insert(all.end(), o.begin(), o.end());
+  }
+  return all;
+}
+
 bool pair_steps() {
   static int v = -1;
   if (v < 0) {
@@ -1252,22 +1293,38 @@ bool pair_steps() {
   return v != 0;
 }
 
+// ACE_SIDE2: pair steps run the second block's lookahead cross on a second
+// side stream, concurrently with the first block's panel chain (default 1)
+static bool side2_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_SIDE2");
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
 std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t> &off) {
   const int64_t nT = naug / UT;
   constexpr int KT = NB / UT;
   const int ng = (steps + 1) / 2;
+  const int S = update_order_block();
   std::vector<Tile> all;
-  off.assign(2, 0);  // group 0 has no cross list
+  off.assign(3, 0);  // group 0 has no cross lists
+  auto in_blk = [&](int64_t t, int blk) { return t >= (int64_t)blk * KT && t < (int64_t)(blk + 1) * KT; };
   for (int g = 1; g < ng; ++g) {
-    const int64_t x0 = (int64_t)(2 * g) * KT, x1 = (int64_t)std::min(2 * g + 2, steps) * KT;
-    std::vector<Tile> t;
+    const int b0 = 2 * g, b1 = 2 * g + 1;
+    std::vector<Tile> ta, tb;
     for (int64_t I = 0; I < nT; ++I)
-      for (int64_t J = 0; J <= I; ++J)
-        if ((I >= x0 && I < x1) || (J >= x0 && J < x1)) t.push_back(Tile{(int)I, (int)J});
-    const int S = update_order_block();
-    const std::vector<Tile> o = S > 0 ? xcd_update_order(t, S) : t;
-    all.insert(all.end(), o.begin(), o.end());
-    off.push_back((int64_t)all.size());
+      for (int64_t J = 0; J <= I; ++J) {
+        if (in_blk(I, b0) || in_blk(J, b0)) ta.push_back(Tile{(int)I, (int)J});
+        else if (b1 < steps && (in_blk(I, b1) || in_blk(J, b1))) tb.push_back(Tile{(int)I, (int)J});
+      }
+    for (auto *t : {&ta, &tb}) {
+      const std::vector<Tile> o = S > 0 ? xcd_update_order(*t, S) : *t;
+      all.insert(all.end(), o.begin(), o.end());
+      off.push_back((int64_t)all.size());
+    }
   }
   return all;
 }
@@ -1299,7 +1356,8 @@ std::vector<Tile> own_tiles(int64_t ntile, int T, int G, int r) {
   return t;
 }
 
-std::vector<Tile> xcd_update_order(const std::vector<Tile> &tl, int S) {
+std::vector<Tile> xcd_update_order(const std::vector<Tile> &tl, int S,
+                                   const std::function<double(const Tile &)> &cost) {
   // super-blocks (I / S, J / S) in row-major order; each goes whole to the
   // XCD with the fewest tiles so far, so an XCD's in-flight tiles share few
   // row / column panel blocks in its L2 (about -1 % per update launch at C2
@@ -1314,6 +1372,10 @@ std::vector<Tile> xcd_update_order(const std::vector<Tile> &tl, int S) {
       if (q[i].size() < q[x].size()) x = i;
     q[x].insert(q[x].end(), kv.second.begin(), kv.second.end());
   }
+  if (cost)  // each XCD's dearest tiles first: its launch tail is the cheap ones
+    for (auto &v : q)
+      std::stable_sort(v.begin(), v.end(),
+                       [&](const Tile &a, const Tile &b) { return cost(a) > cost(b); });
   size_t len = 0;
   for (auto &v : q) len = std::max(len, v.size());
   std::vector<Tile> out(len * X, Tile{-1, -1});
@@ -1348,7 +1410,15 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
   auto zsize = [&](int g) { return std::min(2, steps - 2 * g); };
   auto slot = [](int k) { return k & 3; };
   hipError_t e;
-  auto produce = [&](int g) -> hipError_t {  // group g's panels, on `side`
+  // a second side stream runs group g+1's second-block cross concurrently
+  // with the first panel's chain (events 2 steps + 1 ..: E1 / E2 per group)
+  const bool two2 = two && side2_on() && sy->side2 && sy->nev >= 4 * steps + 4;
+  hipStream_t side2 = two2 ? sy->side2 : side;
+  auto E1 = [&](int g) { return sy->ev[2 * steps + 1 + 2 * g]; };
+  auto E2 = [&](int g) { return sy->ev[2 * steps + 2 + 2 * g]; };
+  // group g's panels, on `side`; wait2 (g >= 1): the second block's cross,
+  // launched on side2, must be done before the single cross below
+  auto produce = [&](int g, bool wait2) -> hipError_t {
     const int k = 2 * g;
     hipError_t r = panel_sweep(b, slot(k), (int64_t)k * NB, side);
     if (r != hipSuccess || zsize(g) < 2) return r;
@@ -1358,6 +1428,7 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
       r = hipStreamWaitEvent(side, sy->ev[2 * steps - 1], 0);
       if (r != hipSuccess) return r;
     }
+    if (wait2 && two2 && (r = hipStreamWaitEvent(side, E2(g), 0)) != hipSuccess) return r;
     const int64_t x0 = b.xoff[k], nx = b.xoff[k + 1] - x0;  // cross of block k+1, panel k
     hipLaunchKernelGGL(k_update, dim3((unsigned)nx), dim3(UTHREADS), 0, side, b.A, b.ld,
                        b.W[slot(k)], b.P[slot(k)], b.W[slot(k)], b.ld, (int64_t)k * NB, -1,
@@ -1378,7 +1449,7 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
     e = hipEventRecord(sy->ev[2 * steps - 1], st);
     if (e != hipSuccess) return e;
   }
-  e = produce(0);
+  e = produce(0, false);
   if (e != hipSuccess) return e;
   if (two && (e = hipEventRecord(sy->ev[0], side)) != hipSuccess) return e;
   for (int g = 0; g < ng; ++g) {
@@ -1391,24 +1462,39 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
         if ((e = hipEventRecord(sy->ev[2 * g + 1], st)) != hipSuccess) return e;  // bulk g-1 done
         if ((e = hipStreamWaitEvent(side, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
       }
-      const int64_t p0 = b.poff[g + 1], np = b.poff[g + 2] - p0;
-      hipLaunchKernelGGL(k_update_pair, dim3((unsigned)np), dim3(UTHREADS), 0, side, b.A, b.ld,
+      // group g+1's cross with group g's panels: block 2g+2 first (its
+      // panel's chain waits for it), block 2g+3 on side2 meanwhile
+      const int64_t pa = b.poff[2 * (g + 1)], na = b.poff[2 * (g + 1) + 1] - pa;
+      const int64_t pb = b.poff[2 * (g + 1) + 1], nb = b.poff[2 * (g + 1) + 2] - pb;
+      hipLaunchKernelGGL(k_update_pair, dim3((unsigned)na), dim3(UTHREADS), 0, side, b.A, b.ld,
                          b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0,
-                         -1, -1, b.ptiles + p0);
-      if ((e = produce(g + 1)) != hipSuccess) return e;
+                         -1, -1, b.ptiles + pa);
+      if (nb > 0) {
+        if (two2) {
+          if ((e = hipEventRecord(E1(g + 1), side)) != hipSuccess) return e;
+          if ((e = hipStreamWaitEvent(side2, E1(g + 1), 0)) != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nb), dim3(UTHREADS), 0, side2, b.A, b.ld,
+                           b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld,
+                           ka0, -1, -1, b.ptiles + pb);
+        if (two2 && (e = hipEventRecord(E2(g + 1), side2)) != hipSuccess) return e;
+      }
+      if ((e = produce(g + 1, nb > 0)) != hipSuccess) return e;
       if (two && (e = hipEventRecord(sy->ev[2 * (g + 1)], side)) != hipSuccess) return e;
     }
     const bool timed = tm && tm->ev && used + 2 <= tm->nev;
     if (timed) (void)hipEventRecord(tm->ev[used], st);
-    const unsigned grid = b.order ? (unsigned)b.norder : nT * (nT + 1) / 2;
+    const unsigned grid = b.gorder ? (unsigned)b.glen
+                                   : (b.order ? (unsigned)b.norder : nT * (nT + 1) / 2);
+    const Tile *ord = b.gorder ? b.gorder + (int64_t)g * b.glen : b.order;
     const int kx0 = more ? 2 * (g + 1) : -1, kx1 = more ? 2 * (g + 1) + zsize(g + 1) : -1;
     if (zsize(g) == 2)
       hipLaunchKernelGGL(k_update_pair, dim3(grid), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[slot(k)],
                          b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0, kx0, kx1,
-                         b.order);
+                         ord);
     else
       hipLaunchKernelGGL(k_update, dim3(grid), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[slot(k)],
-                         b.P[slot(k)], b.W[slot(k)], b.ld, ka0, -1, b.order, 1);
+                         b.P[slot(k)], b.W[slot(k)], b.ld, ka0, -1, ord, 1);
     if (timed) {
       (void)hipEventRecord(tm->ev[used + 1], st);
       if (tm->flops)

@@ -480,7 +480,9 @@ def test_cross_update_on_tiles_is_bitwise_neutral(A, tmp_path):
 def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     """Two sweep steps per bulk launch (k_update_pair, ACE_PAIR=1) run every
     element's MFMA chain over the same k order as one step per launch: the
-    inverse is bit-identical.  n = 1100: 5 steps (a last single step), 1500: 6."""
+    inverse is bit-identical.  n = 1100: 5 steps (a last single step), 1500: 6.
+    So are the second block's cross on its own stream (ACE_SIDE2=0 runs it on
+    the panel stream) and the cost-sorted bulk order (ACE_TAIL_SORT=1)."""
     import os
     import subprocess
     import sys
@@ -491,13 +493,17 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     inp = str(tmp_path / "k.npz")
     np.savez(inp, K=K, s=th[0])
     outs = {}
-    for v in ("0", "1"):
-        out = str(tmp_path / f"inv{v}.npy")
-        env = dict(os.environ, ACE_PAIR=v)
+    variants = {"single": {"ACE_PAIR": "0"}, "pair": {"ACE_PAIR": "1"},
+                "one_side": {"ACE_PAIR": "1", "ACE_SIDE2": "0"},
+                "tail": {"ACE_PAIR": "1", "ACE_TAIL_SORT": "1"}}
+    for name, ev in variants.items():
+        out = str(tmp_path / f"inv_{name}.npy")
+        env = dict(os.environ, **ev)
         subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
                        env=env, check=True, timeout=100)
-        outs[v] = np.load(out)
-    assert np.array_equal(outs["0"], outs["1"])
+        outs[name] = np.load(out)
+    for name in variants:
+        assert np.array_equal(outs["single"], outs[name]), name
 
 
 def test_gather_pivot_is_bitwise_neutral(A, tmp_path):
