@@ -576,6 +576,51 @@ static_assert(BK == 16, "staging maps 512 threads x 4 doubles onto a 128 x 16 ch
 __device__ __forceinline__ void st_a(double *p, double v) { __builtin_nontemporal_store(v, p); }
 __device__ __forceinline__ double ld_a(const double *p) { return __builtin_nontemporal_load(p); }
 
+// Gather fused into a lookahead cross launch (ACE_XGATHER): the cross tiles
+// of block kg are exactly the lower tiles holding column block kg of the
+// symmetric matrix, so the launch that writes them can also write what
+// k_gather would read back from them -- P = -A[:, kg], W = A[:, kg] on the
+// pivot rows, the sub-block-0 snapshot S0 -- from the values it stores: the
+// same doubles, one chain launch less per panel.  k0 < 0: no gather.
+struct GatherOut {
+  double *P, *W, *S0;
+  int64_t k0, ldp;
+};
+static inline GatherOut no_gather() { return GatherOut{nullptr, nullptr, nullptr, -1, 0}; }
+
+// the value v stored at lower position (r, c) of A (r >= c; entries above
+// the diagonal of a diagonal tile are not part of the lower storage)
+__device__ __forceinline__ void gput(const GatherOut &g, int64_t r, int64_t c, double v) {
+  if (r < c) return;
+  const int64_t cc = c - g.k0, rr = r - g.k0;
+  if ((uint64_t)cc < (uint64_t)NB) {  // column block kg: row r of the panel
+    g.P[r + cc * g.ldp] = -v;
+    if ((uint64_t)rr < (uint64_t)NB) {
+      g.W[r + cc * g.ldp] = v;
+      if (rr < SUB) g.S0[rr + cc * SUB] = v;
+    }
+  }
+  if ((uint64_t)rr < (uint64_t)NB && r != c) {  // row block kg: row c of the panel (symmetry)
+    g.P[c + rr * g.ldp] = -v;
+    if ((uint64_t)cc < (uint64_t)NB) {
+      g.W[c + rr * g.ldp] = v;
+      if (cc < SUB) g.S0[cc + rr * SUB] = v;
+    }
+  }
+}
+
+// the AUG row block's dead rows (16 .. 127: zero padding, not computed):
+// k_gather copies them too
+__device__ __forceinline__ void gput_aug_dead(const GatherOut &g, const double *A, int64_t ld,
+                                              int64_t R0, int64_t C0, int tid, int nthr) {
+  const int64_t cc0 = C0 - g.k0;
+  if ((uint64_t)cc0 >= (uint64_t)NB) return;
+  for (int e = tid; e < (UT - 16) * UT; e += nthr) {
+    const int a = 16 + e % (UT - 16), c = e / (UT - 16);
+    g.P[(R0 + a) + (cc0 + c) * g.ldp] = -A[(R0 + a) + (C0 + c) * ld];
+  }
+}
+
 // Every lower tile except the "cross" of block kx (tiles with I or J in
 // block kx, updated earlier by k_update_x for the lookahead; kx < 0: none).
 // tiles == nullptr: all lower tiles, 1-D grid in row-major order; otherwise
@@ -585,7 +630,8 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
                                                         const double *__restrict__ Cop,
                                                         const double *__restrict__ Wk,
                                                         int64_t ldp, int64_t k0, int kx,
-                                                        const Tile *__restrict__ tiles, int G) {
+                                                        const Tile *__restrict__ tiles, int G,
+                                                        GatherOut go) {
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
   constexpr int KT = NB / UT;
@@ -625,14 +671,18 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
           __syncthreads();
           for (int e = tid; e < 4096; e += UTHREADS) {
             const int a = e & 63, c = e >> 6;
-            A[(R0 + 64 * sa + a) + (L0 + 64 * sb + c) * ld] = tileT[a * 65 + c];
+            const double v = tileT[a * 65 + c];
+            A[(R0 + 64 * sa + a) + (L0 + 64 * sb + c) * ld] = v;
+            if (go.k0 >= 0) gput(go, R0 + 64 * sa + a, C0 + 64 * sb + c, v);
           }
         }
     } else {
       // column block k (and the diagonal block): A[r, k0+j] = Wk[r, j]
       for (int e = tid; e < UT * UT; e += UTHREADS) {
         const int a = e & (UT - 1), c = e >> 7;
-        A[(R0 + a) + (L0 + c) * ld] = Wk[(R0 + a) + (C0 - k0 + c) * ldp];
+        const double v = Wk[(R0 + a) + (C0 - k0 + c) * ldp];
+        A[(R0 + a) + (L0 + c) * ld] = v;
+        if (go.k0 >= 0) gput(go, R0 + a, C0 + c, v);
       }
     }
     return;
@@ -663,6 +713,11 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) st_a(&A[r + (c + 4 * j) * ld], acc[j]);
+    if (go.k0 >= 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gput(go, r, C0 + 16 * wv + lk + 4 * j, acc[j]);
+      gput_aug_dead(go, A, ld, R0, C0, tid, UTHREADS);
+    }
     return;
   }
   // staging: each thread moves 4 doubles of each operand per chunk (issued
@@ -735,6 +790,15 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
 #pragma unroll
       for (int j = 0; j < 4; ++j) st_a(&A[r + (c + 4 * j) * ld], acc[ci][ri][j]);
     }
+  if (go.k0 >= 0) {
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int ri = 0; ri < 4; ++ri)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          gput(go, R0 + 64 * wr + 16 * ri + lr, C0 + 32 * wc + 16 * ci + lk + 4 * j, acc[ci][ri][j]);
+  }
 }
 
 // Two sweep steps per launch: A_IJ += W_a,I Pn_a,J^T + W_b,I Pn_b,J^T with
@@ -749,7 +813,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
 __global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
     double *__restrict__ A, int64_t ld, const double *__restrict__ Ra,
     const double *__restrict__ Ca, const double *__restrict__ Rb, const double *__restrict__ Cb,
-    int64_t ldp, int64_t ka0, int kx0, int kx1, const Tile *__restrict__ tiles) {
+    int64_t ldp, int64_t ka0, int kx0, int kx1, const Tile *__restrict__ tiles, GatherOut go) {
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
   constexpr int KT = NB / UT;
@@ -789,13 +853,17 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
           __syncthreads();
           for (int e = tid; e < 4096; e += UTHREADS) {
             const int a = e & 63, c = e >> 6;
-            A[(R0 + 64 * sa + a) + (C0 + 64 * sb + c) * ld] = tileT[a * 65 + c];
+            const double v = tileT[a * 65 + c];
+            A[(R0 + 64 * sa + a) + (C0 + 64 * sb + c) * ld] = v;
+            if (go.k0 >= 0) gput(go, R0 + 64 * sa + a, C0 + 64 * sb + c, v);
           }
         }
     } else {
       for (int e = tid; e < UT * UT; e += UTHREADS) {
         const int a = e & (UT - 1), c = e >> 7;
-        A[(R0 + a) + (C0 + c) * ld] = Wb[(R0 + a) + (C0 - kb0 + c) * ldp];
+        const double v = Wb[(R0 + a) + (C0 - kb0 + c) * ldp];
+        A[(R0 + a) + (C0 + c) * ld] = v;
+        if (go.k0 >= 0) gput(go, R0 + a, C0 + c, v);
       }
     }
     return;
@@ -831,6 +899,11 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) st_a(&A[r + (c + 4 * j) * ld], acc[j]);
+    if (go.k0 >= 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gput(go, r, c + 4 * j, acc[j]);
+      gput_aug_dead(go, A, ld, R0, C0, tid, UTHREADS);
+    }
     return;
   }
   const int sk = tid >> 5, sm = (tid & 31) * 4;
@@ -914,6 +987,15 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
 #pragma unroll
       for (int j = 0; j < 4; ++j) st_a(&A[r + (c + 4 * j) * ld], acc[ci][ri][j]);
     }
+  if (go.k0 >= 0) {
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int ri = 0; ri < 4; ++ri)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          gput(go, R0 + 64 * wr + 16 * ri + lr, C0 + 32 * wc + 16 * ci + lk + 4 * j, acc[ci][ri][j]);
+  }
 }
 
 // Lookahead update: only the tiles with I or J in block kx (the next panel).
@@ -1169,11 +1251,26 @@ static bool gather_pivot() {
   return v != 0;
 }
 
-static hipError_t panel_sweep(const SweepBufs &b, int buf, int64_t k0, hipStream_t st) {
+// ACE_XGATHER: pair steps fuse each panel's gather into the lookahead cross
+// launch that writes its column block (GatherOut; default 1)
+static bool xgather() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_XGATHER");
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
+// gathered: P, W and S[0] of this panel were written by the cross launch
+static hipError_t panel_sweep(const SweepBufs &b, int buf, int64_t k0, hipStream_t st,
+                              bool gathered = false) {
   const int64_t naug = b.ld;
   // with the split panel, k_gather's D_0 workgroup sweeps sub-block 0 too
-  const bool gp = panel_split() && gather_pivot();
-  if (gp)
+  const bool gp = !gathered && panel_split() && gather_pivot();
+  if (gathered)
+    ;
+  else if (gp)
     hipLaunchKernelGGL(k_gather<true>, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st, b.A,
                        b.ld, k0, b.P[buf], b.W[buf], b.ld, b.S[0], b.SW, b.piv, b.flag);
   else
@@ -1418,9 +1515,13 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
   auto E2 = [&](int g) { return sy->ev[2 * steps + 2 + 2 * g]; };
   // group g's panels, on `side`; wait2 (g >= 1): the second block's cross,
   // launched on side2, must be done before the single cross below
+  const bool xg = xgather();
+  auto gout = [&](int k) {
+    return xg ? GatherOut{b.P[slot(k)], b.W[slot(k)], b.S[0], (int64_t)k * NB, b.ld} : no_gather();
+  };
   auto produce = [&](int g, bool wait2) -> hipError_t {
     const int k = 2 * g;
-    hipError_t r = panel_sweep(b, slot(k), (int64_t)k * NB, side);
+    hipError_t r = panel_sweep(b, slot(k), (int64_t)k * NB, side, xg && g > 0);
     if (r != hipSuccess || zsize(g) < 2) return r;
     if (g == 0 && two) {
       // the caller may have signalled "inputs ready" after assembling only
@@ -1432,8 +1533,8 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
     const int64_t x0 = b.xoff[k], nx = b.xoff[k + 1] - x0;  // cross of block k+1, panel k
     hipLaunchKernelGGL(k_update, dim3((unsigned)nx), dim3(UTHREADS), 0, side, b.A, b.ld,
                        b.W[slot(k)], b.P[slot(k)], b.W[slot(k)], b.ld, (int64_t)k * NB, -1,
-                       b.xtiles + x0, 1);
-    return panel_sweep(b, slot(k + 1), (int64_t)(k + 1) * NB, side);
+                       b.xtiles + x0, 1, gout(k + 1));
+    return panel_sweep(b, slot(k + 1), (int64_t)(k + 1) * NB, side, xg);
   };
   int used = 0;
   if (two) {
@@ -1468,7 +1569,7 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
       const int64_t pb = b.poff[2 * (g + 1) + 1], nb = b.poff[2 * (g + 1) + 2] - pb;
       hipLaunchKernelGGL(k_update_pair, dim3((unsigned)na), dim3(UTHREADS), 0, side, b.A, b.ld,
                          b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0,
-                         -1, -1, b.ptiles + pa);
+                         -1, -1, b.ptiles + pa, gout(k + 2));
       if (nb > 0) {
         if (two2) {
           if ((e = hipEventRecord(E1(g + 1), side)) != hipSuccess) return e;
@@ -1476,7 +1577,7 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
         }
         hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nb), dim3(UTHREADS), 0, side2, b.A, b.ld,
                            b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld,
-                           ka0, -1, -1, b.ptiles + pb);
+                           ka0, -1, -1, b.ptiles + pb, no_gather());
         if (two2 && (e = hipEventRecord(E2(g + 1), side2)) != hipSuccess) return e;
       }
       if ((e = produce(g + 1, nb > 0)) != hipSuccess) return e;
@@ -1491,10 +1592,10 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
     if (zsize(g) == 2)
       hipLaunchKernelGGL(k_update_pair, dim3(grid), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[slot(k)],
                          b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0, kx0, kx1,
-                         ord);
+                         ord, no_gather());
     else
       hipLaunchKernelGGL(k_update, dim3(grid), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[slot(k)],
-                         b.P[slot(k)], b.W[slot(k)], b.ld, ka0, -1, ord, 1);
+                         b.P[slot(k)], b.W[slot(k)], b.ld, ka0, -1, ord, 1, no_gather());
     if (timed) {
       (void)hipEventRecord(tm->ev[used + 1], st);
       if (tm->flops)
@@ -1558,7 +1659,8 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
       if (b.xtiles) {  // the cross of block k+1 on k_update's 128-tiles
         const int64_t x0 = b.xoff[k], nx = b.xoff[k + 1] - x0;
         hipLaunchKernelGGL(k_update, dim3((unsigned)nx), dim3(UTHREADS), 0, side, b.A, b.ld,
-                           b.W[buf], b.P[buf], b.W[buf], b.ld, k0, -1, b.xtiles + x0, 1);
+                           b.W[buf], b.P[buf], b.W[buf], b.ld, k0, -1, b.xtiles + x0, 1,
+                           no_gather());
       } else {
         hipLaunchKernelGGL(k_update_x, dim3((unsigned)(naug / XT), 2 * (NB / XT)), dim3(256), 0,
                            side, b.A, b.ld, b.W[buf], b.P[buf], b.W[buf], b.ld, k0, k + 1, 1, 0);
@@ -1574,7 +1676,7 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
     if (timed) (void)hipEventRecord(tm->ev[used], st);
     hipLaunchKernelGGL(k_update, dim3(b.order ? (unsigned)b.norder : nT * (nT + 1) / 2),
                        dim3(UTHREADS), 0, st, b.A, b.ld, b.W[buf], b.P[buf], b.W[buf], b.ld, k0,
-                       more ? k + 1 : -1, b.order, 1);
+                       more ? k + 1 : -1, b.order, 1, no_gather());
     if (timed) {
       (void)hipEventRecord(tm->ev[used + 1], st);
       if (tm->flops) tm->flops[used / 2] =
@@ -1623,7 +1725,8 @@ hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t s
 hipError_t shard_update_main(const ShardSweep &b, int k, int buf, int kx, hipStream_t st) {
   if (b.ntiles > 0)
     hipLaunchKernelGGL(k_update, dim3((unsigned)b.ntiles), dim3(UTHREADS), 0, st, b.A, b.ld,
-                       b.P[buf], b.W[buf], b.W[buf], b.ld, (int64_t)k * NB, kx, b.tiles, b.G);
+                       b.P[buf], b.W[buf], b.W[buf], b.ld, (int64_t)k * NB, kx, b.tiles, b.G,
+                       no_gather());
   return hipGetLastError();
 }
 

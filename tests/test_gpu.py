@@ -482,7 +482,9 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     element's MFMA chain over the same k order as one step per launch: the
     inverse is bit-identical.  n = 1100: 5 steps (a last single step), 1500: 6.
     So are the second block's cross on its own stream (ACE_SIDE2=0 runs it on
-    the panel stream) and the cost-sorted bulk order (ACE_TAIL_SORT=1)."""
+    the panel stream), the cost-sorted bulk order (ACE_TAIL_SORT=1), the
+    gather fused into the cross launches (ACE_XGATHER=0: k_gather) and one
+    stream for everything (ACE_LOOKAHEAD=0)."""
     import os
     import subprocess
     import sys
@@ -495,7 +497,9 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     outs = {}
     variants = {"single": {"ACE_PAIR": "0"}, "pair": {"ACE_PAIR": "1"},
                 "one_side": {"ACE_PAIR": "1", "ACE_SIDE2": "0"},
-                "tail": {"ACE_PAIR": "1", "ACE_TAIL_SORT": "1"}}
+                "tail": {"ACE_PAIR": "1", "ACE_TAIL_SORT": "1"},
+                "gather": {"ACE_PAIR": "1", "ACE_XGATHER": "0"},
+                "one_stream": {"ACE_PAIR": "1", "ACE_LOOKAHEAD": "0"}}
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)
