@@ -801,6 +801,88 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
   }
 }
 
+// Panel GEMM on the update kernel's 128 x 128 tiles (ACE_PGEMM_TILES, the
+// default): W_I,J = Pn_I W_kk[:, J] for the two 128-column halves J of the
+// panel, K = NB.  Same operand roles, k order and zero start as
+// k_panel_gemm, so bit-identical to it, but each workgroup runs the bulk
+// update's pipelined 8-wave tile: under the bulk update k_panel_gemm's 64-row
+// strips held 258 update-sized CU slots for ~185 us per panel (skipping it
+// took 6 ms off a C2 evaluation, profiles/r02_chain_ab.txt).
+__global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict__ W,
+                                                              const double *__restrict__ Pn,
+                                                              int64_t ldp, int64_t k0, int G,
+                                                              int r) {
+  __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];  // Pn rows of the tile
+  __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];  // W_kk rows c
+  const int64_t R0 = (int64_t)blockIdx.x * UT, C0 = (int64_t)blockIdx.y * UT;
+  if (R0 >= k0 && R0 < k0 + NB) return;  // pivot rows are already final
+  if (G > 1 && !owns_col(R0, G, r) && !(owns_col(k0, G, r) && R0 >= k0)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int sk = tid >> 5, sm = (tid & 31) * 4;
+  const double *gW = Pn + (R0 + sm) + (int64_t)sk * ldp;
+  const double *gP = W + (k0 + C0 + sm) + (int64_t)sk * ldp;  // W_kk(c, k) = W[k0 + c, k]
+  double2 rw[2], rp[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    rw[e] = *reinterpret_cast<const double2 *>(gW + 2 * e);
+    rp[e] = *reinterpret_cast<const double2 *>(gP + 2 * e);
+  }
+  const int wr = wv & 1, wc = wv >> 1;
+  d4 acc[2][4];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 4; ++ri) acc[ci][ri] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2 * e]) = rw[e];
+    *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2 * e]) = rp[e];
+  }
+  __syncthreads();
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int cur = ch & 1;
+    if (ch + 1 < NCH) {
+      const int64_t off = (int64_t)(ch + 1) * BK * ldp;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        rw[e] = *reinterpret_cast<const double2 *>(gW + off + 2 * e);
+        rp[e] = *reinterpret_cast<const double2 *>(gP + off + 2 * e);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double a[2], b[4];
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci) a[ci] = sP[cur][4 * kk + lk][32 * wc + 16 * ci + lr];
+#pragma unroll
+      for (int ri = 0; ri < 4; ++ri) b[ri] = sW[cur][4 * kk + lk][64 * wr + 16 * ri + lr];
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+        for (int ri = 0; ri < 4; ++ri)
+          acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
+    }
+    if (ch + 1 < NCH) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2 * e]) = rw[e];
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2 * e]) = rp[e];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 4; ++ri) {
+      const int64_t rr = R0 + 64 * wr + 16 * ri + lr;
+      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) W[rr + (c + 4 * j) * ldp] = acc[ci][ri][j];
+    }
+}
+
 // Two sweep steps per launch: A_IJ += W_a,I Pn_a,J^T + W_b,I Pn_b,J^T with
 // panels a (block [ka0, ka0 + NB)) and b = a + 1 (the next block), K = 2 NB
 // per tile -- every accumulator runs the same MFMA chain over the same k
@@ -1217,12 +1299,29 @@ static bool panel_split() {
 }
 
 // pivot0: sub-block 0 was already swept (by k_gather<true>)
+// ACE_PGEMM_TILES=0 selects the 64-row k_panel_gemm (A/B switch; the tile
+// form k_panel_gemm_t is the default and bit-identical)
+static bool pgemm_tiles() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_PGEMM_TILES");
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
+// ACE_DIAG_SKIP (compile-time, timing diagnostics only -- the results are
+// wrong): bit 1 skips the pivot sub-sweeps and panel updates, bit 2 the panel
+// GEMM, bit 4 the lookahead cross launches of the pair schedule
+#ifndef ACE_DIAG_SKIP
+#define ACE_DIAG_SKIP 0
+#endif
 static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, double *SW,
                         double *const S[2], double *piv, int *flag, int G, int r,
                         hipStream_t st, bool pivot0 = false) {
   const bool split = panel_split();
   double *const SWb[2] = {SW, SW + SUB * SUB};  // ping-pong by sub-step
-  for (int s = 0; s < NB / SUB; ++s) {
+  for (int s = 0; s < ((ACE_DIAG_SKIP & 1) ? 0 : NB / SUB); ++s) {
     if (!split || (s == 0 && !pivot0))
       launch_pivot(S[s & 1], s, SWb[s & 1], piv, k0 + (int64_t)s * SUB, flag, st);
     if (split)
@@ -1233,8 +1332,13 @@ static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, dou
       hipLaunchKernelGGL(k_panel, dim3(NB / SUB), dim3(256), 0, st, W, ld, k0, s, SWb[s & 1],
                          S[s & 1], S[(s + 1) & 1], k0);
   }
-  hipLaunchKernelGGL(k_panel_gemm, dim3((unsigned)(ld / SUB)), dim3(512), 0, st, W, Pn, ld, k0,
-                     G, r);
+  if (ACE_DIAG_SKIP & 2) return;
+  if (pgemm_tiles())
+    hipLaunchKernelGGL(k_panel_gemm_t, dim3((unsigned)(ld / UT), NB / UT), dim3(UTHREADS), 0, st,
+                       W, Pn, ld, k0, G, r);
+  else
+    hipLaunchKernelGGL(k_panel_gemm, dim3((unsigned)(ld / SUB)), dim3(512), 0, st, W, Pn, ld, k0,
+                       G, r);
 }
 
 // ACE_GATHER_PIV=1: sub-block 0's sweep inside k_gather's D_0 workgroup
@@ -1530,8 +1634,8 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
       if (r != hipSuccess) return r;
     }
     if (wait2 && two2 && (r = hipStreamWaitEvent(side, E2(g), 0)) != hipSuccess) return r;
-    const int64_t x0 = b.xoff[k], nx = b.xoff[k + 1] - x0;  // cross of block k+1, panel k
-    hipLaunchKernelGGL(k_update, dim3((unsigned)nx), dim3(UTHREADS), 0, side, b.A, b.ld,
+    const int64_t x0 = b.xoff[k], nx = (ACE_DIAG_SKIP & 4) ? 0 : b.xoff[k + 1] - x0;  // cross of block k+1, panel k
+    if (nx > 0) hipLaunchKernelGGL(k_update, dim3((unsigned)nx), dim3(UTHREADS), 0, side, b.A, b.ld,
                        b.W[slot(k)], b.P[slot(k)], b.W[slot(k)], b.ld, (int64_t)k * NB, -1,
                        b.xtiles + x0, 1, gout(k + 1));
     return panel_sweep(b, slot(k + 1), (int64_t)(k + 1) * NB, side, xg);
@@ -1565,9 +1669,9 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
       }
       // group g+1's cross with group g's panels: block 2g+2 first (its
       // panel's chain waits for it), block 2g+3 on side2 meanwhile
-      const int64_t pa = b.poff[2 * (g + 1)], na = b.poff[2 * (g + 1) + 1] - pa;
-      const int64_t pb = b.poff[2 * (g + 1) + 1], nb = b.poff[2 * (g + 1) + 2] - pb;
-      hipLaunchKernelGGL(k_update_pair, dim3((unsigned)na), dim3(UTHREADS), 0, side, b.A, b.ld,
+      const int64_t pa = b.poff[2 * (g + 1)], na = (ACE_DIAG_SKIP & 4) ? 0 : b.poff[2 * (g + 1) + 1] - pa;
+      const int64_t pb = b.poff[2 * (g + 1) + 1], nb = (ACE_DIAG_SKIP & 4) ? 0 : b.poff[2 * (g + 1) + 2] - pb;
+      if (na > 0) hipLaunchKernelGGL(k_update_pair, dim3((unsigned)na), dim3(UTHREADS), 0, side, b.A, b.ld,
                          b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0,
                          -1, -1, b.ptiles + pa, gout(k + 2));
       if (nb > 0) {

@@ -176,9 +176,21 @@ def make_step(kernel, p, B, theta, std_y, ctx, y, X, Z, model=None):
         k.use_model(model, y, X, Z)
     state = {"it": 0}
 
+    # ACE_BENCH_DIAG=1: timing of deliberately broken diagnostic builds
+    # (tools/build_variant.sh -DACE_DIAG_SKIP=...): a non-finite gradient
+    # keeps the parameters instead of ending the run
+    diag = os.environ.get("ACE_BENCH_DIAG") == "1"
+    theta0 = k.parameters.copy()
+
     def step():
         state["it"] += 1
-        return k.para_update(state["it"], y, X, Z, opt, verbose=False)
+        if not diag:
+            return k.para_update(state["it"], y, X, Z, opt, verbose=False)
+        try:
+            return k.para_update(state["it"], y, X, Z, opt, verbose=False)
+        except ace.AceError:
+            k.parameters = theta0.copy()
+            return [float("nan"), float("nan")]
     step.kernel_object = k
     return step, model
 

@@ -483,8 +483,9 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     inverse is bit-identical.  n = 1100: 5 steps (a last single step), 1500: 6.
     So are the second block's cross on its own stream (ACE_SIDE2=0 runs it on
     the panel stream), the cost-sorted bulk order (ACE_TAIL_SORT=1), the
-    gather fused into the cross launches (ACE_XGATHER=0: k_gather) and one
-    stream for everything (ACE_LOOKAHEAD=0)."""
+    gather fused into the cross launches (ACE_XGATHER=0: k_gather), one
+    stream for everything (ACE_LOOKAHEAD=0) and the panel GEMM on 128-tiles
+    (ACE_PGEMM_TILES=0: the 64-row k_panel_gemm)."""
     import os
     import subprocess
     import sys
@@ -499,7 +500,9 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
                 "one_side": {"ACE_PAIR": "1", "ACE_SIDE2": "0"},
                 "tail": {"ACE_PAIR": "1", "ACE_TAIL_SORT": "1"},
                 "gather": {"ACE_PAIR": "1", "ACE_XGATHER": "0"},
-                "one_stream": {"ACE_PAIR": "1", "ACE_LOOKAHEAD": "0"}}
+                "one_stream": {"ACE_PAIR": "1", "ACE_LOOKAHEAD": "0"},
+                "pgemm_rows": {"ACE_PAIR": "1", "ACE_PGEMM_TILES": "0"},
+                "single_pgemm_rows": {"ACE_PAIR": "0", "ACE_PGEMM_TILES": "0"}}
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)

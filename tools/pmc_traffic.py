@@ -35,6 +35,7 @@ def read(d, counter):
     """Per kernel, the counter summed per dispatch (a counter comes as one row
     per dimension instance), in dispatch order."""
     per = defaultdict(dict)
+    grid = defaultdict(dict)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
@@ -44,13 +45,16 @@ def read(d, counter):
                     if key in row["Kernel_Name"]:
                         k = (f, int(row["Dispatch_Id"]))
                         per[short][k] = per[short].get(k, 0.0) + float(row["Counter_Value"])
+                        grid[short][k] = int(row.get("Grid_Size", 0) or 0)
     vals = {s: [v for _, v in sorted(m.items())] for s, m in per.items()}
-    # k_update_pair runs both as the bulk update (every tile) and as the side
-    # stream's lookahead cross (a few hundred tiles): report the bulk
-    # launches -- the larger half -- on their own
-    if "k_update_pair" in vals:
-        v = sorted(vals["k_update_pair"])
-        vals["k_update_pair_bulk"] = v[len(v) // 2 + 1:]
+    # k_update_pair runs both as the bulk update (every lower tile: the
+    # largest grid) and as the side stream's lookahead cross (a few hundred
+    # tiles): report the bulk launches, selected by grid size, on their own
+    if "k_update_pair" in per:
+        g = grid["k_update_pair"]
+        gmax = max(g.values())
+        vals["k_update_pair_bulk"] = [v for k, v in sorted(per["k_update_pair"].items())
+                                      if g[k] == gmax]
     return vals
 
 
