@@ -51,10 +51,17 @@ int ace_create(int device, ace_ctx **out) {
   if (e == hipSuccess) {
     // the lookahead panel chain is latency-bound: give it the highest priority
     // so its workgroups take the first free CU slots next to the update kernel
+    // (ACE_SIDE_PRIO=0: default priority, A/B switch; ACE_SIDE2_PRIO=0: the
+    // second side stream only)
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-    e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, hi);
+    auto prio = [&](const char *var) {
+      const char *v = getenv(var);
+      return (v && atoi(v) == 0) ? lo : hi;
+    };
+    const int p1 = prio("ACE_SIDE_PRIO"), p2 = p1 == lo ? lo : prio("ACE_SIDE2_PRIO");
+    e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, p1);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, p2);
   }
   if (e != hipSuccess) {
     g_create_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
@@ -431,8 +438,9 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, m->n, m->y.d(), st), "aug init");
   ck(ctx, hipMemsetAsync(w.flag.p, 0, sizeof(int), st), "memset flag");
   SweepSync sy = w.sync(ctx);
-  // the first panel's columns first: the sweep's first pivot chain (side
-  // stream) then runs under the rest of the assembly
+  // the first two panels' columns first: the sweep's first pivot chains
+  // and the cross of block 1 (side stream) then run under the rest of the
+  // assembly
   const int ts = m->tset;
   if (timed) ck(ctx, hipEventRecord(m->ev_asm[2 * ts], st), "event");
   ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,

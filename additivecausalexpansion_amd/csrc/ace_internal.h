@@ -64,9 +64,9 @@ struct PairSide {
 //         cube is non-null it receives the lower Kfull (same ld).
 // mode 1: symmetric ABI output -- full n x n Kfull (ld = n) + optional cube.
 // mode 2: cross ABI output -- n1 x n2 Kfull + optional cube.
-// part (mode 0 without a tile list): 0 all tiles, 1 the first panel's
-// columns (J < NB/AT), 2 the rest -- 1 then 2 lets the sweep's first pivot
-// chain start while part 2 runs.
+// part (mode 0 without a tile list): 0 all tiles, 1 the first two panels'
+// columns (J < 2 NB/AT), 2 the rest -- 1 then 2 lets the sweep's first
+// group of pivot chains (and the cross of block 1) run while part 2 runs.
 // b0 / b1 (modes 1 and 2, no cube): sum only slices [b0, b1) -- the
 // marginal kernels of prediction (src/pred_cpp.cpp:55-67); b1 < 0 means B.
 hipError_t launch_assembly(int mode, int kind, int PM, PairSide rows,

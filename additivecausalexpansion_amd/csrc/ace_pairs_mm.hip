@@ -372,6 +372,10 @@ __device__ __forceinline__ void gemm1_mm(const double *sXJ, const RowX<PM, FP> &
 // identity on padding) and of the Kfull copy; same outputs as
 // k_assembly<PM, KIND, 0>.
 // ---------------------------------------------------------------------------
+// tile columns of the assembly's first part (model_pipeline): the first two
+// panels' columns, at most all of them
+__host__ __device__ inline int asm_first_cols(int nt) { return 2 * NB / AT < nt ? 2 * NB / AT : nt; }
+
 template <int PM, int KIND>
 __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, int B, int ZS, TabView tab,
                                                 double sig, double *__restrict__ out, int64_t ld,
@@ -381,10 +385,11 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const double sg = tab.sig ? *tab.sig : sig;  // exp(theta[0]) on the diagonal
   int64_t I, J;
-  // part 1: the tiles of the first panel's columns (J < NB / AT, column by
-  // column) -- what the sweep's first pivot chain needs; part 2: the rest
-  // (the lower triangle of tiles >= NB / AT); 0: every lower tile / the list
-  constexpr int JB = NB / AT;
+  // part 1: the tiles of the first two panels' columns (J < JB = 2 NB / AT,
+  // column by column) -- what the sweep's first group (two pivot chains and
+  // the cross of block 1) needs; part 2: the rest (the lower triangle of
+  // tiles >= JB); 0: every lower tile / the list
+  const int JB = asm_first_cols(nt);
   if (tiles || part == 0) {
     tile_of(tiles, blockIdx.x, I, J);
   } else if (part == 1) {
@@ -892,7 +897,7 @@ template <int PM>
 static hipError_t asm_mm_pm(int kind, PairSide S, int64_t npad, int B, int ZS, TabView tab,
                             double sig, double *out, int64_t ld, double *kcopy, hipStream_t st,
                             const Tile *tiles, int64_t ntiles, int G, int part) {
-  const int64_t nt = npad / AT, JB = NB / AT;
+  const int64_t nt = npad / AT, JB = asm_first_cols((int)nt);
   if (tiles) part = 0;
   const int64_t nblk = tiles ? ntiles
                        : part == 1 ? JB * nt - JB * (JB - 1) / 2

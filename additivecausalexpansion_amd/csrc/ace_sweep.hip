@@ -1626,13 +1626,11 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
   auto produce = [&](int g, bool wait2) -> hipError_t {
     const int k = 2 * g;
     hipError_t r = panel_sweep(b, slot(k), (int64_t)k * NB, side, xg && g > 0);
+    // (g = 0: the caller may have signalled "inputs ready" after assembling
+    // only the first two panels' columns (model_pipeline) -- every tile the
+    // cross of block 1 reads or writes, disjoint from the rest of the
+    // assembly, which runs on under this group's chains)
     if (r != hipSuccess || zsize(g) < 2) return r;
-    if (g == 0 && two) {
-      // the caller may have signalled "inputs ready" after assembling only
-      // the first panel's columns (model_pipeline): block 1 must be complete
-      r = hipStreamWaitEvent(side, sy->ev[2 * steps - 1], 0);
-      if (r != hipSuccess) return r;
-    }
     if (wait2 && two2 && (r = hipStreamWaitEvent(side, E2(g), 0)) != hipSuccess) return r;
     const int64_t x0 = b.xoff[k], nx = (ACE_DIAG_SKIP & 4) ? 0 : b.xoff[k + 1] - x0;  // cross of block k+1, panel k
     if (nx > 0) hipLaunchKernelGGL(k_update, dim3((unsigned)nx), dim3(UTHREADS), 0, side, b.A, b.ld,
@@ -1647,11 +1645,6 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
       if (e != hipSuccess) return e;
     }
     e = hipStreamWaitEvent(side, sy->ev[2 * steps], 0);
-    if (e != hipSuccess) return e;
-    // everything enqueued on st so far: the whole matrix (ev index unused by
-    // the groups: 2 ng <= steps + 1 < 2 steps - 1 for steps >= 3; steps = 2
-    // has one group, whose produce(0) is the only user)
-    e = hipEventRecord(sy->ev[2 * steps - 1], st);
     if (e != hipSuccess) return e;
   }
   e = produce(0, false);
