@@ -107,6 +107,25 @@ def pmc_traffic(kernel="k_update"):
         return None, None
 
 
+def rocprof_bulk_avg():
+    """Average duration (ms) of the bulk k_update_pair launch in the newest
+    committed rocprofv3 kernel-trace summary (profiles/rNN_vMM_kernel_stats_split.csv,
+    tools/kernel_stats_split.py: the bulk launches on their own line), for the
+    cross-check against this run's HIP-event average."""
+    import csv
+    import glob
+    files = _newest_first_last(glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats_split.csv")))
+    if not files:
+        return None, None
+    try:
+        for row in csv.DictReader(open(files[-1])):
+            if row["Name"] == "ace::k_update_pair[bulk]":
+                return float(row["AverageNs"]) / 1e6, os.path.relpath(files[-1], ROOT)
+    except (KeyError, ValueError, OSError):
+        pass
+    return None, None
+
+
 def pair_hbm_gbs(asm_ms, grad_ms):
     """HBM GB/s of the fused assembly and gradient phases (SURVEY §8d asks for
     them beside their VALU/MFMA rates): PMC bytes per eval from the newest
@@ -324,6 +343,12 @@ def main():
     line = None
     if rank == 0:
         traffic, traffic_src = pmc_traffic("k_update_pair_bulk")
+        rp_ms, rp_src = rocprof_bulk_avg()
+        naug = -(-n // 256) * 256 + 128
+        nt = naug // 128
+        # compulsory bytes of one bulk launch: every lower 128-tile of A read
+        # and written once, plus the two steps' W and Pn panels
+        alg_bytes = nt * (nt + 1) // 2 * 128 * 128 * 8 * 2 + 4 * naug * 256 * 8
         evals = a.steps * world
         value = evals / dt_max
         achieved = upd_work / (upd_ms * 1e-3) / 1e12 if upd_ms > 0 else None
@@ -358,6 +383,9 @@ def main():
                 "traffic": traffic,
                 "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
                 "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "rocprof_avg_launch_ms": rp_ms,
+                "rocprof_source": rp_src,
                 "launches": upd_n,
                 "avg_launch_ms": upd_ms / upd_n if upd_n else None,
                 "algorithmic_flops_per_launch": upd_work / upd_n if upd_n else None,
