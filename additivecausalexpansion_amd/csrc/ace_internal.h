@@ -144,7 +144,23 @@ struct SweepBufs {
   const int64_t *poff = nullptr;
   const Tile *gorder = nullptr;  // per-group bulk orders (tail_sort), glen each
   int64_t glen = 0;
+  // merged schedule (merge_cross()): group g's bulk launch runs the list
+  // morder[moff[g], moff[g+1]) = [group g+1's cross tiles (mfront[g]
+  // entries, mtarget[g] of them real) | the bulk order]; the front tiles
+  // count into mcnt[g] (device; zeroed per sweep); null: not merged
+  const Tile *morder = nullptr;
+  const int64_t *moff = nullptr;
+  const int *mfront = nullptr, *mtarget = nullptr;
+  int *mcnt = nullptr;
 };
+// ACE_XMERGE=1: the next group's lookahead cross tiles run at the head of the
+// bulk launch instead of as side-stream launches (merged_bulk_orders)
+bool merge_cross();
+// per group g: [group g+1's pair cross tiles | group g's bulk order (gorder)]
+// (g + 1 < ngroups; the last group has no front), offsets off (ngroups + 1),
+// front entries and real front tiles per group
+std::vector<Tile> merged_bulk_orders(int64_t naug, int steps, std::vector<int64_t> &off,
+                                     std::vector<int> &front, std::vector<int> &target);
 // Two sweep steps per bulk update launch (k_update_pair, K = 2 NB per tile;
 // default): ACE_PAIR=0 selects one step per launch (A/B switch).
 bool pair_steps();

@@ -8,8 +8,10 @@
 
 // Buffers of one Gauss-Jordan sweep and its lookahead events.
 struct SweepWork {
-  DBuf A, P0, P1, W0, W1, P2, P3, W2, W3, SW, S0, S1, piv, flag, order, xtiles, ptiles, gorder;
-  std::vector<int64_t> xoff, poff;
+  DBuf A, P0, P1, W0, W1, P2, P3, W2, W3, SW, S0, S1, piv, flag, order, xtiles, ptiles, gorder,
+      morder, mcnt;
+  std::vector<int64_t> xoff, poff, moff;
+  std::vector<int> mfront, mtarget;
   int64_t glen = 0;
   std::vector<hipEvent_t> ev;
   int64_t n = 0, npad = 0, naug = 0, norder = 0;
@@ -52,6 +54,14 @@ struct SweepWork {
         ck(ctx, hipMemcpy(gorder.p, o.data(), o.size() * sizeof(Tile), hipMemcpyHostToDevice),
            "upload bulk orders");
       }
+      moff.clear();
+      if (glen > 0 && merge_cross()) {
+        const std::vector<Tile> m = merged_bulk_orders(naug, (int)(npad / NB), moff, mfront, mtarget);
+        alloc(ctx, morder, m.size() * sizeof(Tile), "alloc merged orders");
+        ck(ctx, hipMemcpy(morder.p, m.data(), m.size() * sizeof(Tile), hipMemcpyHostToDevice),
+           "upload merged orders");
+        alloc(ctx, mcnt, (size_t)round_up((int64_t)mfront.size(), 4) * sizeof(int), "alloc counters");
+      }
     }
     xoff.clear();
     if (cross_update_on_tiles()) {
@@ -88,6 +98,13 @@ struct SweepWork {
     if (glen > 0) {
       b.gorder = reinterpret_cast<const Tile *>(gorder.p);
       b.glen = glen;
+    }
+    if (!moff.empty()) {
+      b.morder = reinterpret_cast<const Tile *>(morder.p);
+      b.moff = moff.data();
+      b.mfront = mfront.data();
+      b.mtarget = mtarget.data();
+      b.mcnt = mcnt.i();
     }
     b.SW = SW.d();
     b.S[0] = S0.d();

@@ -134,6 +134,61 @@ __device__ __forceinline__ double exp_tb5(double x, const double *tab) {
   return __builtin_amdgcn_ldexp(q * tab[ki & 31], ki >> 5);
 }
 
+// Table-free form for the gradient's trace factors (ACE_GRAD_EXP=1):
+// x = m ln2 + r, |r| <= ln2/2, exp(r) by a degree-10 polynomial with the
+// first three Taylor coefficients pinned and the rest fitted on Chebyshev
+// nodes against an extended-precision exp (3.9e-16 relative over the
+// interval), so the per-pair chain has no LDS lookup.
+#ifndef ACE_GRAD_EXP
+#define ACE_GRAD_EXP 0
+#endif
+__device__ __forceinline__ double exp_pl(double x) {
+  const double kf = __builtin_rint(x * 1.4426950408889634);  // 1 / ln2
+  double r = fma(-kf, 0.6931471805599453, x);                 // ln2 hi
+  r = fma(-kf, 2.3190468138462996e-17, r);                    // ln2 lo
+  double q = 2.7545674171354605e-07;
+  q = fma(q, r, 2.763525742080496e-06);
+  q = fma(q, r, 2.4801715258403783e-05);
+  q = fma(q, r, 0.0001984118454548405);
+  q = fma(q, r, 0.001388888875659234);
+  q = fma(q, r, 0.008333333371438512);
+  q = fma(q, r, 0.04166666666704061);
+  q = fma(q, r, 0.1666666666661009);
+  q = fma(q, r, 0.5);
+  q = fma(q, r, 1.0);
+  q = fma(q, r, 1.0);
+  return __builtin_amdgcn_ldexp(q, (int)kf);
+}
+__device__ __forceinline__ double exp_grad(double x, const double *tab) {
+  return ACE_GRAD_EXP ? exp_pl(x) : exp_tb5(x, tab);
+}
+// degree-11 form of exp_pl (7e-18 relative over the interval) for the
+// assembly (ACE_ASM_EXP=1): K enters the inverse
+#ifndef ACE_ASM_EXP
+#define ACE_ASM_EXP 0
+#endif
+__device__ __forceinline__ double exp_pl11(double x) {
+  const double kf = __builtin_rint(x * 1.4426950408889634);
+  double r = fma(-kf, 0.6931471805599453, x);
+  r = fma(-kf, 2.3190468138462996e-17, r);
+  double q = 2.491759739472051e-08;
+  q = fma(q, r, 2.762544312686786e-07);
+  q = fma(q, r, 2.75578396598084e-06);
+  q = fma(q, r, 2.480150797092874e-05);
+  q = fma(q, r, 0.00019841269233459403);
+  q = fma(q, r, 0.0013888888927429829);
+  q = fma(q, r, 0.008333333333614103);
+  q = fma(q, r, 0.04166666666660212);
+  q = fma(q, r, 0.16666666666666238);
+  q = fma(q, r, 0.5);
+  q = fma(q, r, 1.0);
+  q = fma(q, r, 1.0);
+  return __builtin_amdgcn_ldexp(q, (int)kf);
+}
+__device__ __forceinline__ double exp_asm(double x, const double *tab) {
+  return ACE_ASM_EXP ? exp_pl11(x) : exp_tb(x, tab);
+}
+
 // sqrt(x), x >= 0 and normal or 0 (r2 values): hardware rsq (~2^-24
 // relative), one Goldschmidt step and one correction -- 0 ulp against the
 // correctly rounded sqrt over 4M samples (tools/probe_trans.hip; the
@@ -167,12 +222,12 @@ template <int KIND>
 __device__ __forceinline__ double kval_mm(int b, double r2, double lam, double zlo, double zhi,
                                           double lzlo, double lzhi, const double *etab) {
   if (KIND == 0) {
-    if (b == 0) return exp_tb(lam - r2, etab);
+    if (b == 0) return exp_asm(lam - r2, etab);
     if (zlo == 0.0 || zhi == 0.0) return 0.0;
-    return (sgn_mm(zlo) * sgn_mm(zhi)) * exp_tb(((lam - r2) + lzlo) + lzhi, etab);
+    return (sgn_mm(zlo) * sgn_mm(zhi)) * exp_asm(((lam - r2) + lzlo) + lzhi, etab);
   } else {
     const double t = sqrt_pk(r2);
-    const double e = (1.0 + SQRT3 * t) * exp_tb(lam - SQRT3 * t, etab);
+    const double e = (1.0 + SQRT3 * t) * exp_asm(lam - SQRT3 * t, etab);
     if (b == 0) return e;
     return (e * zlo) * zhi;  // z = 0 gives 0 (the reference's explicit zero test)
   }
@@ -652,12 +707,12 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
           // log|0| = -inf makes the exponential NaN: a select (not a branch)
           // puts the reference's 0 there
           const double kz = (sgn_mm(zlo) * sgn_mm(zhi)) *
-                            exp_tb5(((lam - r2) + (rlo ? lzr : lzc)) + (rlo ? lzc : lzr), L.E);
+                            exp_grad(((lam - r2) + (rlo ? lzr : lzc)) + (rlo ? lzc : lzr), L.E);
           kb = sel_f64(zlo == 0.0 || zhi == 0.0, 0.0, kz);
         } else {
           const double tt = sqrt_gs(r2);
           f = 1.0 + SQRT3 * tt;
-          const double e = f * exp_tb5(lam - SQRT3 * tt, L.E);
+          const double e = f * exp_grad(lam - SQRT3 * tt, L.E);
           // z = 0 gives a zero product (of either sign: it only enters sums)
           kb = (e * zlo) * zhi;
         }

@@ -892,28 +892,12 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
 // tiles of block a take W_a (what step a left there) and then only panel b's
 // product; tiles with I or J in blocks [kx0, kx1) (the lookahead cross,
 // updated on the side stream) are skipped.  Single GPU only (G = 1).
-__global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
-    double *__restrict__ A, int64_t ld, const double *__restrict__ Ra,
-    const double *__restrict__ Ca, const double *__restrict__ Rb, const double *__restrict__ Cb,
-    int64_t ldp, int64_t ka0, int kx0, int kx1, const Tile *__restrict__ tiles, GatherOut go) {
-  __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
-  __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
+__device__ __forceinline__ void update_pair_tile(
+    int I, int J, double (&sW)[2][BK][LDL], double (&sP)[2][BK][LDL], double *__restrict__ A,
+    int64_t ld, const double *__restrict__ Ra, const double *__restrict__ Ca,
+    const double *__restrict__ Rb, const double *__restrict__ Cb, int64_t ldp, int64_t ka0,
+    const GatherOut &go) {
   constexpr int KT = NB / UT;
-  int I, J;
-  if (tiles) {
-    const Tile tt = tiles[blockIdx.x];
-    I = tt.I;
-    J = tt.J;
-    if (I < 0) return;  // padding of the XCD order
-  } else {
-    const int t = blockIdx.x;
-    int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-    while ((i + 1) * (i + 2) / 2 <= t) ++i;
-    while (i * (i + 1) / 2 > t) --i;
-    I = i;
-    J = t - i * (i + 1) / 2;
-  }
-  if (kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT))) return;
   const int64_t kb0 = ka0 + NB;
   const int ta0 = (int)(ka0 / UT), tb0 = ta0 + KT;
   const bool Ia = I >= ta0 && I < tb0, Ja = J >= ta0 && J < tb0;
@@ -1077,6 +1061,73 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           gput(go, R0 + 64 * wr + 16 * ri + lr, C0 + 32 * wc + 16 * ci + lk + 4 * j, acc[ci][ri][j]);
+  }
+}
+
+// nfront < 0: every entry of the list is a plain tile (skip rule [kx0, kx1),
+// gather go on all of them).  nfront >= 0 (ACE_XMERGE, the merged bulk
+// launch): entries [0, nfront) are the next group's lookahead cross tiles,
+// run first, never skipped, gathered into go; each one, once its stores are
+// done, releases them at agent scope and adds 1 to *cnt, which the side
+// stream's k_wait_count polls before that group's panel chain.
+// The rest of the list is the bulk order, with the skip rule and no gather.
+__global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
+    double *__restrict__ A, int64_t ld, const double *__restrict__ Ra,
+    const double *__restrict__ Ca, const double *__restrict__ Rb, const double *__restrict__ Cb,
+    int64_t ldp, int64_t ka0, int kx0, int kx1, const Tile *__restrict__ tiles, GatherOut go,
+    int nfront, int *cnt) {
+  __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
+  __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
+  constexpr int KT = NB / UT;
+  int I, J;
+  if (tiles) {
+    const Tile tt = tiles[blockIdx.x];
+    I = tt.I;
+    J = tt.J;
+    if (I < 0) return;  // padding of the XCD order (not counted by the host's target)
+  } else {
+    const int t = blockIdx.x;
+    int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((i + 1) * (i + 2) / 2 <= t) ++i;
+    while (i * (i + 1) / 2 > t) --i;
+    I = i;
+    J = t - i * (i + 1) / 2;
+  }
+  const bool front = nfront >= 0 && (int)blockIdx.x < nfront;
+  if (!front && kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT)))
+    return;
+  GatherOut g = go;
+  if (nfront >= 0 && !front) g.k0 = -1;
+  update_pair_tile(I, J, sW, sP, A, ld, Ra, Ca, Rb, Cb, ldp, ka0, g);
+  if (front && cnt) {
+    // publish (cdna_hip_programming.md §6 Guideline 16, counter form): every
+    // wave drains its stores, then one lane releases at agent scope and adds
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Side stream, merged schedule: wait until *cnt >= target (the merged bulk
+// launch's front tiles are stored and released), then acquire.  One lane
+// polls relaxed with s_sleep; bounded: after ~0.5 s it gives up and sets
+// *flag = 2 (read like a non-positive pivot: the evaluation reports NaN
+// instead of hanging).
+__global__ __launch_bounds__(64) void k_wait_count(int *cnt, int target, int *flag) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(4);
+      if (wall_clock64() - t0 > 50000000ull) {  // 100 MHz counter: 0.5 s
+        __hip_atomic_store(flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
 }
 
@@ -1484,6 +1535,41 @@ std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len) {
   return all;
 }
 
+bool merge_cross() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_XMERGE");
+    v = e ? (atoi(e) != 0) : 0;
+  }
+  return v != 0;
+}
+
+std::vector<Tile> merged_bulk_orders(int64_t naug, int steps, std::vector<int64_t> &off,
+                                     std::vector<int> &front, std::vector<int> &target) {
+  const int ng = (steps + 1) / 2;
+  std::vector<int64_t> poff;
+  const std::vector<Tile> cross = pair_cross_tiles(naug, steps, poff);
+  int64_t glen = 0;
+  const std::vector<Tile> bulk = pair_bulk_orders(naug, steps, &glen);
+  std::vector<Tile> all;
+  off.assign(1, 0);
+  front.assign(ng, 0);
+  target.assign(ng, 0);
+  for (int g = 0; g < ng; ++g) {
+    if (g + 1 < ng) {  // group g+1's two cross lists (each XCD-dealt, padded to 8)
+      const int64_t a = poff[2 * (g + 1)], z = poff[2 * (g + 1) + 2];
+      for (int64_t i = a; i < z; ++i) {
+        all.push_back(cross[i]);
+        if (cross[i].I >= 0) ++target[g];
+      }
+      front[g] = (int)(z - a);
+    }
+    all.insert(all.end(), bulk.begin() + g * glen, bulk.begin() + (g + 1) * glen);
+    off.push_back((int64_t)all.size());
+  }
+  return all;
+}
+
 bool pair_steps() {
   static int v = -1;
   if (v < 0) {
@@ -1639,6 +1725,13 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
     return panel_sweep(b, slot(k + 1), (int64_t)(k + 1) * NB, side, xg);
   };
   int used = 0;
+  // merged schedule (ACE_XMERGE): group g+1's cross tiles lead bulk launch g
+  // and count into mcnt[g]; every group's counter starts at 0
+  const bool merged = two && b.morder && b.mcnt;
+  if (merged) {
+    e = hipMemsetAsync(b.mcnt, 0, (size_t)((ng + 3) / 4 * 4) * sizeof(int), st);
+    if (e != hipSuccess) return e;
+  }
   if (two) {
     if (!sy->ready_recorded) {
       e = hipEventRecord(sy->ev[2 * steps], st);  // inputs ready
@@ -1660,43 +1753,60 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
         if ((e = hipEventRecord(sy->ev[2 * g + 1], st)) != hipSuccess) return e;  // bulk g-1 done
         if ((e = hipStreamWaitEvent(side, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
       }
-      // group g+1's cross with group g's panels: block 2g+2 first (its
-      // panel's chain waits for it), block 2g+3 on side2 meanwhile
-      const int64_t pa = b.poff[2 * (g + 1)], na = (ACE_DIAG_SKIP & 4) ? 0 : b.poff[2 * (g + 1) + 1] - pa;
-      const int64_t pb = b.poff[2 * (g + 1) + 1], nb = (ACE_DIAG_SKIP & 4) ? 0 : b.poff[2 * (g + 1) + 2] - pb;
-      if (na > 0) hipLaunchKernelGGL(k_update_pair, dim3((unsigned)na), dim3(UTHREADS), 0, side, b.A, b.ld,
-                         b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0,
-                         -1, -1, b.ptiles + pa, gout(k + 2));
-      if (nb > 0) {
-        if (two2) {
-          if ((e = hipEventRecord(E1(g + 1), side)) != hipSuccess) return e;
-          if ((e = hipStreamWaitEvent(side2, E1(g + 1), 0)) != hipSuccess) return e;
+      if (merged) {
+        // the cross tiles lead bulk launch g: the chain of panel 2g+2 starts
+        // once they are stored (both blocks' -- the single cross of block
+        // 2g+3 below reads the second block's)
+        hipLaunchKernelGGL(k_wait_count, dim3(1), dim3(64), 0, side, b.mcnt + g, b.mtarget[g],
+                           b.flag);
+        if ((e = produce(g + 1, false)) != hipSuccess) return e;
+      } else {
+        // group g+1's cross with group g's panels: block 2g+2 first (its
+        // panel's chain waits for it), block 2g+3 on side2 meanwhile
+        const int64_t pa = b.poff[2 * (g + 1)], na = (ACE_DIAG_SKIP & 4) ? 0 : b.poff[2 * (g + 1) + 1] - pa;
+        const int64_t pb = b.poff[2 * (g + 1) + 1], nb = (ACE_DIAG_SKIP & 4) ? 0 : b.poff[2 * (g + 1) + 2] - pb;
+        if (na > 0) hipLaunchKernelGGL(k_update_pair, dim3((unsigned)na), dim3(UTHREADS), 0, side, b.A, b.ld,
+                           b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0,
+                           -1, -1, b.ptiles + pa, gout(k + 2), -1, nullptr);
+        if (nb > 0) {
+          if (two2) {
+            if ((e = hipEventRecord(E1(g + 1), side)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(side2, E1(g + 1), 0)) != hipSuccess) return e;
+          }
+          hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nb), dim3(UTHREADS), 0, side2, b.A, b.ld,
+                             b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld,
+                             ka0, -1, -1, b.ptiles + pb, no_gather(), -1, nullptr);
+          if (two2 && (e = hipEventRecord(E2(g + 1), side2)) != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nb), dim3(UTHREADS), 0, side2, b.A, b.ld,
-                           b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld,
-                           ka0, -1, -1, b.ptiles + pb, no_gather());
-        if (two2 && (e = hipEventRecord(E2(g + 1), side2)) != hipSuccess) return e;
+        if ((e = produce(g + 1, nb > 0)) != hipSuccess) return e;
       }
-      if ((e = produce(g + 1, nb > 0)) != hipSuccess) return e;
       if (two && (e = hipEventRecord(sy->ev[2 * (g + 1)], side)) != hipSuccess) return e;
     }
     const bool timed = tm && tm->ev && used + 2 <= tm->nev;
     if (timed) (void)hipEventRecord(tm->ev[used], st);
-    const unsigned grid = b.gorder ? (unsigned)b.glen
-                                   : (b.order ? (unsigned)b.norder : nT * (nT + 1) / 2);
+    unsigned grid = b.gorder ? (unsigned)b.glen
+                             : (b.order ? (unsigned)b.norder : nT * (nT + 1) / 2);
     const Tile *ord = b.gorder ? b.gorder + (int64_t)g * b.glen : b.order;
     const int kx0 = more ? 2 * (g + 1) : -1, kx1 = more ? 2 * (g + 1) + zsize(g + 1) : -1;
+    // merged: [group g+1's cross tiles | the bulk order]
+    const bool mfront = merged && more && zsize(g) == 2;
+    if (mfront) {
+      grid = (unsigned)(b.moff[g + 1] - b.moff[g]);
+      ord = b.morder + b.moff[g];
+    }
     if (zsize(g) == 2)
       hipLaunchKernelGGL(k_update_pair, dim3(grid), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[slot(k)],
                          b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0, kx0, kx1,
-                         ord, no_gather());
+                         ord, mfront ? gout(k + 2) : no_gather(), mfront ? b.mfront[g] : -1,
+                         mfront ? b.mcnt + g : nullptr);
     else
       hipLaunchKernelGGL(k_update, dim3(grid), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[slot(k)],
                          b.P[slot(k)], b.W[slot(k)], b.ld, ka0, -1, ord, 1, no_gather());
     if (timed) {
       (void)hipEventRecord(tm->ev[used + 1], st);
       if (tm->flops)
-        tm->flops[used / 2] = (zsize(g) == 2 ? update_gemm_tiles_pair(naug, ka0, kx0, kx1)
+        tm->flops[used / 2] = (zsize(g) == 2 ? update_gemm_tiles_pair(naug, ka0, mfront ? -1 : kx0,
+                                                                      mfront ? -1 : kx1)
                                              : update_gemm_tiles(naug, ka0, -1, false)) *
                               2.0 * UT * UT * NB;
       used += 2;

@@ -484,8 +484,10 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     So are the second block's cross on its own stream (ACE_SIDE2=0 runs it on
     the panel stream), the cost-sorted bulk order (ACE_TAIL_SORT=1), the
     gather fused into the cross launches (ACE_XGATHER=0: k_gather), one
-    stream for everything (ACE_LOOKAHEAD=0) and the panel GEMM on 128-tiles
-    (ACE_PGEMM_TILES=0: the 64-row k_panel_gemm)."""
+    stream for everything (ACE_LOOKAHEAD=0), the panel GEMM on 128-tiles
+    (ACE_PGEMM_TILES=0: the 64-row k_panel_gemm) and the next group's cross
+    tiles at the head of the bulk launch (ACE_XMERGE=1, with and without the
+    fused gather) instead of side-stream launches."""
     import os
     import subprocess
     import sys
@@ -502,7 +504,10 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
                 "gather": {"ACE_PAIR": "1", "ACE_XGATHER": "0"},
                 "one_stream": {"ACE_PAIR": "1", "ACE_LOOKAHEAD": "0"},
                 "pgemm_rows": {"ACE_PAIR": "1", "ACE_PGEMM_TILES": "0"},
-                "single_pgemm_rows": {"ACE_PAIR": "0", "ACE_PGEMM_TILES": "0"}}
+                "single_pgemm_rows": {"ACE_PAIR": "0", "ACE_PGEMM_TILES": "0"},
+                "merged": {"ACE_PAIR": "1", "ACE_XMERGE": "1"},
+                "merged_gather": {"ACE_PAIR": "1", "ACE_XMERGE": "1", "ACE_XGATHER": "0"},
+                "unmerged": {"ACE_PAIR": "1", "ACE_XMERGE": "0"}}
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)
@@ -551,3 +556,42 @@ def test_split_panel_is_bitwise_neutral(A, tmp_path):
     subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
                    env=env, check=True, timeout=100)
     assert np.array_equal(A.invkernel_cpp(K, th[0])["inv"], np.load(out))
+
+
+_MODEL_SNIPPET = """
+import sys, numpy as np
+sys.path.insert(0, {root!r})
+import additivecausalexpansion_amd as A
+from additivecausalexpansion_amd.synthetic import make_problem
+y, X, Z, th, sy = make_problem({n}, 6, 4, seed=31)
+m = A.DeviceModel("Matern32", {n}, 6, 4)
+m.set_data(y, X, Z, sy)
+outs = []
+for it in (1, 2):
+    g, st, mu = m.para_update(it, th)
+    outs += [g, st, np.array([mu])]
+    th = th + 0.01 * g / max(1.0, float(np.abs(g).max()))
+np.save({out!r}, np.concatenate(outs))
+"""
+
+
+@pytest.mark.parametrize("n", [2000, 2600])
+def test_merged_cross_model_is_bitwise_neutral(tmp_path, n):
+    """The fused model's para_update with the next group's cross tiles at the
+    head of the bulk launch (ACE_XMERGE=1: device counter + side-stream wait
+    kernel) gives the same gradient and stats bit for bit as the side-stream
+    cross launches, over two evaluations (the per-sweep counter reset).
+    n = 2000: 8 steps; 2600: 11 (a last single step)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for v in ("0", "1"):
+        out = str(tmp_path / f"m{v}.npy")
+        env = dict(os.environ, ACE_XMERGE=v)
+        subprocess.run([sys.executable, "-c", _MODEL_SNIPPET.format(root=root, n=n, out=out)],
+                       env=env, check=True, timeout=100)
+        outs[v] = np.load(out)
+    assert np.all(np.isfinite(outs["1"]))
+    assert np.array_equal(outs["0"], outs["1"])
