@@ -611,9 +611,26 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   const int64_t r = R0 + rl;
   const bool rvalid = r < n;
   const double *wlast = (KIND == 1) ? tab.wg + (B - 1) * PM : tab.wk;
+  // the tile's A and alpha values are loaded before the staging (ACE_GRAD_PRELOAD,
+  // default), so their latency overlaps the staging loads and barriers
+#ifndef ACE_GRAD_PRELOAD
+#define ACE_GRAD_PRELOAD 1
+#endif
+  double av[CB][4], alc[CB][4];
+  if (ACE_GRAD_PRELOAD) {
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int64_t c = C0 + cbase + 16 * cb + lk + 4 * v;
+        const bool ok = rvalid && c < n && !(I == J && c > r);
+        av[cb][v] = ok ? A[r + c * ld] : 0.0;
+        alc[cb][v] = ok ? alpha[c] : 0.0;
+      }
+  }
+  const double ar = rvalid ? alpha[r] : 0.0;
   const MmLds L = mm_stage<PM, KIND, true, NT>(lds, S, B, ZS, tab.wk, wlast, R0, C0, tid);
   // T = w_rc (sA A[r,c] - alpha_r alpha_c), w = 2 off the diagonal (lower pairs)
-  const double ar = rvalid ? alpha[r] : 0.0;
   double tv[CB][4];
   double tr = 0.0;
 #pragma unroll
@@ -623,7 +640,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
       const int64_t c = C0 + cbase + 16 * cb + lk + 4 * v;
       double x = 0.0;
       if (rvalid && c < n && !(I == J && c > r)) {
-        x = sA * A[r + c * ld] - ar * alpha[c];
+        x = ACE_GRAD_PRELOAD ? sA * av[cb][v] - ar * alc[cb][v] : sA * A[r + c * ld] - ar * alpha[c];
         if (c == r) tr += x;
         else x *= 2.0;
       }
@@ -673,7 +690,13 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   // of ones / zeros; exact), so no per-pair code tests b: a lane's pairs are
   // one straight-line block the scheduler can interleave (a b == 0 test made
   // every pair its own basic block, running its dependent fp64 chain alone)
-  for (int b = B - 1; b >= 0; --b) {
+  // ACE_DIAG_GRAD (timing diagnostics only, results wrong): 1 runs no slice,
+  // 2 only the last slice
+#ifndef ACE_DIAG_GRAD
+#define ACE_DIAG_GRAD 0
+#endif
+  const int bstop = ACE_DIAG_GRAD == 1 ? B : ACE_DIAG_GRAD == 2 ? B - 1 : 0;
+  for (int b = B - 1; b >= bstop; --b) {
     double *red = L.Red + (per_slice ? b : (b & 1)) * PER;
     double zr = 1.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
     if (b > 0) {
