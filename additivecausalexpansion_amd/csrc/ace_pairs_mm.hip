@@ -38,9 +38,22 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 #ifndef ACE_MM_GRAD_WPE
 #define ACE_MM_GRAD_WPE 4
 #endif
-// Most GEMM2 column blocks accumulated per pass of its k-loop.
+// Most GEMM2 column blocks accumulated per pass of its k-loop (QG2: the
+// 512-thread form, whose register cap allowed one).
 #ifndef ACE_MM_QG
 #define ACE_MM_QG 4
+#endif
+#ifndef ACE_MM_QG2
+#define ACE_MM_QG2 1
+#endif
+// Gradient A/B switches: row sums R_r gathered through LDS (1) or
+// ds_bpermute (0); GEMM2 epilogue row covariates in registers (1: spills at
+// the 4-wave register cap) or read from LDS per slice (0)
+#ifndef ACE_GRAD_RVLDS
+#define ACE_GRAD_RVLDS 0
+#endif
+#ifndef ACE_GRAD_XIREG
+#define ACE_GRAD_XIREG 0
 #endif
 #define MM_PAIR_FENCE(cb, v) \
   if (ACE_MM_PG > 0 && ((4 * (cb) + (v) + 1) % (ACE_MM_PG > 0 ? ACE_MM_PG : 1)) == 0) \
@@ -264,7 +277,7 @@ __device__ __forceinline__ void tile_of(const Tile *tiles, int64_t t, int64_t &I
 // load is issued ahead of each slice's GEMM1.
 // ---------------------------------------------------------------------------
 struct MmLayout {
-  int etab, xj, xi, z, lz, nc, nr, w, red, red_slices, total;
+  int etab, xj, xi, z, lz, nc, nr, w, red, red_slices, rv, total;
 };
 
 // Gradient partials: one buffer per slice (no barrier inside the slice
@@ -298,12 +311,14 @@ __host__ __device__ inline MmLayout mm_layout(int PM, int B, int KIND, bool grad
     o.red_slices = (B * per * 8 <= 40 * 1024) ? B : 2;
     off += o.red_slices * per + nwave;
   }
+  o.rv = off;  // gradient, ACE_GRAD_RVLDS: each wave's 16 row sums R_r of the current slice
+  if (grad && ACE_GRAD_RVLDS) off += 16 * nwave;
   o.total = off;
   return o;
 }
 
 struct MmLds {
-  double *E, *XJ, *XI, *Z, *LZ, *Nc, *Nr, *W, *Red;
+  double *E, *XJ, *XI, *Z, *LZ, *Nc, *Nr, *W, *Red, *Rv;
   int red_slices;
 };
 
@@ -326,6 +341,7 @@ __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS
   L.Nr = lds + o.nr;
   L.W = lds + o.w;
   L.Red = lds + o.red;
+  L.Rv = lds + o.rv;
   L.red_slices = o.red_slices;
   for (int e = tid; e < 64 * PM; e += NT) {
     const int c = e / PM, i = e - c * PM;
@@ -552,6 +568,53 @@ __device__ __forceinline__ double rcp_nr_mm(double f) {
   return fma(q, e, q);
 }
 
+// Lane exchanges of the gradient's slice loop without the LDS crossbar
+// (ACE_GRAD_DPP=1): xor 1 / 2 / 4 / 8 inside a 16-lane row by DPP moves
+// (xor 4 = row_half_mirror, then the quad reversal; xor 8 = row_ror 8),
+// and the xor-16 / xor-32 sums by gfx950's v_permlane16/32_swap.  Each lane
+// gets the same partner value as __shfl_xor (ds_bpermute), and a + b is
+// commutative, so the sums are bit-identical.
+#ifndef ACE_GRAD_DPP
+#define ACE_GRAD_DPP 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+// v of lane (this lane xor m), m = 1, 2, 4, 8
+__device__ __forceinline__ double xor_row(double v, int m) {
+  if (!ACE_GRAD_DPP) return __shfl_xor(v, m, 64);
+  if (m == 1) return dpp64<0xB1>(v);          // quad_perm [1,0,3,2]
+  if (m == 2) return dpp64<0x4E>(v);          // quad_perm [2,3,0,1]
+  if (m == 4) return dpp64<0x1B>(dpp64<0x141>(v));  // xor 7, then xor 3
+  return dpp64<0x128>(v);                     // row_ror 8
+}
+__device__ __forceinline__ double pair_sum(int a_lo, int a_hi, int b_lo, int b_hi) {
+  const double a = __longlong_as_double((long long)(((unsigned long long)(unsigned)a_hi << 32) | (unsigned)a_lo));
+  const double b = __longlong_as_double((long long)(((unsigned long long)(unsigned)b_hi << 32) | (unsigned)b_lo));
+  return a + b;
+}
+// v + v(lane xor 16), v + v(lane xor 32), in every lane
+__device__ __forceinline__ double add_xor16(double v) {
+  if (!ACE_GRAD_DPP) return v + __shfl_xor(v, 16, 64);
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = (int)(unsigned)u, hi = (int)(unsigned)(u >> 32);
+  const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return pair_sum(l[0], h[0], l[1], h[1]);
+}
+__device__ __forceinline__ double add_xor32(double v) {
+  if (!ACE_GRAD_DPP) return v + __shfl_xor(v, 32, 64);
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = (int)(unsigned)u, hi = (int)(unsigned)(u >> 32);
+  const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return pair_sum(l[0], h[0], l[1], h[1]);
+}
+
 // CB = column blocks (16 wide) per wave.  CB = 4: 256 threads, every wave
 // holds 16 rows x 64 columns (16 pairs per lane, 2 workgroups per CU).
 // CB = 2: 512 threads, wave w holds rows 16 (w & 3).., columns 32 (w >> 2)..
@@ -576,7 +639,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   constexpr int NV = PM + 1;
   constexpr int NQ = (PM + 15) / 16;         // GEMM2 16-wide column blocks
   // GEMM2 column blocks per pass of its k-loop (one at CB = 2: register cap)
-  constexpr int QG = CB == 2 ? 1 : (NQ < ACE_MM_QG ? NQ : ACE_MM_QG);
+  constexpr int QG = CB == 2 ? (NQ < ACE_MM_QG2 ? NQ : ACE_MM_QG2) : (NQ < ACE_MM_QG ? NQ : ACE_MM_QG);
   constexpr int RS = PM + 1;                 // partial row: [x part | T K]
   constexpr int PER = NWV * RS + 4 * 64;     // per-slice partials (+ column sums)
   constexpr int NKK = 4 * CB;                // GEMM2 k-steps (the wave's columns / 4)
@@ -648,6 +711,19 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
     }
   RowX<PM, XIL> xr;  // x_r from the staged rows when they are in LDS
   xr.load(XIL ? L.XI + rl * (PM + 1) : S.X + r * PM, lk);
+  // GEMM2 epilogue row covariates x[16 wr + lk + 4 v][16 q + lr]: the same
+  // for every slice, so held in registers (ACE_GRAD_XIREG) where they fit
+  constexpr bool XIR = ACE_GRAD_XIREG && XIL && CB == 2 && NQ <= 2;
+  double xiv[XIR ? NQ : 1][4];
+  if (XIR) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int nn = 16 * q + lr;
+        xiv[q][v] = nn < PM ? L.XI[(16 * wr + lk + 4 * v) * (PM + 1) + nn] : 0.0;
+      }
+  }
   double fc[CB][4];  // Matern: 1 + sqrt3 t of slice b+1
   d4 acc[CB];
   if (KIND == 1) {  // Matern, last slice: r~2 with its own weights
@@ -691,11 +767,12 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   // one straight-line block the scheduler can interleave (a b == 0 test made
   // every pair its own basic block, running its dependent fp64 chain alone)
   // ACE_DIAG_GRAD (timing diagnostics only, results wrong): 1 runs no slice,
-  // 2 only the last slice
+  // 2 only the last slice; bits 4 / 8 / 16 / 32 drop the sqrt / exp /
+  // reciprocal / GEMM2 of the Matern slice loop
 #ifndef ACE_DIAG_GRAD
 #define ACE_DIAG_GRAD 0
 #endif
-  const int bstop = ACE_DIAG_GRAD == 1 ? B : ACE_DIAG_GRAD == 2 ? B - 1 : 0;
+  const int bstop = (ACE_DIAG_GRAD & 3) == 1 ? B : (ACE_DIAG_GRAD & 3) == 2 ? B - 1 : 0;
   for (int b = B - 1; b >= bstop; --b) {
     double *red = L.Red + (per_slice ? b : (b & 1)) * PER;
     double zr = 1.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
@@ -733,9 +810,9 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
                             exp_grad(((lam - r2) + (rlo ? lzr : lzc)) + (rlo ? lzc : lzr), L.E);
           kb = sel_f64(zlo == 0.0 || zhi == 0.0, 0.0, kz);
         } else {
-          const double tt = sqrt_gs(r2);
+          const double tt = (ACE_DIAG_GRAD & 4) ? r2 : sqrt_gs(r2);
           f = 1.0 + SQRT3 * tt;
-          const double e = f * exp_grad(lam - SQRT3 * tt, L.E);
+          const double e = (ACE_DIAG_GRAD & 8) ? f * (lam - SQRT3 * tt) : f * exp_grad(lam - SQRT3 * tt, L.E);
           // z = 0 gives a zero product (of either sign: it only enters sums)
           kb = (e * zlo) * zhi;
         }
@@ -745,7 +822,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
         if (KIND == 0) {
           u = tk;
         } else {
-          u = tk * rcp_nr_mm(fc[cb][v]);
+          u = (ACE_DIAG_GRAD & 16) ? tk * fc[cb][v] : tk * rcp_nr_mm(fc[cb][v]);
           fc[cb][v] = f;
         }
         acc[cb][v] = u;
@@ -753,14 +830,25 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
         MM_PAIR_FENCE(cb, v);
       }
     // R_r: row sums of U over the wave's columns (lanes of one lr hold the 4 quarters)
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
+    rs = add_xor16(rs);
+    rs = add_xor32(rs);
     double Rv[4];
+    if (ACE_GRAD_RVLDS) {
+      // through the wave's LDS slot: one write, four reads (LDS operations of
+      // one wave execute in order) instead of four 64-bit ds_bpermute pairs
+      double *rvs = L.Rv + 16 * w;
+      if (lk == 0) rvs[lr] = rs;
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int v = 0; v < 4; ++v) Rv[v] = __shfl(rs, lk + 4 * v, 64);  // row 16 wr + lk + 4v
+      for (int v = 0; v < 4; ++v) Rv[v] = rvs[lk + 4 * v];
+      __builtin_amdgcn_wave_barrier();
+    } else {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) Rv[v] = __shfl(rs, lk + 4 * v, 64);  // row 16 wr + lk + 4v
+    }
     // GEMM2: V = U X_J, QG column blocks per pass of the k-loop
 #pragma unroll
-    for (int q0 = 0; q0 < NQ; q0 += QG) {
+    for (int q0 = 0; q0 < ((ACE_DIAG_GRAD & 32) ? 0 : NQ); q0 += QG) {
       d4 a2[QG];
 #pragma unroll
       for (int j = 0; j < QG; ++j) a2[j] = d4{0.0, 0.0, 0.0, 0.0};
@@ -786,12 +874,13 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
             const int rr = 16 * wr + lk + 4 * v;
-            const double x = XIL ? L.XI[rr * (PM + 1) + nn] : S.X[(R0 + rr) * PM + nn];
+            const double x = XIR ? xiv[q0 + j][v]
+                                 : XIL ? L.XI[rr * (PM + 1) + nn] : S.X[(R0 + rr) * PM + nn];
             part += fma(x * x, Rv[v], -2.0 * x * a2[j][v]);
           }
         }
-        part += __shfl_xor(part, 16, 64);
-        part += __shfl_xor(part, 32, 64);
+        part = add_xor16(part);
+        part = add_xor32(part);
         if (lk == 0 && nn < PM) red[w * RS + nn] = part;
       }
     }
@@ -815,23 +904,23 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
             const double lo = cv[j], hi = cv[j + h];
             const double mine = sel_f64(up, hi, lo);
             const double other = sel_f64(up, lo, hi);
-            cv[j] = mine + __shfl_xor(other, m, 64);
+            cv[j] = mine + xor_row(other, m);
           }
           if (up) kk0 += h;
           cnt = h;
         } else {
-          cv[0] += __shfl_xor(cv[0], m, 64);
+          cv[0] += xor_row(cv[0], m);
         }
       }
       if ((lr & (16 / NVAL - 1)) == 0)
         red[NWV * RS + wr * 64 + cbase + 16 * (kk0 >> 2) + lk + 4 * (kk0 & 3)] = cv[0];
     }
-    gl += __shfl_xor(gl, 1, 64);
-    gl += __shfl_xor(gl, 2, 64);
-    gl += __shfl_xor(gl, 4, 64);
-    gl += __shfl_xor(gl, 8, 64);
-    gl += __shfl_xor(gl, 16, 64);
-    gl += __shfl_xor(gl, 32, 64);
+    gl += xor_row(gl, 1);
+    gl += xor_row(gl, 2);
+    gl += xor_row(gl, 4);
+    gl += xor_row(gl, 8);
+    gl = add_xor16(gl);
+    gl = add_xor32(gl);
     if (lane == 0) red[w * RS + PM] = gl;
     if (!per_slice) {
       __syncthreads();  // the waves' partials of slice b are in red
@@ -839,12 +928,12 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
     }
   }
   // trace of T
-  tr += __shfl_xor(tr, 1, 64);
-  tr += __shfl_xor(tr, 2, 64);
-  tr += __shfl_xor(tr, 4, 64);
-  tr += __shfl_xor(tr, 8, 64);
-  tr += __shfl_xor(tr, 16, 64);
-  tr += __shfl_xor(tr, 32, 64);
+  tr += xor_row(tr, 1);
+  tr += xor_row(tr, 2);
+  tr += xor_row(tr, 4);
+  tr += xor_row(tr, 8);
+  tr = add_xor16(tr);
+  tr = add_xor32(tr);
   double *str = L.Red + L.red_slices * PER;
   if (lane == 0) str[w] = tr;
   __syncthreads();
