@@ -447,8 +447,15 @@ __device__ __forceinline__ void gemm1_mm(const double *sXJ, const RowX<PM, FP> &
 // panels' columns, at most all of them
 __host__ __device__ inline int asm_first_cols(int nt) { return 2 * NB / AT < nt ? 2 * NB / AT : nt; }
 
+// Column blocks per wave of the assembly: ACE_ASM_CB = 4 (256 threads, 16
+// pairs per lane) or 2 (512 threads, wave w: rows 16 (w & 3).., columns
+// 32 (w >> 2)..; 8 pairs per lane), the gradient kernel's layout.
+#ifndef ACE_ASM_CB
+#define ACE_ASM_CB 4
+#endif
+constexpr int ASM_NT = 64 * 4 * (4 / ACE_ASM_CB);
 template <int PM, int KIND>
-__global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, int B, int ZS, TabView tab,
+__global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, int B, int ZS, TabView tab,
                                                 double sig, double *__restrict__ out, int64_t ld,
                                                 double *__restrict__ kcopy,
                                                 const Tile *__restrict__ tiles, int G, int part,
@@ -481,18 +488,20 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
     out += coff * ld;
     if (kcopy) kcopy += coff * ld;
   }
+  constexpr int CB = ACE_ASM_CB;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
+  const int wr = w & 3, cbase = 16 * CB * (w >> 2);
   const int64_t R0 = I * AT, C0 = J * AT, n = S.n;
-  const int rl = 16 * w + lr;
+  const int rl = 16 * wr + lr;
   const int64_t r = R0 + rl;
   constexpr int XP = PM + 1;
-  const MmLds L = mm_stage<PM, KIND, false>(lds, S, B, ZS, tab.wk, tab.wk, R0, C0, tid);
+  const MmLds L = mm_stage<PM, KIND, false, ASM_NT>(lds, S, B, ZS, tab.wk, tab.wk, R0, C0, tid);
   RowX<PM> xr;
   xr.load(S.X + r * PM, lk);
-  double kf[4][4];
+  double kf[CB][4];
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb)
+  for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
     for (int v = 0; v < 4; ++v) kf[cb][v] = 0.0;
   // diagonal tiles (I == J) need the r == c and r < c tests; below the
@@ -505,23 +514,23 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
         zr = S.Z[r * ZS + b - 1];
         if (KIND == 0) lzr = S.LZ[r * ZS + b - 1];
       }
-      d4 acc[4];
-      gemm1_mm<XP>(L.XJ, xr, L.W + b * PM, lr, lk, acc);
+      d4 acc[CB];
+      gemm1_mm<XP, CB>(L.XJ, xr, L.W + b * PM, lr, lk, acc, cbase);
       const double sr = L.Nr[b * 64 + rl];
-      const double *nc = L.Nc + b * 64;
+      const double *nc = L.Nc + b * 64 + cbase;
       const double lam = tab.lam[b];
   #pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
+      for (int cb = 0; cb < CB; ++cb)
   #pragma unroll
         for (int v = 0; v < 4; ++v) {
           const int cl = 16 * cb + lk + 4 * v;
-          const int64_t c = C0 + cl;
+          const int64_t c = C0 + cbase + cl;
           double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), 0.0);
           if (DG && c == r) r2 = 0.0;
           double zc = 0.0, lzc = 0.0;
           if (b > 0) {
-            zc = L.Z[(b - 1) * 64 + cl];
-            if (KIND == 0) lzc = L.LZ[(b - 1) * 64 + cl];
+            zc = L.Z[(b - 1) * 64 + cbase + cl];
+            if (KIND == 0) lzc = L.LZ[(b - 1) * 64 + cbase + cl];
           }
           const double kb = (DG && r < c) ? kval_mm<KIND>(b, r2, lam, zr, zc, lzr, lzc, L.E)
                                           : kval_mm<KIND>(b, r2, lam, zc, zr, lzc, lzr, L.E);
@@ -533,10 +542,10 @@ __global__ __launch_bounds__(256, (PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, 
   if (I == J) slices(std::true_type{});
   else slices(std::false_type{});
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb)
+  for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const int64_t c = C0 + 16 * cb + lk + 4 * v;
+      const int64_t c = C0 + cbase + 16 * cb + lk + 4 * v;
       if (r < n && c < n) {
         out[r + c * ld] = (r == c) ? kf[cb][v] + sg : kf[cb][v];
         if (kcopy) kcopy[r + c * ld] = kf[cb][v];
@@ -1078,10 +1087,10 @@ static hipError_t asm_mm_pm(int kind, PairSide S, int64_t npad, int B, int ZS, T
     if (e != hipSuccess) return e;
   }
   if (kind == 0)
-    hipLaunchKernelGGL((k_asm_mm<PM, 0>), dim3((unsigned)nblk), dim3(256), lds, st, S, B, ZS,
+    hipLaunchKernelGGL((k_asm_mm<PM, 0>), dim3((unsigned)nblk), dim3(ASM_NT), lds, st, S, B, ZS,
                        tab, sig, out, ld, kcopy, tiles, G, part, (int)nt);
   else
-    hipLaunchKernelGGL((k_asm_mm<PM, 1>), dim3((unsigned)nblk), dim3(256), lds, st, S, B, ZS,
+    hipLaunchKernelGGL((k_asm_mm<PM, 1>), dim3((unsigned)nblk), dim3(ASM_NT), lds, st, S, B, ZS,
                        tab, sig, out, ld, kcopy, tiles, G, part, (int)nt);
   return hipGetLastError();
 }
