@@ -337,6 +337,17 @@ hipError_t launch_symm(const double *A, int64_t ld, int64_t n, int G, int rank, 
 // a[c] = sum_q T[q + c ldt] w[q], d[c] = sum_q T[q + c ldt] K[c + q ldk], c < nx
 hipError_t launch_pred_cols(const double *T, int64_t ldt, const double *K, int64_t ldk, int64_t n,
                             int64_t nx, const double *w, double *a, double *d, hipStream_t st);
+// single GPU: out (n x k, ldo) = scale * L V^T, L the strictly lower part of
+// the stored matrix, V given as k x n (V[p][c] = V[c + p ldv])
+hipError_t launch_trmm_lower(const double *A, int64_t ld, int64_t n, const double *V, int64_t ldv,
+                             int64_t k, double scale, double *out, int64_t ldo, hipStream_t st);
+// a[c] = sum_q K[c][q] s[q], d[c] = sum_q K[c][q] (2 Y[q][c] + D[q] K[c][q])
+hipError_t launch_pred_cols_tri(const double *Y, int64_t ldt, const double *K, int64_t ldk,
+                                int64_t n, int64_t nx, const double *sv, const double *D, double *a,
+                                double *d, hipStream_t st);
+// D[q] = scale * A[q + q ld], q < n
+hipError_t launch_diag_scaled(const double *A, int64_t ld, int64_t n, double scale, double *D,
+                              hipStream_t st);
 // w = y - mu
 hipError_t launch_center(const double *y, int64_t n, double mu, double *w, hipStream_t st);
 

@@ -170,6 +170,12 @@ struct PredOps {
   // out (n x k, ld n) = A^-1 V^T for V = K_xX rows (k x n, ld ldv): this
   // rank's share when sharded (summed by allreduce)
   std::function<void(const double *V, int64_t ldv, int64_t k, double *out, DBuf &tmp)> symm;
+  // optional (single GPU, ACE_PRED_TRI): the triangular form of the variance.
+  // trmm: out (n x k) = L V^T, L the strictly lower part of A^-1; symv: out
+  // (n x k) = A^-1 V for V n x k (ld ldv); sdiag: diag(A^-1) (n)
+  std::function<void(const double *V, int64_t ldv, int64_t k, double *out)> trmm;
+  std::function<void(const double *V, int64_t ldv, int64_t k, double *out, DBuf &tmp)> symv;
+  const double *sdiag = nullptr;
   std::function<void(double *buf, int64_t count)> allreduce;  // empty: single process
   // K_xX rows c0 .. c0 + nc (marginal slice sum for predict_marginal): a
   // device pointer with leading dimension *ld, possibly built in scratch

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <vector>
 
@@ -64,6 +65,18 @@ void symm_resident(ace_model *m, const double *V, int64_t ldv, bool vt, int64_t 
   }
 }
 
+// ACE_PRED_TRI (default 1): single-GPU prediction takes the variance's
+// quadratic form through the strictly lower triangle of A^-1 (half the
+// MFMA work of the full symmetric product; 0 = the full product, A/B)
+bool pred_tri() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_PRED_TRI");
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
 void require_inverse(ace_model *m) {
   arg(m->ctx, m->has_data, "ace_model_set_data() not called");
   arg(m->ctx, m->has_inverse, "no resident inverse: call ace_model_para_update() first");
@@ -101,24 +114,42 @@ void pred_pipeline(const PredOps &op, int64_t nx, bool marginal, const double *Z
     ck(ctx, launch_fill(dS3.d(), 3 * n, 0.0, st), "zero");
     ck(ctx, launch_fill(dU3.d(), 3 * n, 0.0, st), "zero");
   }
+  // triangular form (op.trmm): the variance from Y = L K_xX^T, L the
+  // strictly lower part of A^-1 (half of the full product's flops), the map
+  // from s = A^-1 w, and u_j = A^-1 s_j once after the loop
+  const bool tri = (bool)op.trmm;
+  DBuf dsv;
+  if (tri) {
+    alloc(ctx, dsv, (size_t)n * sizeof(double), "alloc s");
+    op.symv(op.w, n, 1, dsv.d(), dtmp);
+  }
   for (int64_t c0 = 0; c0 < nx; c0 += chunk) {
     const int64_t nc = std::min<int64_t>(chunk, nx - c0);
     int64_t ldk = 0;
     const double *Kc = op.cross(c0, nc, &ldk, dKc);  // K_xX rows c0 .. c0 + nc
-    // T' = A^-1 K_xX^T (n x nc): the transpose of tmp = K_xX invK_XX
-    op.symm(Kc, ldk, nc, dT.d(), dtmp);
-    ck(ctx, launch_pred_cols(dT.d(), n, Kc, ldk, n, nc, op.w, dad.d() + c0, dad.d() + nx + c0, st),
-       "pred sums");
+    if (tri) {
+      op.trmm(Kc, ldk, nc, dT.d());
+      ck(ctx, launch_pred_cols_tri(dT.d(), n, Kc, ldk, n, nc, dsv.d(), op.sdiag, dad.d() + c0,
+                                   dad.d() + nx + c0, st),
+         "pred sums");
+    } else {
+      // T' = A^-1 K_xX^T (n x nc): the transpose of tmp = K_xX invK_XX
+      op.symm(Kc, ldk, nc, dT.d(), dtmp);
+      ck(ctx, launch_pred_cols(dT.d(), n, Kc, ldk, n, nc, op.w, dad.d() + c0, dad.d() + nx + c0, st),
+         "pred sums");
+    }
     if (ate)
       for (int j = 0; j < 3; ++j) {
         const double *wj = dW3.d() + j * nx + c0;
         // s_j += K_xX^T w_j, u_j += T' w_j = A^-1 K_xX^T w_j
         ck(ctx, launch_gemv_t(Kc, ldk, nc, n, wj, dvt.d(), st), "gemv_t");
         ck(ctx, launch_add(dvt.d(), dS3.d() + j * n, n, st), "add");
+        if (tri) continue;
         ck(ctx, launch_gemv(dT.d(), n, n, nc, wj, dvt.d(), st), "gemv");
         ck(ctx, launch_add(dvt.d(), dU3.d() + j * n, n, st), "add");
       }
   }
+  if (tri && ate) op.symv(dS3.d(), n, 3, dU3.d(), dtmp);  // u_j = A^-1 s_j
   op.kdiag(dkd.d());
   std::vector<double> q3(3, 0.0), dots(3, 0.0);
   if (ate) {
@@ -184,6 +215,18 @@ void predict_impl(ace_model *m, const double *theta, int64_t nx, const double *X
   op.symm = [&](const double *V, int64_t ldv, int64_t k, double *out, DBuf &tmp) {
     symm_resident(m, V, ldv, true, k, out, tmp);
   };
+  DBuf ddiag;
+  if (!m->shard && pred_tri()) {  // -A^-1 is stored: scale -1
+    alloc(ctx, ddiag, (size_t)n * sizeof(double), "alloc diag");
+    ck(ctx, launch_diag_scaled(m->sw.A.d(), m->naug, n, -1.0, ddiag.d(), st), "diag");
+    op.sdiag = ddiag.d();
+    op.trmm = [&](const double *V, int64_t ldv, int64_t k, double *out) {
+      ck(ctx, launch_trmm_lower(m->sw.A.d(), m->naug, n, V, ldv, k, -1.0, out, n, st), "trmm");
+    };
+    op.symv = [&](const double *V, int64_t ldv, int64_t k, double *out, DBuf &tmp) {
+      symm_resident(m, V, ldv, false, k, out, tmp);
+    };
+  }
   if (m->shard) op.allreduce = [&](double *b, int64_t c) { shard_allreduce_sum(m->shard, b, c); };
   op.cross = [&](int64_t c0, int64_t nc, int64_t *ld, DBuf &scratch) -> const double * {
     alloc(ctx, scratch, (size_t)(nc * n) * sizeof(double), "alloc K_xX");

@@ -34,7 +34,12 @@ constexpr int SR = 128, SC = 64, SBK = 16;
 constexpr int SLS = SR + 16;  // LDS pitch of the S stage
 constexpr int SLV = SC + 16;  // LDS pitch of the V stage
 
-template <bool VT>
+// TRI (single GPU): Out = scale L V with L the STRICTLY lower part of the
+// stored matrix (row q, column p < q) -- the k-chunks below the tile's rows
+// and the masked diagonal block only, so half of k_symm's MFMA work on
+// average and only coalesced column loads (prediction's variance, see
+// k_pred_cols_tri).
+template <bool VT, bool TRI>
 __global__ __launch_bounds__(256) void k_symm(const double *__restrict__ A, int64_t ld, int64_t n,
                                               int G, int rank, const double *__restrict__ V,
                                               int64_t ldv, int64_t k, double scale,
@@ -57,6 +62,7 @@ __global__ __launch_bounds__(256) void k_symm(const double *__restrict__ A, int6
   // chunk class of k-chunk kk: 0 skip, 1 lower (all p < q), 2 upper (all
   // p > q), 3 mixed (the chunk crosses the tile's rows: same NB block)
   auto cls = [&](int64_t kk) -> int {
+    if (TRI) return kk + SBK <= R0 ? 1 : (kk < R0 + SR ? 4 : 0);
     if (kk + SBK <= R0) return owns_col(kk, G, rank) ? 1 : 0;
     if (kk >= R0 + SR) return rowown ? 2 : 0;
     return rowown ? 3 : 0;
@@ -77,6 +83,12 @@ __global__ __launch_bounds__(256) void k_symm(const double *__restrict__ A, int6
       for (int e = 0; e < 8; ++e) {
         const int64_t p = kk + tj + e;
         rs[e] = (q < n && p < n) ? col[p] : 0.0;
+      }
+    } else if (c == 4) {  // TRI diagonal block: row q, column p < q only
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int64_t p = kk + si, q = R0 + sm + e;
+        rs[e] = (q < n && p < n && q > p) ? A[q + p * ld] : 0.0;
       }
     } else {
 #pragma unroll
@@ -123,20 +135,21 @@ __global__ __launch_bounds__(256) void k_symm(const double *__restrict__ A, int6
 #pragma unroll
     for (int ri = 0; ri < 2; ++ri) acc[ci][ri] = d4{0.0, 0.0, 0.0, 0.0};
   // the owned chunks, in order; cur / nxt chunk and their classes
+  const int64_t kend = TRI ? (n < R0 + SR ? n : R0 + SR) : n;
   int64_t kk = 0;
   int c = 0;
-  while (kk < n && (c = cls(kk)) == 0) kk += SBK;
-  if (kk < n) {
+  while (kk < kend && (c = cls(kk)) == 0) kk += SBK;
+  if (kk < kend) {
     load(kk, c);
     store(0, c);
   }
   __syncthreads();
   int buf = 0;
-  while (kk < n) {
+  while (kk < kend) {
     int64_t kn = kk + SBK;
     int cn = 0;
-    while (kn < n && (cn = cls(kn)) == 0) kn += SBK;
-    if (kn < n) load(kn, cn);
+    while (kn < kend && (cn = cls(kn)) == 0) kn += SBK;
+    if (kn < kend) load(kn, cn);
 #pragma unroll
     for (int q4 = 0; q4 < SBK / 4; ++q4) {
       double a[4], b[2];
@@ -150,7 +163,7 @@ __global__ __launch_bounds__(256) void k_symm(const double *__restrict__ A, int6
         for (int ri = 0; ri < 2; ++ri)
           acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
     }
-    if (kn < n) store(buf ^ 1, cn);
+    if (kn < kend) store(buf ^ 1, cn);
     __syncthreads();
     buf ^= 1;
     kk = kn;
@@ -175,11 +188,20 @@ hipError_t launch_symm(const double *A, int64_t ld, int64_t n, int G, int rank, 
   if (n <= 0 || k <= 0) return hipSuccess;
   const dim3 grid((unsigned)((k + SC - 1) / SC), (unsigned)((n + SR - 1) / SR));
   if (vt)
-    hipLaunchKernelGGL(k_symm<true>, grid, dim3(256), 0, st, A, ld, n, G, rank, V, ldv, k, scale,
-                       out, ldo);
+    hipLaunchKernelGGL((k_symm<true, false>), grid, dim3(256), 0, st, A, ld, n, G, rank, V, ldv, k,
+                       scale, out, ldo);
   else
-    hipLaunchKernelGGL(k_symm<false>, grid, dim3(256), 0, st, A, ld, n, G, rank, V, ldv, k, scale,
-                       out, ldo);
+    hipLaunchKernelGGL((k_symm<false, false>), grid, dim3(256), 0, st, A, ld, n, G, rank, V, ldv, k,
+                       scale, out, ldo);
+  return hipGetLastError();
+}
+
+hipError_t launch_trmm_lower(const double *A, int64_t ld, int64_t n, const double *V, int64_t ldv,
+                             int64_t k, double scale, double *out, int64_t ldo, hipStream_t st) {
+  if (n <= 0 || k <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((k + SC - 1) / SC), (unsigned)((n + SR - 1) / SR));
+  hipLaunchKernelGGL((k_symm<true, true>), grid, dim3(256), 0, st, A, ld, n, 1, 0, V, ldv, k, scale,
+                     out, ldo);
   return hipGetLastError();
 }
 
@@ -223,6 +245,65 @@ hipError_t launch_pred_cols(const double *T, int64_t ldt, const double *K, int64
   if (nx <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_pred_cols, dim3((unsigned)nx), dim3(256), 0, st, T, ldt, K, ldk, n, w, a,
                      d);
+  return hipGetLastError();
+}
+
+// Triangular form (single GPU): with S = L + L^T + D (L strictly lower),
+// Y = L K^T (n x nx, ld ldt) from launch_trmm_lower and s = S w:
+//   a[c] = sum_q K[c][q] s[q]
+//   d[c] = (K S K^T)[c][c] = sum_q K[c][q] (2 Y[q][c] + D[q] K[c][q])
+__global__ __launch_bounds__(256) void k_pred_cols_tri(const double *__restrict__ Y, int64_t ldt,
+                                                       const double *__restrict__ K, int64_t ldk,
+                                                       int64_t n, const double *__restrict__ sv,
+                                                       const double *__restrict__ D,
+                                                       double *__restrict__ a,
+                                                       double *__restrict__ d) {
+  __shared__ double sh[2][4];
+  const int64_t c = blockIdx.x;
+  const double *yc = Y + c * ldt;
+  double sa = 0.0, sd = 0.0;
+  for (int64_t q = threadIdx.x; q < n; q += 256) {
+    const double kq = K[c + q * ldk];
+    sa = fma(kq, sv[q], sa);
+    sd = fma(kq, fma(D[q], kq, 2.0 * yc[q]), sd);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    sa += __shfl_xor(sa, o, 64);
+    sd += __shfl_xor(sd, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    sh[0][wv] = sa;
+    sh[1][wv] = sd;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a[c] = (sh[0][0] + sh[0][1]) + (sh[0][2] + sh[0][3]);
+    d[c] = (sh[1][0] + sh[1][1]) + (sh[1][2] + sh[1][3]);
+  }
+}
+
+hipError_t launch_pred_cols_tri(const double *Y, int64_t ldt, const double *K, int64_t ldk,
+                                int64_t n, int64_t nx, const double *sv, const double *D, double *a,
+                                double *d, hipStream_t st) {
+  if (nx <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pred_cols_tri, dim3((unsigned)nx), dim3(256), 0, st, Y, ldt, K, ldk, n, sv,
+                     D, a, d);
+  return hipGetLastError();
+}
+
+// D[q] = scale A[q][q] (the diagonal of the stored matrix)
+__global__ void k_diag_scaled(const double *__restrict__ A, int64_t ld, int64_t n, double scale,
+                              double *__restrict__ D) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n) D[q] = scale * A[q + q * ld];
+}
+
+hipError_t launch_diag_scaled(const double *A, int64_t ld, int64_t n, double scale, double *D,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(k_diag_scaled, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A, ld, n,
+                     scale, D);
   return hipGetLastError();
 }
 

@@ -175,3 +175,51 @@ def test_predict_before_para_update_raises(A):
     m.set_data(y, X, Z, sy)
     with pytest.raises(A.AceError, match="ARG"):
         m.predict(th, X[:5], Z[:5], 0.0, 1.0)
+
+
+_TRI_SNIPPET = """
+import sys, numpy as np
+sys.path.insert(0, {root!r})
+import additivecausalexpansion_amd as A
+from additivecausalexpansion_amd.synthetic import make_problem
+y, X, Z, th, sy = make_problem({n}, 8, 6, seed=41)
+m = A.DeviceModel({kernel!r}, {n}, 8, 6)
+m.set_data(y, X, Z, sy)
+m.para_update(2, th.copy())
+th2 = th + 0.01
+_, X2, Z2, _, _ = make_problem({nx}, 8, 6, seed=42)
+p = m.predict(th2, X2, Z2, 0.2, 1.4)
+zx = (np.arange({nx}) % 2 == 0).astype(float)
+q = m.predict_marginal(th2, X2, np.asfortranarray(0.5 * Z2), zx, 1.4, 0.9, True)
+out = [p["map"], p["var"], q["map"], q["var"]]
+for k in ("ate", "att", "atu"):
+    out += [np.atleast_1d(q[k]["map"]), np.atleast_1d(q[k]["var"])]
+np.save({out!r}, np.concatenate([np.ravel(v) for v in out]))
+"""
+
+
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+def test_triangular_variance_matches_full_product(tmp_path, kernel):
+    """The single-GPU prediction's triangular form (ACE_PRED_TRI=1, default:
+    Y = L K_xX^T with L the strictly lower part of A^-1, d = K (2Y + D K),
+    the map from A^-1 w, u_j = A^-1 s_j) against the full symmetric product
+    (ACE_PRED_TRI=0): predict and predict_marginal with ATE/ATT/ATU at
+    n = 2300 (a diagonal block cut by n), nx = 700, to 1e-9 of the scale of
+    each output (the two forms only round differently)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for v in ("0", "1"):
+        out = str(tmp_path / f"p{v}.npy")
+        env = dict(os.environ, ACE_PRED_TRI=v)
+        subprocess.run([sys.executable, "-c",
+                        _TRI_SNIPPET.format(root=root, n=2300, nx=700, kernel=kernel, out=out)],
+                       env=env, check=True, timeout=100)
+        outs[v] = np.load(out)
+    a, b = outs["0"], outs["1"]
+    assert a.shape == b.shape and np.all(np.isfinite(a) == np.isfinite(b))
+    f = np.isfinite(a)
+    scale = np.max(np.abs(a[f]))
+    assert np.max(np.abs(a[f] - b[f])) <= 1e-9 * scale
