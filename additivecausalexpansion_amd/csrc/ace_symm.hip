@@ -24,6 +24,8 @@
 // 256 threads, 128 (rows) x 64 (columns) output tile, 4 waves of 32 x 64
 // (2 x 4 v_mfma_f64_16x16x4_f64 fragments), BK = 16 k-chunks staged
 // through LDS with a register prefetch of the next chunk.
+#include <cstdlib>
+
 #include "ace_internal.h"
 
 namespace ace {
@@ -196,9 +198,104 @@ hipError_t launch_symm(const double *A, int64_t ld, int64_t n, int G, int rank, 
   return hipGetLastError();
 }
 
+// The triangular product on the sweep update's tile machinery (ACE_TRMM_BIG,
+// default): 512 threads, 128 x 128 output tiles (8 waves of 64 x 32), BK =
+// 16 chunks through double-buffered LDS with a register prefetch.  Row tiles
+// are taken bottom-up (blockIdx.y = 0 is the last row tile, the longest k
+// range), so the cheap tiles form the launch's tail.
+constexpr int TT = 128, TBK = 16, TLD = TT + 16;
+__global__ __launch_bounds__(512, 2) void k_trmm_lower(const double *__restrict__ A, int64_t ld,
+                                                       int64_t n, const double *__restrict__ V,
+                                                       int64_t ldv, int64_t k, double scale,
+                                                       double *__restrict__ out, int64_t ldo) {
+  __shared__ __attribute__((aligned(16))) double sS[2][TBK][TLD];  // [p][q - R0]
+  __shared__ __attribute__((aligned(16))) double sV[2][TBK][TLD];  // [p][c - C0]
+  const int64_t nrt = (n + TT - 1) / TT;
+  const int64_t R0 = (nrt - 1 - (int64_t)blockIdx.y) * TT, C0 = (int64_t)blockIdx.x * TT;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int wr = wv & 1, wc = wv >> 1;  // rows 64 wr.., columns 32 wc..
+  const int sp = tid >> 5, sm = (tid & 31) * 4;  // staging: chunk row sp, 4 consecutive entries
+  const int64_t kend = n < R0 + TT ? n : R0 + TT;
+  double rs[4], rv[4];
+  auto load = [&](int64_t kk) {
+    const int64_t p = kk + sp;
+    const bool diag = kk + TBK > R0;  // the chunk reaches the tile's rows: keep p < q only
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t q = R0 + sm + e, c = C0 + sm + e;
+      rs[e] = (p < n && q < n && (!diag || q > p)) ? A[q + p * ld] : 0.0;
+      rv[e] = (p < n && c < k) ? V[c + p * ldv] : 0.0;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sS[buf][sp][sm + e] = rs[e];
+      sV[buf][sp][sm + e] = rv[e];
+    }
+  };
+  d4 acc[2][4];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 4; ++ri) acc[ci][ri] = d4{0.0, 0.0, 0.0, 0.0};
+  if (kend > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int64_t kk = 0; kk < kend; kk += TBK) {
+    const bool more = kk + TBK < kend;
+    if (more) load(kk + TBK);
+#pragma unroll
+    for (int q4 = 0; q4 < TBK / 4; ++q4) {
+      double a[2], b[4];
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci) a[ci] = sV[buf][4 * q4 + lk][32 * wc + 16 * ci + lr];
+#pragma unroll
+      for (int ri = 0; ri < 4; ++ri) b[ri] = sS[buf][4 * q4 + lk][64 * wr + 16 * ri + lr];
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+        for (int ri = 0; ri < 4; ++ri)
+          acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 4; ++ri) {
+      const int64_t q = R0 + 64 * wr + 16 * ri + lr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t c = C0 + 32 * wc + 16 * ci + lk + 4 * j;
+        if (q < n && c < k) out[q + c * ldo] = scale * acc[ci][ri][j];
+      }
+    }
+}
+
+static bool trmm_big() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_TRMM_BIG");
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
 hipError_t launch_trmm_lower(const double *A, int64_t ld, int64_t n, const double *V, int64_t ldv,
                              int64_t k, double scale, double *out, int64_t ldo, hipStream_t st) {
   if (n <= 0 || k <= 0) return hipSuccess;
+  if (trmm_big()) {
+    const dim3 grid((unsigned)((k + TT - 1) / TT), (unsigned)((n + TT - 1) / TT));
+    hipLaunchKernelGGL(k_trmm_lower, grid, dim3(512), 0, st, A, ld, n, V, ldv, k, scale, out, ldo);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)((k + SC - 1) / SC), (unsigned)((n + SR - 1) / SR));
   hipLaunchKernelGGL((k_symm<true, true>), grid, dim3(256), 0, st, A, ld, n, 1, 0, V, ldv, k, scale,
                      out, ldo);
