@@ -176,6 +176,8 @@ struct PredOps {
   std::function<void(const double *V, int64_t ldv, int64_t k, double *out)> trmm;
   std::function<void(const double *V, int64_t ldv, int64_t k, double *out, DBuf &tmp)> symv;
   const double *sdiag = nullptr;
+  // optional: dst (n) = A^-1 w without a product (the model's swept AUG rows)
+  std::function<void(double *dst)> ainv_w;
   std::function<void(double *buf, int64_t count)> allreduce;  // empty: single process
   // K_xX rows c0 .. c0 + nc (marginal slice sum for predict_marginal): a
   // device pointer with leading dimension *ld, possibly built in scratch

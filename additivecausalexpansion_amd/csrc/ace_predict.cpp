@@ -121,7 +121,10 @@ void pred_pipeline(const PredOps &op, int64_t nx, bool marginal, const double *Z
   DBuf dsv;
   if (tri) {
     alloc(ctx, dsv, (size_t)n * sizeof(double), "alloc s");
-    op.symv(op.w, n, 1, dsv.d(), dtmp);
+    if (op.ainv_w)
+      op.ainv_w(dsv.d());
+    else
+      op.symv(op.w, n, 1, dsv.d(), dtmp);
   }
   for (int64_t c0 = 0; c0 < nx; c0 += chunk) {
     const int64_t nc = std::min<int64_t>(chunk, nx - c0);
@@ -215,7 +218,7 @@ void predict_impl(ace_model *m, const double *theta, int64_t nx, const double *X
   op.symm = [&](const double *V, int64_t ldv, int64_t k, double *out, DBuf &tmp) {
     symm_resident(m, V, ldv, true, k, out, tmp);
   };
-  DBuf ddiag;
+  DBuf ddiag, dscal;
   if (!m->shard && pred_tri()) {  // -A^-1 is stored: scale -1
     alloc(ctx, ddiag, (size_t)n * sizeof(double), "alloc diag");
     ck(ctx, launch_diag_scaled(m->sw.A.d(), m->naug, n, -1.0, ddiag.d(), st), "diag");
@@ -225,6 +228,14 @@ void predict_impl(ace_model *m, const double *theta, int64_t nx, const double *X
     };
     op.symv = [&](const double *V, int64_t ldv, int64_t k, double *out, DBuf &tmp) {
       symm_resident(m, V, ldv, false, k, out, tmp);
+    };
+    // A^-1 (y - mu) = A^-1 y - mu A^-1 1: the AUG rows the sweep left in A
+    // (k_alpha_from_aug with the caller's mu), no n^2 pass
+    alloc(ctx, dscal, 8 * sizeof(double), "alloc scalars");
+    op.ainv_w = [&](double *dst) {
+      ck(ctx, launch_alpha_from_aug(m->sw.A.d(), m->naug, m->npad, n, mu, 0, dst, dscal.d(), st,
+                                    nullptr),
+         "A^-1 w");
     };
   }
   if (m->shard) op.allreduce = [&](double *b, int64_t c) { shard_allreduce_sum(m->shard, b, c); };
