@@ -71,7 +71,7 @@ struct SweepWork {
         ck(ctx, hipMemcpy(xtiles.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
            "upload cross tiles");
     }
-    const size_t need = (size_t)(4 * (npad / NB) + 4);
+    const size_t need = (size_t)(5 * (npad / NB) + 8);
     while (ev.size() < need) {
       hipEvent_t e;
       ck(ctx, hipEventCreateWithFlags(&e, ACE_SYNC_EVENT_FLAGS), "event");

@@ -567,6 +567,7 @@ constexpr int BK = ACE_BK;  // panel columns staged per LDS buffer
 constexpr int LDL = 144;    // LDS row pitch (doubles): 128 + 16, bank-conflict free
 constexpr int NCH = NB / BK;
 constexpr int UTHREADS = 512;
+constexpr int XSPLIT_HEAD = 8;  // entries of the split cross's head launch (3 tiles + padding)
 static_assert(BK == 16, "staging maps 512 threads x 4 doubles onto a 128 x 16 chunk");
 
 // A tiles are read and written once per sweep step, by whichever XCD runs
@@ -1369,7 +1370,7 @@ static bool pgemm_tiles() {
 #endif
 static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, double *SW,
                         double *const S[2], double *piv, int *flag, int G, int r,
-                        hipStream_t st, bool pivot0 = false) {
+                        hipStream_t st, bool pivot0 = false, hipEvent_t before_gemm = nullptr) {
   const bool split = panel_split();
   double *const SWb[2] = {SW, SW + SUB * SUB};  // ping-pong by sub-step
   for (int s = 0; s < ((ACE_DIAG_SKIP & 1) ? 0 : NB / SUB); ++s) {
@@ -1384,6 +1385,9 @@ static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, dou
                          S[s & 1], S[(s + 1) & 1], k0);
   }
   if (ACE_DIAG_SKIP & 2) return;
+  // (split cross: the panel rows outside the pivot block come from a launch
+  // on the second side stream)
+  if (before_gemm) (void)hipStreamWaitEvent(st, before_gemm, 0);
   if (pgemm_tiles())
     hipLaunchKernelGGL(k_panel_gemm_t, dim3((unsigned)(ld / UT), NB / UT), dim3(UTHREADS), 0, st,
                        W, Pn, ld, k0, G, r);
@@ -1419,7 +1423,7 @@ static bool xgather() {
 
 // gathered: P, W and S[0] of this panel were written by the cross launch
 static hipError_t panel_sweep(const SweepBufs &b, int buf, int64_t k0, hipStream_t st,
-                              bool gathered = false) {
+                              bool gathered = false, hipEvent_t before_gemm = nullptr) {
   const int64_t naug = b.ld;
   // with the split panel, k_gather's D_0 workgroup sweeps sub-block 0 too
   const bool gp = !gathered && panel_split() && gather_pivot();
@@ -1433,7 +1437,7 @@ static hipError_t panel_sweep(const SweepBufs &b, int buf, int64_t k0, hipStream
                        b.A, b.ld, k0, b.P[buf], b.W[buf], b.ld, b.S[0], nullptr, nullptr, nullptr);
   // sweep the NB x NB pivot block in place, then every other panel row:
   // W_i = Pn_i W_kk
-  panel_chain(b.P[buf], b.W[buf], b.ld, k0, b.SW, b.S, b.piv, b.flag, 1, 0, st, gp);
+  panel_chain(b.P[buf], b.W[buf], b.ld, k0, b.SW, b.S, b.piv, b.flag, 1, 0, st, gp, before_gemm);
   return hipGetLastError();
 }
 
@@ -1591,6 +1595,18 @@ static bool side2_on() {
   return v != 0;
 }
 
+// ACE_XSPLIT=1: the pair cross of block 2g+2 runs as two launches -- the
+// pivot block's 3 tiles on the panel stream (its chain starts right after
+// them), the rest on the second side stream, which the panel GEMM waits for
+bool xsplit_cross() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_XSPLIT");
+    v = e ? (atoi(e) != 0) : 0;
+  }
+  return v != 0;
+}
+
 std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t> &off) {
   const int64_t nT = naug / UT;
   constexpr int KT = NB / UT;
@@ -1607,8 +1623,21 @@ std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t>
         if (in_blk(I, b0) || in_blk(J, b0)) ta.push_back(Tile{(int)I, (int)J});
         else if (b1 < steps && (in_blk(I, b1) || in_blk(J, b1))) tb.push_back(Tile{(int)I, (int)J});
       }
+    if (xsplit_cross()) {
+      // the pivot block's own tiles (I and J in block b0) lead block b0's
+      // list, padded to XSPLIT_HEAD entries: the split schedule launches
+      // them alone so the pivot chain can start before the rest is done
+      std::vector<Tile> head, rest;
+      for (const Tile &t : ta) (in_blk(t.I, b0) && in_blk(t.J, b0) ? head : rest).push_back(t);
+      head.resize(XSPLIT_HEAD, Tile{-1, -1});
+      const std::vector<Tile> o = S > 0 ? xcd_update_order(rest, S) : rest;
+      head.insert(head.end(), o.begin(), o.end());
+      ta.swap(head);
+    }
+    bool first = true;
     for (auto *t : {&ta, &tb}) {
-      const std::vector<Tile> o = S > 0 ? xcd_update_order(*t, S) : *t;
+      const std::vector<Tile> o = (S > 0 && !(first && xsplit_cross())) ? xcd_update_order(*t, S) : *t;
+      first = false;
       all.insert(all.end(), o.begin(), o.end());
       off.push_back((int64_t)all.size());
     }
@@ -1709,9 +1738,13 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
   auto gout = [&](int k) {
     return xg ? GatherOut{b.P[slot(k)], b.W[slot(k)], b.S[0], (int64_t)k * NB, b.ld} : no_gather();
   };
+  // split cross (xsplit_cross): E3(g) = the rest of block 2g's cross done
+  const bool xs = two2 && xsplit_cross() && sy->nev >= 5 * steps + 5;
+  auto E3 = [&](int g) { return sy->ev[4 * steps + 4 + g]; };
   auto produce = [&](int g, bool wait2) -> hipError_t {
     const int k = 2 * g;
-    hipError_t r = panel_sweep(b, slot(k), (int64_t)k * NB, side, xg && g > 0);
+    hipError_t r = panel_sweep(b, slot(k), (int64_t)k * NB, side, xg && g > 0,
+                               xs && g > 0 ? E3(g) : nullptr);
     // (g = 0: the caller may have signalled "inputs ready" after assembling
     // only the first two panels' columns (model_pipeline) -- every tile the
     // cross of block 1 reads or writes, disjoint from the rest of the
@@ -1765,11 +1798,24 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
         // panel's chain waits for it), block 2g+3 on side2 meanwhile
         const int64_t pa = b.poff[2 * (g + 1)], na = (ACE_DIAG_SKIP & 4) ? 0 : b.poff[2 * (g + 1) + 1] - pa;
         const int64_t pb = b.poff[2 * (g + 1) + 1], nb = (ACE_DIAG_SKIP & 4) ? 0 : b.poff[2 * (g + 1) + 2] - pb;
-        if (na > 0) hipLaunchKernelGGL(k_update_pair, dim3((unsigned)na), dim3(UTHREADS), 0, side, b.A, b.ld,
+        const int64_t nah = xs ? std::min<int64_t>(na, XSPLIT_HEAD) : na;  // head on `side`
+        if (xs) {  // side2 starts with `side` (bulk g-1 done), not after the head
+          if ((e = hipEventRecord(E1(g + 1), side)) != hipSuccess) return e;
+          if ((e = hipStreamWaitEvent(side2, E1(g + 1), 0)) != hipSuccess) return e;
+        }
+        if (nah > 0) hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nah), dim3(UTHREADS), 0, side, b.A, b.ld,
                            b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0,
                            -1, -1, b.ptiles + pa, gout(k + 2), -1, nullptr);
+        if (xs) {  // the rest of block 2g+2's cross on side2; its panel GEMM waits for E3
+          if (na > nah)
+            hipLaunchKernelGGL(k_update_pair, dim3((unsigned)(na - nah)), dim3(UTHREADS), 0, side2,
+                               b.A, b.ld, b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)],
+                               b.P[slot(k + 1)], b.ld, ka0, -1, -1, b.ptiles + pa + nah, gout(k + 2),
+                               -1, nullptr);
+          if ((e = hipEventRecord(E3(g + 1), side2)) != hipSuccess) return e;
+        }
         if (nb > 0) {
-          if (two2) {
+          if (two2 && !xs) {
             if ((e = hipEventRecord(E1(g + 1), side)) != hipSuccess) return e;
             if ((e = hipStreamWaitEvent(side2, E1(g + 1), 0)) != hipSuccess) return e;
           }

@@ -507,7 +507,8 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
                 "single_pgemm_rows": {"ACE_PAIR": "0", "ACE_PGEMM_TILES": "0"},
                 "merged": {"ACE_PAIR": "1", "ACE_XMERGE": "1"},
                 "merged_gather": {"ACE_PAIR": "1", "ACE_XMERGE": "1", "ACE_XGATHER": "0"},
-                "unmerged": {"ACE_PAIR": "1", "ACE_XMERGE": "0"}}
+                "unmerged": {"ACE_PAIR": "1", "ACE_XMERGE": "0"},
+                "xsplit": {"ACE_PAIR": "1", "ACE_XSPLIT": "1"}}
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)
@@ -587,11 +588,12 @@ def test_merged_cross_model_is_bitwise_neutral(tmp_path, n):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
-    for v in ("0", "1"):
+    for v in ("0", "1", "split"):
         out = str(tmp_path / f"m{v}.npy")
-        env = dict(os.environ, ACE_XMERGE=v)
+        env = dict(os.environ, ACE_XMERGE=v) if v != "split" else dict(os.environ, ACE_XSPLIT="1")
         subprocess.run([sys.executable, "-c", _MODEL_SNIPPET.format(root=root, n=n, out=out)],
                        env=env, check=True, timeout=100)
         outs[v] = np.load(out)
     assert np.all(np.isfinite(outs["1"]))
     assert np.array_equal(outs["0"], outs["1"])
+    assert np.array_equal(outs["0"], outs["split"])  # the split cross (ACE_XSPLIT=1)
