@@ -263,7 +263,11 @@ int ace_model_apply_inverse(ace_model *m, int64_t k, const double *V, double *ou
  * parameters), inverse = the resident one of the last para_update (Q6: the
  * R6 invKmatn).  X2 nx x p, Z2 nx x (B-1) column-major (the test basis).
  * map (nx), ci (nx x 2), var (nx) as pred_cpp's list.  K_xX is assembled
- * on the device, only diag(K_xx) is formed; nothing n x n crosses PCIe. */
+ * on the device, only diag(K_xx) is formed; nothing n x n crosses PCIe.
+ * Single GPU: diag(K_xX A^-1 K_xX^T) through the strictly lower triangle of
+ * A^-1 (half the flops of the full product) and K_xX A^-1 (y - mu) from the
+ * sweep's augmented rows; results equal the full-product form up to
+ * rounding (ACE_PRED_TRI=0 selects it). */
 int ace_model_predict(ace_model *m, const double *theta, int64_t nx, const double *X2,
                       const double *Z2, double mean_y, double std_y, double *map, double *ci,
                       double *var);
