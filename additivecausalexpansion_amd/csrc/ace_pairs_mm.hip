@@ -586,6 +586,11 @@ __device__ __forceinline__ double rcp_nr_mm(double f) {
 #ifndef ACE_GRAD_DPP
 #define ACE_GRAD_DPP 1
 #endif
+// wave priority experiment: 1 = raised around the GEMMs, 2 = around the
+// per-pair VALU section, 0 = none
+#ifndef ACE_GRAD_PRIO
+#define ACE_GRAD_PRIO 1
+#endif
 template <int CTRL>
 __device__ __forceinline__ double dpp64(double v) {
   const unsigned long long u = __double_as_longlong(v);
@@ -789,7 +794,10 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
       zr = S.Z[r * ZS + b - 1];
       if (KIND == 0) lzr = S.LZ[r * ZS + b - 1];
     }
+    if (ACE_GRAD_PRIO == 1) __builtin_amdgcn_s_setprio(2);
     gemm1_mm<XP, CB>(L.XJ, xr, L.W + b * PM, lr, lk, acc, cbase);
+    if (ACE_GRAD_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    if (ACE_GRAD_PRIO == 2) __builtin_amdgcn_s_setprio(2);
     const double sr = L.Nr[b * 64 + rl];
     const double *nc = L.Nc + b * 64 + cbase;
     const double *zcol = L.Z + (b - 1) * 64 + cbase;
@@ -855,6 +863,8 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
 #pragma unroll
       for (int v = 0; v < 4; ++v) Rv[v] = __shfl(rs, lk + 4 * v, 64);  // row 16 wr + lk + 4v
     }
+    if (ACE_GRAD_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+    if (ACE_GRAD_PRIO == 1) __builtin_amdgcn_s_setprio(2);
     // GEMM2: V = U X_J, QG column blocks per pass of the k-loop
 #pragma unroll
     for (int q0 = 0; q0 < ((ACE_DIAG_GRAD & 32) ? 0 : NQ); q0 += QG) {
@@ -893,6 +903,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
         if (lk == 0 && nn < PM) red[w * RS + nn] = part;
       }
     }
+    if (ACE_GRAD_PRIO == 1) __builtin_amdgcn_s_setprio(0);
     // C_c: column sums of U over the wave's 16 rows, reduce-scatter over lr
     {
       // (after GEMM2: U's registers are free again)
