@@ -509,8 +509,10 @@ void model_collect_timing(ace_model *m, int ts) {
 
 // Host syncs of the device-fused training loop: every ACE_TRAIN_SYNC
 // iterations (default 4).  Iterations enqueued after the one that converged
-// still run but change nothing (k_train_step checks the stop flag), so a fit
-// spends at most ACE_TRAIN_SYNC - 1 extra evaluations.
+// still run but change nothing in theta or the stats (k_train_step checks the
+// stop flag); their evaluations do overwrite the resident inverse, so the
+// stopping iteration's evaluation is re-run once at its saved theta.  A fit
+// spends at most ACE_TRAIN_SYNC extra evaluations.
 int train_sync_every() {
   static int v = -1;
   if (v < 0) {
@@ -535,7 +537,7 @@ int train_device(ace_model *m, int optimizer, double learn_rate, double momentum
   const int P = 2 + s.B * (s.p + 1);
   hipStream_t st = ctx->stream;
   DBuf dst, dhist, dctl;
-  std::vector<double> init((size_t)(4 * P), 0.0);
+  std::vector<double> init((size_t)(5 * P), 0.0);
   std::copy(theta, theta + P, init.begin());
   upload(ctx, dst, init.data(), init.size(), "upload train state");
   std::vector<double> hz((size_t)(2 * (maxiter + 2)), 0.0);
@@ -561,6 +563,7 @@ int train_device(ace_model *m, int optimizer, double learn_rate, double momentum
   const int K = train_sync_every();
   int ctl[4] = {0, 0, 0, 0};
   bool interrupted = false;
+  int queued = 0;  // last iteration enqueued
   for (int it = 1; it <= maxiter; ++it) {
     if (ctx->poll && ctx->poll(ctx->poll_user)) {  // before iteration it, like para_update
       interrupted = true;
@@ -570,6 +573,7 @@ int train_device(ace_model *m, int optimizer, double learn_rate, double momentum
     ck(ctx, launch_train_step(c, it, m->gsum.d(), m->sums.d(), m->scal.d(), m->sw.flag.i(), dst.d(),
                               dhist.d(), dctl.i(), st),
        "train step");
+    queued = it;
     if (it % K == 0 || it == maxiter) {
       ck(ctx, hipMemcpyAsync(ctl, dctl.p, sizeof(ctl), hipMemcpyDeviceToHost, st), "download control");
       sync(ctx);
@@ -577,6 +581,15 @@ int train_device(ace_model *m, int optimizer, double learn_rate, double momentum
     }
   }
   ck(ctx, hipMemcpyAsync(ctl, dctl.p, sizeof(ctl), hipMemcpyDeviceToHost, st), "download control");
+  sync(ctx);
+  if (ctl[0] >= 1 && queued > ctl[0]) {
+    // iterations queued after the stopping one ran their evaluation at the
+    // final theta into m->sw; the reference's invKmatn is the one of the last
+    // para_update (Q6, R/main_ace.R:215-227, R/kernel_SE_R6.R:37): re-run
+    // iteration ctl[0]'s evaluation at the theta it saw (deterministic, so
+    // bit-identical to what that iteration left)
+    model_pipeline(m, m->sw, nullptr, ctl[0] == 1 ? 1 : 0, false, dst.d() + 4 * P);
+  }
   download(ctx, theta, dst.d(), (size_t)P, "download theta");
   download(ctx, stats, dhist.d(), (size_t)(2 * (maxiter + 2)), "download stats");
   sync(ctx);

@@ -284,10 +284,11 @@ struct TrainCfg {
 };
 // One iteration's host-side tail of ace_model_train on the device (one
 // workgroup): compose_grad + stats of para_update, norm clip, optimizer step,
-// the mu overwrite and the convergence test.  st = [theta | m1 | m2 | g]
-// (4 P), hist = the stats matrix (2 x (maxiter + 2)), ctl = {last iteration
-// done, stop: 0 running / 1 converged / 2 non-finite gradient}.  Once ctl[1]
-// is set, later launches change nothing.
+// the mu overwrite and the convergence test.  st = [theta | m1 | m2 | g |
+// prev] (5 P; prev = the theta the iteration's evaluation ran at), hist = the
+// stats matrix (2 x (maxiter + 2)), ctl = {last iteration done, stop: 0
+// running / 1 converged / 2 non-finite gradient}.  Once ctl[1] is set, later
+// launches change nothing.
 hipError_t launch_train_step(const TrainCfg &c, int it, const double *gsum, const double *sums,
                              const double *scal, const int *flag, double *st, double *hist,
                              int *ctl, hipStream_t stream);

@@ -74,7 +74,12 @@ __global__ __launch_bounds__(1024) void k_train_step(TrainCfg c, int it,
   __shared__ double sh[16];
   if (ctl[1] != 0) return;  // stopped at an earlier iteration: this one is discarded
   const int P = c.P, B = c.B, PM = c.PM, tid = threadIdx.x;
-  double *th = st, *m1 = st + P, *m2 = st + 2 * P, *g = st + 3 * P;
+  double *th = st, *m1 = st + P, *m2 = st + 2 * P, *g = st + 3 * P, *prev = st + 4 * P;
+  // the theta this iteration's evaluation ran at: the host re-runs it into
+  // the resident inverse when later, discarded iterations overwrote it
+  // (Q6: predict uses invKmatn of the last para_update, R/kernel_SE_R6.R:37)
+  for (int j = tid; j < P; j += 1024) prev[j] = th[j];
+  __syncthreads();
   const double kNaN = __builtin_nan("");
   const double mu = scal[3];
   const bool bad = *flag != 0;  // not positive definite: non-finite outputs

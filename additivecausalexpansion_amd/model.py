@@ -264,7 +264,7 @@ class _KernelClass:
         return model
 
     def para_update(self, iter, y, X, Z, Optim, printevery=100, verbose=True):  # noqa: A002
-        """R/kernel_SE_R6.R:40-62 (R/kernel_Matern32_R6.R:142-163)."""
+        """R/kernel_SE_R6.R:40-62 (R/kernel_Matern32_R6.R:39-60)."""
         model = self._ensure_model(y, X, Z)
         self._mark_kernel(X, Z)
         gradients, stats, mu_post = model.para_update(iter, self.parameters)

@@ -230,7 +230,7 @@ int ace_normalize_test(int64_t n, int px, int pz, double *X, double *Z,
  * keeps X, Z, y, the swept matrix and the training inverse resident in HBM
  * and never materialises the cube: one ace_model_para_update() is the
  * native work of one para_update (R/kernel_SE_R6.R:40-62,
- * R/kernel_Matern32_R6.R:142-163) -- kernel assembly, factorisation +
+ * R/kernel_Matern32_R6.R:39-60) -- kernel assembly, factorisation +
  * inverse + log-determinant, and every gradient and statistic.
  */
 int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B,

@@ -320,15 +320,20 @@ def pred_marginal_cpp(y_X, Z_x, sigma, mu, invK_XX, K_xX, K_xx, mean_y, std_y, s
     if not calculate_ate:
         return out
     zx = np.ravel(Z_x).astype(np.float64)
-    ate = float(np.mean(y_x))
-    ate_sd = std_y * math.sqrt(float(np.sum(Km_xx))) / nx
-    ntx = int(np.sum(zx))  # unsigned int in the reference (src/pred_cpp.cpp:95)
-    att = float(np.dot(y_x, zx)) / ntx
-    att_sd = std_y * math.sqrt(float(np.dot(Km_xx @ zx, zx))) / ntx
-    nux = nx - ntx
-    atu = (ate * nx - att * ntx) / nux
-    u = (zx == 0).astype(np.float64)
-    atu_sd = std_y * math.sqrt(float(np.dot(Km_xx @ u, u))) / nux
+    # C double semantics: sqrt of a negative quadratic form is NaN and a
+    # division by a zero count is +-inf / NaN (no exception), as in the
+    # reference's doubles; the counts are `unsigned int` (src/pred_cpp.cpp:43,95,104)
+    f64 = np.float64
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ate = float(np.mean(y_x))
+        ate_sd = float(std_y * np.sqrt(f64(np.sum(Km_xx))) / f64(nx))
+        ntx = int(np.sum(zx)) % 2 ** 32  # truncation toward zero, like the C conversion
+        att = float(f64(np.dot(y_x, zx)) / f64(ntx))
+        att_sd = float(std_y * np.sqrt(f64(np.dot(Km_xx @ zx, zx))) / f64(ntx))
+        nux = (nx - ntx) % 2 ** 32  # unsigned subtraction (src/pred_cpp.cpp:104)
+        atu = float((f64(ate) * f64(nx) - f64(att) * f64(ntx)) / f64(nux))
+        u = (zx == 0).astype(np.float64)
+        atu_sd = float(std_y * np.sqrt(f64(np.dot(Km_xx @ u, u))) / f64(nux))
     for key, m, sd in (("ate", ate, ate_sd), ("att", att, att_sd), ("atu", atu, atu_sd)):
         out[key] = {"map": m, "ci": np.array([m - 1.96 * sd, m + 1.96 * sd]), "var": sd ** 2}
     return out
@@ -482,7 +487,7 @@ def ncs_basis_deriv(x, knots):
 
 
 # --------------------------------------------------------------------------
-# One para_update (R/kernel_SE_R6.R:40-62, R/kernel_Matern32_R6.R:142-163)
+# One para_update (R/kernel_SE_R6.R:40-62, R/kernel_Matern32_R6.R:39-60)
 # and the training loop (R/main_ace.R:213-235), Nadam/Adam/Nesterov classes
 # (R/optimizer_classes.R).
 # --------------------------------------------------------------------------

@@ -185,3 +185,29 @@ def test_sweep_model_inverts_and_logdets():
         assert np.allclose(r["u"], ref["inv"] @ y, rtol=1e-9, atol=1e-10 * scale)
         assert r["oK1"] == pytest.approx(ref["inv"].sum(), rel=1e-10)
         assert r["yK1"] == pytest.approx(np.sum(ref["inv"] @ y), rel=1e-9, abs=1e-9 * scale)
+
+
+@pytest.mark.parametrize("zx_val", [0.0, 1.0])
+def test_pred_marginal_empty_group_is_c_semantics(zx_val):
+    """src/pred_cpp.cpp:95-110 divides doubles by `unsigned int` counts: with
+    no treated (ntx = 0) or no untreated (nux = 0) test point the reference
+    returns NaN / inf, it does not fail.  The oracle must do the same."""
+    rng = np.random.default_rng(4)
+    n, nx, B = 12, 7, 3
+    X = rng.uniform(-1, 1, (n, 2))
+    Z = rng.normal(size=(n, B - 1))
+    X2 = rng.uniform(-1, 1, (nx, 2))
+    Z2 = rng.normal(size=(nx, B - 1))
+    th = np.concatenate([[math.log(0.1), 0.2], np.zeros(B), np.full(2 * B, math.log(2.0))])
+    inv = O.invkernel_cpp(O.kernmat_SE_symmetric_cpp(X, Z, th)["full"], th[0])["inv"]
+    out = O.pred_marginal_cpp(rng.normal(size=n), np.full(nx, zx_val), th[0], th[1], inv,
+                              O.kernmat_SE_cpp(X2, X, Z2, Z, th)["elements"],
+                              O.kernmat_SE_symmetric_cpp(X2, Z2, th)["elements"], 0.0, 1.3, 0.7,
+                              True)
+    assert np.isfinite(out["ate"]["map"])
+    if zx_val == 0.0:  # ntx = 0: 0/0
+        assert np.isnan(out["att"]["map"]) and np.isnan(out["att"]["var"])
+        assert np.isnan(out["atu"]["map"])  # (ate nx - NaN * 0) / nx
+    else:  # nux = 0
+        assert np.isfinite(out["att"]["map"])
+        assert not np.isfinite(out["atu"]["map"]) and np.isnan(out["atu"]["var"])

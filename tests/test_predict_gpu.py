@@ -101,6 +101,51 @@ def test_device_predict_marginal_ate_matches_oracle(A, O, kernel, B):
     assert "ate" not in plain and np.array_equal(plain["map"], got["map"])
 
 
+def _check_avg_edge(got, ref, case):
+    """ATE/ATT/ATU with a zero treated (ntx = 0) or untreated (nux = 0) count:
+    the reference divides doubles by the unsigned count, so its outputs are
+    the C results (src/pred_cpp.cpp:95-110): 0/0 = NaN for the empty group's
+    sd, NaN for ATT's map when ntx = 0 (and so for ATU's, via NaN * 0), and a
+    non-finite ATU map when nux = 0 (0/0 or +-tiny/0, by summation rounding)."""
+    close(got["ate"]["map"], ref["ate"]["map"])
+    close(got["ate"]["var"], ref["ate"]["var"], 1e-6, 1e-10)
+    if case == "none_treated":
+        for k in ("map", "var"):
+            assert np.isnan(got["att"][k]) and np.isnan(ref["att"][k])
+        assert np.all(np.isnan(got["att"]["ci"])) and np.all(np.isnan(ref["att"]["ci"]))
+        assert np.isnan(got["atu"]["map"]) and np.isnan(ref["atu"]["map"])
+        close(got["atu"]["var"], ref["atu"]["var"], 1e-6, 1e-10)
+    else:
+        close(got["att"]["map"], ref["att"]["map"])
+        close(got["att"]["var"], ref["att"]["var"], 1e-6, 1e-10)
+        assert not np.isfinite(got["atu"]["map"]) and not np.isfinite(ref["atu"]["map"])
+        assert np.isnan(got["atu"]["var"]) and np.isnan(ref["atu"]["var"])
+        assert np.all(~np.isfinite(got["atu"]["ci"])) and np.all(~np.isfinite(ref["atu"]["ci"]))
+
+
+@pytest.mark.parametrize("case", ["none_treated", "all_treated"])
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+def test_predict_marginal_empty_group_semantics(A, O, kernel, case):
+    """Z_x all 0 (ntx = 0) or all 1 (nux = 0): the device-resident
+    predict_marginal and the pred_marginal_cpp ABI reproduce the reference's
+    inf / NaN outputs instead of raising."""
+    n, p, B, nx = 300, 3, 4, 64
+    m, y, X, Z, th, sy, inv = _fit_state(O, kernel, n, p, B, seed=31, A=A, mix=False)
+    X2, Z2 = _test_points(p, B, nx, seed=32)
+    dZ2 = np.asfortranarray(Z2 * 0.5 + 0.2)
+    zx = np.zeros(nx) if case == "none_treated" else np.ones(nx)
+    sym, cross = O.KERNELS[kernel][0], O.KERNELS[kernel][1]
+    Km_xX = cross(X2, X, dZ2, Z, th)["elements"]
+    Km_xx = sym(X2, dZ2, th)["elements"]
+    ref = O.pred_marginal_cpp(y, zx, th[0], th[1], inv, Km_xX, Km_xx, 0.3, 1.7, 0.8, True)
+    got = m.predict_marginal(th, X2, dZ2, zx, 1.7, 0.8, True)
+    close(got["map"], ref["map"])
+    _check_avg_edge(got, ref, case)
+    abi = A.pred_marginal_cpp(y, zx, th[0], th[1], inv, Km_xX, Km_xx, 0.3, 1.7, 0.8, True)
+    close(abi["map"], ref["map"])
+    _check_avg_edge(abi, ref, case)
+
+
 def test_device_predict_chunks_and_padding(A, O):
     """nx above one 8192-point chunk plus a ragged tail, n not a multiple of
     the 128-row product tile."""
