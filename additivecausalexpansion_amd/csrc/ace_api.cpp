@@ -409,6 +409,56 @@ int ace_pred_marginal(ace_ctx *ctx, int64_t nX, int64_t nx, int B, const double 
 
 }  // extern "C"
 
+// A = Kfull + sig I (lower 64-tiles, assembly mode 0) into w.A with the AUG
+// rows [y; 1] (y null: the 1 row only), then the sweep.  The first two
+// panels' columns are assembled first: the sweep's first pivot chains and the
+// cross of block 1 (side stream) then run under the rest of the assembly.
+// ev_asm (optional): two timing events around the assembly.
+void assemble_and_sweep(ace_ctx *ctx, SweepWork &w, const Shape &s, const PairSide &ps,
+                        const TabView &tv, double sig, const double *y, int64_t n,
+                        const SweepTiming *tmg, hipEvent_t *ev_asm) {
+  hipStream_t st = ctx->stream;
+  ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, n, y, st), "aug init");
+  ck(ctx, hipMemsetAsync(w.flag.p, 0, sizeof(int), st), "memset flag");
+  SweepSync sy = w.sync(ctx);
+  if (ev_asm) ck(ctx, hipEventRecord(ev_asm[0], st), "event");
+  ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
+                          nullptr, st, nullptr, 0, 1, 1),
+     "assembly (first panel)");
+  const int steps = (int)(w.npad / NB);
+  if (sy.side && sy.nev >= 2 * steps + 1) {  // run_sweep's "inputs ready" event
+    ck(ctx, hipEventRecord(sy.ev[2 * steps], st), "event");
+    sy.ready_recorded = true;
+  }
+  ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
+                          nullptr, st, nullptr, 0, 1, 2),
+     "assembly");
+  if (ev_asm) ck(ctx, hipEventRecord(ev_asm[1], st), "event");
+  ck(ctx, run_sweep(w.bufs(), st, &sy, tmg), "sweep");
+}
+
+// The gradient's tile list for n: diagonal 64-tiles first, then the strictly
+// lower ones dealt to the XCDs in S x S super-blocks (a launch's block b runs
+// on XCD b % 8).  *ndiag = -1 (and no list) for the row-major grid.
+void build_grad_tiles(ace_ctx *ctx, int64_t n, DBuf &tiles, int64_t *ntiles, int64_t *ndiag) {
+  *ntiles = grad_ntiles(n);
+  *ndiag = -1;
+  const int S = grad_order_block();
+  if (S <= 0) return;
+  const int64_t ntr = (n + AT - 1) / AT;
+  std::vector<Tile> lst, low;
+  for (int64_t I = 0; I < ntr; ++I) lst.push_back(Tile{(int)I, (int)I});
+  for (int64_t I = 1; I < ntr; ++I)
+    for (int64_t J = 0; J < I; ++J) low.push_back(Tile{(int)I, (int)J});
+  const std::vector<Tile> o = xcd_update_order(low, S);
+  lst.insert(lst.end(), o.begin(), o.end());
+  alloc(ctx, tiles, lst.size() * sizeof(Tile), "alloc grad tiles");
+  ck(ctx, hipMemcpy(tiles.p, lst.data(), lst.size() * sizeof(Tile), hipMemcpyHostToDevice),
+     "upload grad tiles");
+  *ntiles = (int64_t)lst.size();
+  *ndiag = ntr;
+}
+
 namespace {
 
 // One evaluation on the stream.  theta_dev != nullptr: theta is a device
@@ -435,33 +485,15 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
     sig = std::exp(theta[0]);
   }
   const PairSide ps = m->side.view(m->n);
-  ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, m->n, m->y.d(), st), "aug init");
-  ck(ctx, hipMemsetAsync(w.flag.p, 0, sizeof(int), st), "memset flag");
-  SweepSync sy = w.sync(ctx);
-  // the first two panels' columns first: the sweep's first pivot chains
-  // and the cross of block 1 (side stream) then run under the rest of the
-  // assembly
   const int ts = m->tset;
-  if (timed) ck(ctx, hipEventRecord(m->ev_asm[2 * ts], st), "event");
-  ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
-                          nullptr, st, nullptr, 0, 1, 1),
-     "assembly (first panel)");
-  const int steps = (int)(w.npad / NB);
-  if (sy.side && sy.nev >= 2 * steps + 1) {  // run_sweep's "inputs ready" event
-    ck(ctx, hipEventRecord(sy.ev[2 * steps], st), "event");
-    sy.ready_recorded = true;
-  }
-  ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
-                          nullptr, st, nullptr, 0, 1, 2),
-     "assembly");
-  if (timed) ck(ctx, hipEventRecord(m->ev_asm[2 * ts + 1], st), "event");
   SweepTiming tmg;
   const size_t nset = m->ev_upd.size() / 2;
   tmg.ev = m->ev_upd.data() + ts * nset;
   tmg.nev = (int)nset;
   tmg.used = &m->upd_used[ts];
   tmg.flops = m->upd_flops.data() + ts * (nset / 2);
-  ck(ctx, run_sweep(w.bufs(), st, &sy, timed ? &tmg : nullptr), "sweep");
+  assemble_and_sweep(ctx, w, s, ps, tv, sig, m->y.d(), m->n, timed ? &tmg : nullptr,
+                     timed ? m->ev_asm + 2 * ts : nullptr);
   ck(ctx, launch_alpha_from_aug(w.A.d(), w.naug, w.npad, m->n, theta_dev ? 0.0 : theta[1], use_mu,
                                 m->alpha.d(), m->scal.d(), st, theta_dev ? theta_dev + 1 : nullptr),
      "alpha");
@@ -635,21 +667,7 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
     m->naug = m->sw.naug;
     m->ntiles = grad_ntiles(n);
     m->ntr = (n + AT - 1) / AT;
-    if (const int S = grad_order_block(); S > 0) {
-      // diagonal 64-tiles first, then the strictly lower ones dealt to the
-      // XCDs in S x S super-blocks (a launch's block b runs on XCD b % 8)
-      std::vector<Tile> lst, low;
-      for (int64_t I = 0; I < m->ntr; ++I) lst.push_back(Tile{(int)I, (int)I});
-      for (int64_t I = 1; I < m->ntr; ++I)
-        for (int64_t J = 0; J < I; ++J) low.push_back(Tile{(int)I, (int)J});
-      const std::vector<Tile> o = xcd_update_order(low, S);
-      lst.insert(lst.end(), o.begin(), o.end());
-      alloc(ctx, m->gtiles, lst.size() * sizeof(Tile), "alloc grad tiles");
-      ck(ctx, hipMemcpy(m->gtiles.p, lst.data(), lst.size() * sizeof(Tile), hipMemcpyHostToDevice),
-         "upload grad tiles");
-      m->ntiles = (int64_t)lst.size();
-      m->ngdiag = m->ntr;
-    }
+    build_grad_tiles(ctx, n, m->gtiles, &m->ntiles, &m->ngdiag);
     const Shape &s = m->s;
     alloc(ctx, m->y, (size_t)m->npad * sizeof(double), "alloc y");
     alloc(ctx, m->tab, (size_t)(2 * s.B * s.PM + s.B + 1) * sizeof(double), "alloc tab");

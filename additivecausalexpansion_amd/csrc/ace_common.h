@@ -8,11 +8,14 @@
 #include <cstdio>
 #include <cstring>
 #include <limits>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "../../include/ace_hip.h"
 #include "ace_internal.h"
+
+struct SweepWork;  // ace_model.h
 
 struct ace_ctx {
   int device = 0;
@@ -22,6 +25,10 @@ struct ace_ctx {
   int (*poll)(void *) = nullptr; // optional interrupt poll (ace_set_interrupt_poll)
   void *poll_user = nullptr;
   std::string err;
+  // sweep buffers of freed inverse handles (ace_dmat.cpp), reused by the
+  // next invkernel_dev of the same n instead of a new 2 n^2-byte allocation
+  std::vector<std::shared_ptr<SweepWork>> sweep_pool;
+  std::shared_ptr<void> dmat_state;  // the handle path's cached inputs (ace_dmat.cpp)
 };
 
 extern std::string g_create_err;

@@ -241,8 +241,12 @@ hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t s
 hipError_t shard_update_main(const ShardSweep &b, int k, int buf, int kx, hipStream_t st);
 
 // ---- small helpers -----------------------------------------------------------
+// AUG rows of columns j < n: row 0 = y (zeros if y is null), row 1 = 1
 hipError_t launch_aug_init(double *A, int64_t ld, int64_t npad, int64_t n,
                            const double *y, hipStream_t st, int G = 1, int rank = 0);
+// out[0] = sum_j y_j (A^-1 1)_j (AUG row 1), out[1] = 1^T A^-1 1 (corner)
+hipError_t launch_aug_dot(const double *A, int64_t ld, int64_t npad, int64_t n, const double *y,
+                          double *out, hipStream_t st);
 // sharded: vec = [u | v | yKy, yK1, 1K1] of the rank's own columns (zeros elsewhere)
 hipError_t launch_aug_extract(const double *A, int64_t ld, int64_t npad, int G,
                               int rank, double *vec, hipStream_t st);

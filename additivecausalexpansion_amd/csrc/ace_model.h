@@ -10,6 +10,9 @@
 struct SweepWork {
   DBuf A, P0, P1, W0, W1, P2, P3, W2, W3, SW, S0, S1, piv, flag, order, xtiles, ptiles, gorder,
       morder, mcnt;
+  DBuf gtiles;                          // handle path: the gradient's tile list (build_grad_tiles)
+  DBuf gpart, gwork, gsum;              // handle path: gradient partial-sum scratch
+  int64_t ngtiles = 0, ngdiag = -2;     // -2: not built yet
   std::vector<int64_t> xoff, poff, moff;
   std::vector<int> mfront, mtarget;
   int64_t glen = 0;
@@ -161,6 +164,14 @@ struct ace_model {
   ShardModel *shard = nullptr;  // block-column-sharded model (ace_shard.cpp)
 };
 
+
+// A = Kfull + sig I into w.A (AUG rows [y; 1], y may be null), then the
+// sweep (ace_api.cpp; the fused model's and the handle path's common front)
+void assemble_and_sweep(ace_ctx *ctx, SweepWork &w, const Shape &s, const PairSide &ps,
+                        const TabView &tv, double sig, const double *y, int64_t n,
+                        const SweepTiming *tmg, hipEvent_t *ev_asm);
+// the gradient's XCD-dealt tile list for n (ace_api.cpp)
+void build_grad_tiles(ace_ctx *ctx, int64_t n, DBuf &tiles, int64_t *ntiles, int64_t *ndiag);
 
 // Operands of the device prediction pipeline (pred_pipeline, ace_predict.cpp).
 struct PredOps {

@@ -48,7 +48,7 @@ __global__ void k_aug_init(double *__restrict__ A, int64_t ld, int64_t npad, int
   const int t = threadIdx.x;     // AUG rows
   double v = 0.0;
   if (j < n) {
-    if (t == 0) v = y[j];
+    if (t == 0) v = y ? y[j] : 0.0;  // y == null: the 1 row only
     else if (t == 1) v = 1.0;
   }
   A[(npad + t) + lcol(j, G) * ld] = v;
@@ -86,6 +86,29 @@ hipError_t launch_aug_extract(const double *A, int64_t ld, int64_t npad, int G, 
                               double *vec, hipStream_t st) {
   hipLaunchKernelGGL(k_aug_extract, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, st, A,
                      ld, npad, G, rank, vec);
+  return hipGetLastError();
+}
+
+// out[0] = sum_j y_j (A^-1 1)_j and out[1] = 1^T A^-1 1 from the swept AUG
+// row 1 and corner (one workgroup, fixed order): mu_solution_cpp's
+// sum(inv y) and accu(inv) without a pass over the inverse (Q4).
+__global__ __launch_bounds__(1024) void k_aug_dot(const double *__restrict__ A, int64_t ld,
+                                                  int64_t npad, int64_t n,
+                                                  const double *__restrict__ y,
+                                                  double *__restrict__ out) {
+  __shared__ double sh[16];
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += 1024) s += y[j] * A[(npad + 1) + j * ld];
+  s = block_sum1024(s, sh);
+  if (threadIdx.x == 0) {
+    out[0] = s;
+    out[1] = -A[(npad + 1) + (npad + 1) * ld];
+  }
+}
+
+hipError_t launch_aug_dot(const double *A, int64_t ld, int64_t npad, int64_t n, const double *y,
+                          double *out, hipStream_t st) {
+  hipLaunchKernelGGL(k_aug_dot, dim3(1), dim3(1024), 0, st, A, ld, npad, n, y, out);
   return hipGetLastError();
 }
 

@@ -156,13 +156,14 @@ def cpu_baseline(cfg, timeout=240):
     import glob
     fits = _newest_first_last(glob.glob(os.path.join(ROOT, "profiles", "r*_cpu_baseline.json")))
     cmd = [sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), "--n", str(n),
-           "--p", str(p), "--B", str(B), "--kernel", kernel, "--sample-n", "1536"]
+           "--p", str(p), "--B", str(B), "--kernel", kernel, "--sample-n", "2048"]
     if fits:  # extrapolate with the measured exponents (oracle/cpu_scaling.py)
         cmd += ["--fit", fits[-1]]
     try:
         out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, check=True)
         d = json.loads(out.stdout.strip().splitlines()[-1])
-        return {k: d[k] for k in ("value", "unit", "cores", "kind", "sample", "measured_fit")
+        return {k: d[k] for k in ("value", "unit", "cores", "host_nproc", "kind", "seconds_per_eval", "sample",
+                          "measured_fit")
                 if k in d}
     except Exception as e:  # the baseline is reported, never required
         return {"value": None, "unit": "evals/s", "cores": None, "kind": "port",
@@ -258,6 +259,39 @@ def predict_leg(k, model, p, B, nx=4096, reps=3):
     return out
 
 
+def r6_leg(kernel, p, B, theta, std_y, ctx, y, X, Z, iters=5, warmup=2):
+    """The drop-in rate: the reference's UNCHANGED R6 para_update
+    (R/kernel_SE_R6.R:40-62, R/kernel_Matern32_R6.R:39-60) over the .Call
+    surface on device handles (r6.py, the sequence the R shim serves):
+    kernmat_*_symmetric_cpp -> invkernel_cpp -> [mu_solution_cpp] ->
+    grad_*_cpp -> Nadam -> mu_solution_cpp, per iteration.  Same data and
+    theta as the headline steps; wall time per para_update.  The first two
+    iterations allocate the two sweep buffers the loop then alternates
+    between (a freed inverse handle's buffers are reused; in R the handles
+    are freed by the collector): `ms_per_eval` is the median
+    of the later iterations, `ms_first_two` what the allocating ones took."""
+    import numpy as np
+    from additivecausalexpansion_amd import set_optimizer
+    from additivecausalexpansion_amd.r6 import R6KernelMatern32, R6KernelSE
+    Kc = R6KernelMatern32 if kernel == "Matern32" else R6KernelSE
+    k = Kc(p, B, theta, std_y, ctx=ctx)
+    opt = set_optimizer("Nadam", k, 0.01, 0.0, 0.9, 0.999, True, 1.0)
+    times = []
+    st = None
+    for it in range(1, warmup + iters + 1):
+        t0 = time.perf_counter()
+        st = k.para_update(it, y, X, Z, opt, verbose=False)
+        times.append((time.perf_counter() - t0) * 1e3)
+    ms = float(np.median(times[warmup:]))
+    out = {"ms_per_eval": ms, "evals_per_s": 1e3 / ms, "iters": iters, "warmup": warmup,
+           "ms_each": [round(t, 3) for t in times], "ms_first_two": times[:2],
+           "last_stats": [float(st[0]), float(st[1])], "finite": bool(np.all(np.isfinite(st))),
+           "path": "r6.py: kernmat_sym_dev -> invkernel_dev -> mu_solution_dev -> grad_dev "
+                   "(virtual Kfull / elements, resident inverse)"}
+    del k
+    return out
+
+
 def run_sharded(dist, rank, world, ctx, steps, warmup, name=None):
     """One evaluation over all ranks (block-column-sharded model, RCCL)."""
     import additivecausalexpansion_amd as ace
@@ -304,6 +338,7 @@ def main():
     ap.add_argument("--shard-steps", type=int, default=2)
     ap.add_argument("--shard-timeout", type=float, default=240.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-r6", action="store_true", help="skip the unchanged-R6 drop-in leg")
     ap.add_argument("--no-profile", action="store_true",
                     help="diagnostic: no per-launch HIP events (no roofline / phase times)")
     a = ap.parse_args()
@@ -339,6 +374,13 @@ def main():
     grad_ms, _, grad_work = model.kernel_time(2)
     model.profile(False)
     pred = predict_leg(step.kernel_object, model, p, B) if rank == 0 else None
+    r6 = None
+    if rank == 0 and world == 1 and not a.no_r6:
+        try:
+            r6 = r6_leg(kernel, p, B, theta, std_y, ctx, y, X, Z)
+            r6["vs_fused_ms_ratio"] = r6["ms_per_eval"] / (dt_max / a.steps * 1e3)
+        except Exception as e:  # reported, never fatal for the headline
+            r6 = {"error": f"{type(e).__name__}: {e}"[:300]}
 
     line = None
     if rank == 0:
@@ -400,6 +442,7 @@ def main():
             "pair_kernels_hbm_gbs": pair_hbm_gbs(asm_ms / a.steps, grad_ms / a.steps),
             "last_stats": [float(stats[0]), float(stats[1])],
             "predict": pred,
+            "r6_drop_in": r6,
         }
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(a.config)

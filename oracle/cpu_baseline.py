@@ -80,22 +80,43 @@ def main():
     L.ref_grad(kind, n, p, B, P(y), P(X), P(Kf), P(Ke), P(inv), float(np.sum(np.log(w))), P(th),
                P(st), sy, P(g))
     t_grad = time.perf_counter() - t0
-    s2 = (a.n / n) ** e_pairs
-    s3 = (a.n / n) ** e_inv
-    t_full = (t_asm + t_grad) * s2 + t_inv * s3
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
     try:
         cpu = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":")[1].strip()
     except Exception:
         cpu = "unknown"
+    t_pairs = t_asm + t_grad
+    if fit:
+        # one C2 figure: the measured fit (full evaluations at n <= 8192 on
+        # this host type, oracle/cpu_scaling.py) per component, calibrated by
+        # today's sample against the fit's own prediction at the sample size
+        f = fit["fit"]
+        tgt = fit["c2_extrapolated"]["n"]
+        pred_pairs = f["pairs"]["seconds_at_target"] * (n / tgt) ** e_pairs
+        pred_inv = f["inverse_eigh"]["seconds_at_target"] * (n / tgt) ** e_inv
+        pt = [q for q in fit["points_c2_shape"] if q["n"] == n and q["p"] == p and q["B"] == B]
+        if pt:  # a measured point of the fit: compare like with like
+            pred_pairs, pred_inv = pt[0]["pairs"], pt[0]["inverse_eigh"]
+        r_pairs, r_inv = t_pairs / pred_pairs, t_inv / pred_inv
+        sc = (a.n / tgt)
+        c2_fit = (f["pairs"]["seconds_at_target"] * sc ** e_pairs +
+                  f["inverse_eigh"]["seconds_at_target"] * sc ** e_inv)
+        t_full = (f["pairs"]["seconds_at_target"] * sc ** e_pairs * r_pairs +
+                  f["inverse_eigh"]["seconds_at_target"] * sc ** e_inv * r_inv)
+        how = (f"measured fit {os.path.basename(a.fit)} ({c2_fit:.0f} s at n={a.n}) x today's "
+               f"sample / the fit's {'measured point' if pt else 'prediction'} at n={n} (pairs "
+               f"{r_pairs:.3f}, inverse {r_inv:.3f})")
+    else:
+        t_full = t_pairs * (a.n / n) ** e_pairs + t_inv * (a.n / n) ** e_inv
+        how = "sample x (n/n_s)^2 pairs, ^3 inverse"
     out = {
-        "value": 1.0 / t_full, "unit": "evals/s", "cores": threads, "kind": "port",
-        "sample": (f"one {a.kernel} eval at n={n}, p={p}, B={B} (sample of n={a.n}): pair loops "
-                   f"{t_asm + t_grad:.2f} s single-thread x (n/{n})^{e_pairs:.2f}, eigh+inverse "
-                   f"{t_inv:.2f} s on {threads} BLAS threads x (n/{n})^{e_inv:.2f} -> {t_full:.1f} s "
-                   f"per eval (exponents: " +
-                   (f"measured fit {os.path.basename(a.fit)}" if fit else "n^2 / n^3") +
-                   f"); host CPU: {cpu}"),
+        "value": 1.0 / t_full, "unit": "evals/s", "cores": threads, "host_nproc": os.cpu_count(),
+        "kind": "port",
+        "seconds_per_eval": t_full,
+        "sample": (f"one {a.kernel} eval at n={n}, p={p}, B={B}: pair loops {t_pairs:.2f} s "
+                   f"single-threaded (as the reference), eigh+inverse {t_inv:.2f} s on {threads} "
+                   f"BLAS threads (host nproc {os.cpu_count()}); n={a.n}: {t_full:.0f} s per "
+                   f"eval = {how}; host CPU: {cpu}"),
         "sample_seconds": {"assembly": t_asm, "inverse": t_inv, "gradient": t_grad},
         "extrapolated_seconds_per_eval": t_full}
     if fit:
@@ -104,8 +125,10 @@ def main():
             "exponents": {k: v["exponent"] for k, v in fit["fit"].items()},
             "points_seconds_per_eval": {str(q["n"]): q["eval_reference"]
                                         for q in fit["points_c2_shape"]},
-            "c2_seconds_per_eval_reference": fit["c2_extrapolated"]["seconds_per_eval_reference"],
-            "c2_seconds_per_eval_best_cpu": fit["c2_extrapolated"]["seconds_per_eval_best_cpu"],
+            "c2_seconds_per_eval_fit": fit["c2_extrapolated"]["seconds_per_eval_reference"],
+            "c2_seconds_per_eval_best_cpu_fit": fit["c2_extrapolated"]["seconds_per_eval_best_cpu"],
+            "calibration": {"pairs": r_pairs, "inverse": r_inv},
+            "c2_seconds_per_eval": t_full,
             "c1_median_seconds": fit["c1_measured"]}
     print(json.dumps(out))
 

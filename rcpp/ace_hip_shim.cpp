@@ -80,6 +80,15 @@ void ok_gc(F call) {
   ok(st);
 }
 
+// Status check for code R calls from its C internals (the ALTREP methods):
+// no BEGIN_RCPP/END_RCPP guard surrounds those frames, so a C++ exception
+// must not unwind through them.  Rf_error longjmps to R's handler instead;
+// nothing on these frames needs a destructor (R objects are PROTECTed and
+// unwound by R).
+void ok_altrep(int status) {
+  if (status != ACE_OK) Rf_error("ace: %s", ace_last_error(ctx()));
+}
+
 bool use_handles() {
   SEXP o = Rf_GetOption1(Rf_install("ace.device_handles"));
   return o == R_NilValue || Rf_asLogical(o) != FALSE;
@@ -104,7 +113,7 @@ SEXP materialise(SEXP x) {
   if (d2 == R_NilValue) {
     const R_xlen_t n = dmat_length(x);
     d2 = PROTECT(Rf_allocVector(REALSXP, n));
-    ok(ace_dmat_read(handle_of(x), 0, (int64_t)n, REAL(d2)));
+    ok_altrep(ace_dmat_read(handle_of(x), 0, (int64_t)n, REAL(d2)));
     R_set_altrep_data2(x, d2);
     UNPROTECT(1);
   }
@@ -128,7 +137,7 @@ double dmat_elt(SEXP x, R_xlen_t i) {
   SEXP d2 = R_altrep_data2(x);
   if (d2 != R_NilValue) return REAL(d2)[i];
   double v = NA_REAL;
-  ok(ace_dmat_read(handle_of(x), (int64_t)i, 1, &v));
+  ok_altrep(ace_dmat_read(handle_of(x), (int64_t)i, 1, &v));
   return v;
 }
 
@@ -140,7 +149,7 @@ R_xlen_t dmat_get_region(SEXP x, R_xlen_t i, R_xlen_t n, double *buf) {
   if (d2 != R_NilValue) {
     std::copy(REAL(d2) + i, REAL(d2) + i + m, buf);
   } else {
-    ok(ace_dmat_read(handle_of(x), (int64_t)i, (int64_t)m, buf));
+    ok_altrep(ace_dmat_read(handle_of(x), (int64_t)i, (int64_t)m, buf));
   }
   return m;
 }
