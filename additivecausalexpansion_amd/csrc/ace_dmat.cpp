@@ -68,6 +68,8 @@ struct ace_dmat {
   double sig = 0.0;                     // SWEPT: e^sigma added on the diagonal
   std::shared_ptr<KernSrc> src;         // CUBE / KSYM; SWEPT: the KSYM it inverted (or null)
   std::shared_ptr<const std::vector<double>> yaug;  // SWEPT: the y swept along in AUG row 0
+  DBuf msum;                            // dense CUBE: pred_marginal's slice sum (cached)
+  bool have_msum = false;
 };
 
 namespace {
@@ -146,13 +148,17 @@ const double *marginal_rows(ace_dmat *h, int64_t r0, int64_t nr, int64_t *ld, DB
                             nullptr, 0, 1, 0, b0, b1),
        "marginal assembly");
   } else {
-    const double *v = values(h);
-    const int64_t mn = h->rows * n2;
-    DBuf sum;
-    alloc(ctx, sum, (size_t)mn * sizeof(double), "alloc marginal");
-    ck(ctx, launch_marginal_sum(v, h->rows, n2, B, sum.d(), st), "marginal sum");
-    ck(ctx, hipMemcpy2DAsync(scratch.d(), nr * sizeof(double), sum.d() + r0, h->rows * sizeof(double),
-                             nr * sizeof(double), n2, hipMemcpyDeviceToDevice, st),
+    // dense (or materialised) cube: the marginal slice sum is formed once and
+    // kept with the handle (handles are immutable), then rows are copied out
+    if (!h->have_msum) {
+      const double *v = values(h);
+      alloc(ctx, h->msum, (size_t)(h->rows * n2) * sizeof(double), "alloc marginal");
+      ck(ctx, launch_marginal_sum(v, h->rows, n2, B, h->msum.d(), st), "marginal sum");
+      h->have_msum = true;
+    }
+    ck(ctx, hipMemcpy2DAsync(scratch.d(), nr * sizeof(double), h->msum.d() + r0,
+                             h->rows * sizeof(double), nr * sizeof(double), n2,
+                             hipMemcpyDeviceToDevice, st),
        "copy rows");
     sync(ctx);
   }
@@ -714,7 +720,9 @@ int ace_pred_marginal_dev(ace_ctx *ctx, int64_t nX, int64_t nx, const double *y_
   };
   op.kdiag = [&](double *dst) {
     ace_dmat *h = as(K_xx);
-    if (h->kind == ace_dmat::CUBE && !h->have_copy) {
+    // the r = c shortcut needs the symmetric kernel's record (a cross cube's
+    // diagonal pairs rows of two different sides)
+    if (h->kind == ace_dmat::CUBE && !h->have_copy && h->src->symmetric) {
       const KernSrc &k = *h->src;
       const Shape &s = k.shape;
       ck(ctx, launch_kdiag(s.kind, k.s1->view(nx), s.ZS, tab_view(k.tab, s), B > 1 ? 1 : 0,

@@ -221,7 +221,7 @@ struct ShardSweep {
   int64_t ld;         // naug
   int64_t npad;
   int G, r;
-  double *P[2], *W[2];  // naug x NB: Pn = -panel (all rows), W (own rows)
+  double *P[4], *W[4];  // naug x NB: Pn = -panel (all rows), W (own rows); slot k & 3
   double *SW;
   double *S[2];
   double *piv;        // npad pivots (every rank records all of them)
@@ -239,6 +239,14 @@ hipError_t shard_unpack_chain(const ShardSweep &b, int k, int buf, hipStream_t s
 hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t st);
 // every own tile except the cross of block kx (kx < 0: none)
 hipError_t shard_update_main(const ShardSweep &b, int k, int buf, int kx, hipStream_t st);
+// step k with panel slot `slot` on a tile list (skip rule kx as k_update)
+hipError_t shard_update_tiles(const ShardSweep &b, int k, int slot, int kx, const Tile *tiles,
+                              int64_t nt, hipStream_t st);
+// steps ka, ka + 1 in one launch (k_update_pair, panels in slots ka & 3 and
+// (ka + 1) & 3, operands swapped: R = Pn, C = W) on a tile list, skipping the
+// tiles with I or J in blocks [kx0, kx1)
+hipError_t shard_update_pair(const ShardSweep &b, int ka, int kx0, int kx1, const Tile *tiles,
+                             int64_t nt, hipStream_t st);
 
 // ---- small helpers -----------------------------------------------------------
 // AUG rows of columns j < n: row 0 = y (zeros if y is null), row 1 = 1

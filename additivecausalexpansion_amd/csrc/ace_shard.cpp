@@ -136,10 +136,16 @@ void host_allreduce(ace_ctx *ctx, const ace_comm_ops &o, double *dbuf, size_t co
 struct RankState {
   int r = 0;
   DBuf A[2];  // A[1]: train_stats scratch (keeps A[0]'s inverse, Q6)
-  DBuf P[2], W[2], SW, S[2], piv, flag, low, send, recv;
+  DBuf P[4], W[4], SW, S[2], piv, flag, low, send, recv;  // panel slots k & 3
   DBuf tupd, tasm, tgrad;  // device tile lists
   int64_t nupd = 0, nasm = 0, ngrad = 0, ndiag = 0;
   std::vector<Tile> hupd;  // host copy (flop accounting)
+  // pair schedule: own lookahead cross tiles (XCD-dealt), one device list
+  // with host offsets -- xoff[k] .. xoff[k + 1]: tiles with I or J in block
+  // k + 1 (the single-step cross with panel k); poff[2 g], poff[2 g + 1]:
+  // group g's pair cross, block 2 g first, then block 2 g + 1 minus block 2 g
+  DBuf tx, tp;
+  std::vector<int64_t> xoff, poff;
   DBuf y, tab, alpha, scal, gpart, gwork, red, sums, augvec;
   SideBufs side;
 };
@@ -198,11 +204,11 @@ ShardSweep sweep_view(const ShardModel &m, RankState &R, int which) {
   b.npad = m.npad;
   b.G = m.G;
   b.r = R.r;
-  for (int j = 0; j < 2; ++j) {
-    b.P[j] = R.P[j].d();
-    b.W[j] = R.W[j].d();
-    b.S[j] = R.S[j].d();
+  for (int j = 0; j < 4; ++j) {
+    b.P[j] = R.P[j].p ? R.P[j].d() : nullptr;
+    b.W[j] = R.W[j].p ? R.W[j].d() : nullptr;
   }
+  for (int j = 0; j < 2; ++j) b.S[j] = R.S[j].d();
   b.SW = R.SW.d();
   b.piv = R.piv.d();
   b.flag = R.flag.i();
@@ -228,6 +234,63 @@ double update_flops(const std::vector<Tile> &tl, int64_t naug, int64_t k0, int k
     if (!(Ik || Jk)) cnt += (t.I == taug) ? 16.0 / UT : 1.0;
   }
   return cnt * 2.0 * UT * UT * NB;
+}
+
+// GEMM flops of one k_update_pair launch (steps ka, ka + 1) on a tile list,
+// skipping the cross of blocks [kx0, kx1): a tile outside blocks a and b gets
+// two panels, a tile of block a one (it starts from W_a), block b none.
+double update_flops_pair(const std::vector<Tile> &tl, int64_t naug, int64_t ka0, int kx0, int kx1) {
+  constexpr int KT = NB / UT;
+  const int ta0 = (int)(ka0 / UT), tb0 = ta0 + KT;
+  const int taug = (int)(naug / UT) - 1;
+  double cnt = 0.0;
+  for (const Tile &t : tl) {
+    if (t.I < 0) continue;
+    if (kx0 >= 0 && ((t.I >= kx0 * KT && t.I < kx1 * KT) || (t.J >= kx0 * KT && t.J < kx1 * KT)))
+      continue;
+    const bool Ia = t.I >= ta0 && t.I < tb0, Ja = t.J >= ta0 && t.J < tb0;
+    const bool Ib = t.I >= tb0 && t.I < tb0 + KT, Jb = t.J >= tb0 && t.J < tb0 + KT;
+    if (Ib || Jb) continue;
+    cnt += ((t.I == taug) ? 16.0 / UT : 1.0) * ((Ia || Ja) ? 1.0 : 2.0);
+  }
+  return cnt * 2.0 * UT * UT * NB;
+}
+
+// The rank's own lookahead cross lists of the pair schedule (RankState).
+void build_cross_lists(ace_ctx *ctx, RankState &R, int64_t naug, int steps, int G) {
+  constexpr int KT = NB / UT;
+  const std::vector<Tile> own = own_tiles(naug / UT, UT, G, R.r);
+  auto in_blk = [&](int t, int blk) { return t >= blk * KT && t < (blk + 1) * KT; };
+  const int S = update_order_block();
+  auto deal = [&](const std::vector<Tile> &t) { return S > 0 ? xcd_update_order(t, S) : t; };
+  std::vector<Tile> x, pr;
+  R.xoff.assign(1, 0);
+  for (int k = 0; k + 1 < steps; ++k) {
+    std::vector<Tile> t;
+    for (const Tile &q : own)
+      if (in_blk(q.I, k + 1) || in_blk(q.J, k + 1)) t.push_back(q);
+    const std::vector<Tile> o = deal(t);
+    x.insert(x.end(), o.begin(), o.end());
+    R.xoff.push_back((int64_t)x.size());
+  }
+  const int ng = (steps + 1) / 2;
+  R.poff.assign(2 * ng + 1, 0);
+  for (int g = 1; g < ng; ++g) {
+    const int b0 = 2 * g, b1 = 2 * g + 1;
+    std::vector<Tile> ta, tb;
+    for (const Tile &q : own) {
+      if (in_blk(q.I, b0) || in_blk(q.J, b0)) ta.push_back(q);
+      else if (b1 < steps && (in_blk(q.I, b1) || in_blk(q.J, b1))) tb.push_back(q);
+    }
+    R.poff[2 * g] = (int64_t)pr.size();
+    const std::vector<Tile> oa = deal(ta), ob = deal(tb);
+    pr.insert(pr.end(), oa.begin(), oa.end());
+    R.poff[2 * g + 1] = (int64_t)pr.size();
+    pr.insert(pr.end(), ob.begin(), ob.end());
+    R.poff[2 * g + 2] = (int64_t)pr.size();
+  }
+  upload_tiles(ctx, R.tx, x);
+  upload_tiles(ctx, R.tp, pr);
 }
 
 // ---- collectives over the local ranks -------------------------------------
@@ -296,7 +359,9 @@ void allreduce(ShardModel &m, int which, int64_t count, hipStream_t st) {
 }
 
 // ---- the sharded sweep -------------------------------------------------------
-void run_sweep_sharded(ShardModel &m, int which, bool timed) {
+// One step per update launch, lookahead only over RCCL (ACE_PAIR=0: the
+// round-2 schedule, kept for A/B and for npad < 2 NB).
+void run_sweep_sharded_steps(ShardModel &m, int which, bool timed) {
   ace_ctx *ctx = m.ctx;
   hipStream_t st = ctx->stream;
   // the simulated and the host-callback groups run everything in order on
@@ -349,6 +414,120 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
   }
 }
 
+// Two sweep steps per bulk launch, the single-GPU schedule (ace_sweep.hip
+// run_sweep_pairs) on each rank's own tiles.  Group g = steps 2g, 2g + 1:
+//   main:  wait(ready g) -> k_update_pair over the own tiles outside group
+//          g+1's cross (panels 2g, 2g+1) -> bulkdone(g)
+//   side:  wait(bulkdone g-1) -> pair cross of block 2g+2 with panels 2g,
+//          2g+1 -> prepare(2g+2) [pack, exchange, unpack + pivot chain]
+//          -> cross of block 2g+3 with panel 2g+2 -> prepare(2g+3) -> ready(g+1)
+//   side2: the pair cross of block 2g+3 (minus block 2g+2) meanwhile; the
+//          single cross of block 2g+3 waits for it
+// Panels live in slots k & 3.  Every mode runs the lookahead: RCCL exchanges
+// on the side stream; the simulated group's device copies on the side stream
+// (all simulated ranks share the three streams, so their bulk launches
+// overlap the side path exactly as one rank's do); the host-callback group
+// synchronises the side stream and exchanges on the host while the already
+// enqueued bulk launch runs.  The bulk launch of group g is enqueued before
+// the side path of group g+1 so that a blocking (host) exchange overlaps it.
+// Every tile sees the single-step schedule's MFMA chains in the same order:
+// bit-identical to run_sweep_sharded_steps (tests/test_shard_gpu.py).
+void run_sweep_sharded(ShardModel &m, int which, bool timed) {
+  ace_ctx *ctx = m.ctx;
+  const int steps = (int)(m.npad / NB);
+  if (!pair_steps() || steps < 2 || !m.ranks[0]->P[2].p) {
+    run_sweep_sharded_steps(m, which, timed);
+    return;
+  }
+  hipStream_t st = ctx->stream, side = ctx->side, side2 = ctx->side2;
+  const int ng = (steps + 1) / 2;
+  auto zsize = [&](int g) { return std::min(2, steps - 2 * g); };
+  std::vector<ShardSweep> v;
+  for (auto &R : m.ranks) v.push_back(sweep_view(m, *R, which));
+  // events: [0] inputs, ready(g) 1.., bulkdone(g) 1+ng.., side2 start / done
+  auto EV = [&](int i) { return m.ev[(size_t)i]; };
+  const int E_IN = 0;
+  auto E_READY = [&](int g) { return 1 + g; };
+  auto E_BULK = [&](int g) { return 1 + ng + g; };
+  auto E_S2A = [&](int g) { return 1 + 2 * ng + g; };
+  auto E_S2B = [&](int g) { return 1 + 3 * ng + g; };
+  auto rec = [&](int i, hipStream_t s_) { ck(ctx, hipEventRecord(EV(i), s_), "event"); };
+  auto wait = [&](hipStream_t s_, int i) { ck(ctx, hipStreamWaitEvent(s_, EV(i), 0), "event wait"); };
+  auto prepare = [&](int k) {  // panel k into slot k & 3, on `side`
+    for (auto &b : v) ck(ctx, shard_pack(b, k, side), "shard pack");
+    exchange(m, k, side);
+    for (auto &b : v) ck(ctx, shard_unpack_chain(b, k, k & 3, side), "shard panel");
+  };
+  auto single_cross = [&](int k) {  // cross of block k + 1 with panel k, on `side`
+    for (size_t j = 0; j < v.size(); ++j) {
+      RankState &R = *m.ranks[j];
+      const int64_t x0 = R.xoff[(size_t)k], nx = R.xoff[(size_t)k + 1] - x0;
+      ck(ctx, shard_update_tiles(v[j], k, k & 3, -1, (const Tile *)R.tx.p + x0, nx, side),
+         "shard cross update");
+    }
+  };
+  rec(E_IN, st);  // assembly + AUG rows done
+  wait(side, E_IN);
+  prepare(0);
+  single_cross(0);
+  prepare(1);
+  rec(E_READY(0), side);
+  m.upd_used = 0;
+  for (int g = 0; g < ng; ++g) {
+    const int ka = 2 * g;
+    const bool more = g + 1 < ng;
+    wait(st, E_READY(g));
+    const bool tm = timed && m.upd_used + 2 <= (int)m.ev_upd.size();
+    const int kx0 = more ? 2 * (g + 1) : -1, kx1 = more ? 2 * (g + 1) + zsize(g + 1) : -1;
+    for (size_t j = 0; j < v.size(); ++j) {
+      RankState &R = *m.ranks[j];
+      if (tm && j == 0) ck(ctx, hipEventRecord(m.ev_upd[(size_t)m.upd_used], st), "event");
+      if (zsize(g) == 2)
+        ck(ctx, shard_update_pair(v[j], ka, kx0, kx1, (const Tile *)R.tupd.p, R.nupd, st),
+           "shard pair update");
+      else
+        ck(ctx, shard_update_main(v[j], ka, ka & 3, -1, st), "shard update");
+      if (tm && j == 0) {
+        ck(ctx, hipEventRecord(m.ev_upd[(size_t)m.upd_used + 1], st), "event");
+        m.upd_flops[(size_t)m.upd_used / 2] =
+            zsize(g) == 2 ? update_flops_pair(R.hupd, m.naug, (int64_t)ka * NB, kx0, kx1)
+                          : update_flops(R.hupd, m.naug, (int64_t)ka * NB, -1);
+        m.upd_used += 2;
+      }
+    }
+    rec(E_BULK(g), st);
+    if (!more) break;
+    // side path of group g + 1 (its cross tiles were last touched by bulk g-1)
+    const int kb = ka + 2;  // first block of group g + 1
+    if (g > 0) wait(side, E_BULK(g - 1));
+    const bool two = zsize(g + 1) == 2;
+    if (two) {  // block kb + 1's share of the pair cross on side2, concurrently
+      rec(E_S2A(g + 1), side);
+      wait(side2, E_S2A(g + 1));
+      for (size_t j = 0; j < v.size(); ++j) {
+        RankState &R = *m.ranks[j];
+        const int64_t p0 = R.poff[(size_t)(2 * (g + 1) + 1)], np = R.poff[(size_t)(2 * (g + 1) + 2)] - p0;
+        ck(ctx, shard_update_pair(v[j], ka, -1, -1, (const Tile *)R.tp.p + p0, np, side2),
+           "shard pair cross");
+      }
+      rec(E_S2B(g + 1), side2);
+    }
+    for (size_t j = 0; j < v.size(); ++j) {
+      RankState &R = *m.ranks[j];
+      const int64_t p0 = R.poff[(size_t)(2 * (g + 1))], np = R.poff[(size_t)(2 * (g + 1) + 1)] - p0;
+      ck(ctx, shard_update_pair(v[j], ka, -1, -1, (const Tile *)R.tp.p + p0, np, side),
+         "shard pair cross");
+    }
+    prepare(kb);
+    if (two) {
+      wait(side, E_S2B(g + 1));
+      single_cross(kb);
+      prepare(kb + 1);
+    }
+    rec(E_READY(g + 1), side);
+  }
+}
+
 }  // namespace
 
 // ---- entry points used by ace_api.cpp ------------------------------------------
@@ -398,11 +577,13 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
     const int64_t nloc = ncols_local(naug, world, 0);
     alloc(ctx, R->A[0], (size_t)(naug * nloc) * sizeof(double), "alloc local A");
     ck(ctx, hipMemsetAsync(R->A[0].p, 0, R->A[0].bytes, ctx->stream), "memset A");
-    for (int b = 0; b < 2; ++b) {
+    const int nslot = pair_steps() && steps >= 2 ? 4 : 2;  // pair schedule: slots k & 3
+    for (int b = 0; b < nslot; ++b) {
       alloc(ctx, R->P[b], (size_t)(naug * NB) * sizeof(double), "alloc panel");
       alloc(ctx, R->W[b], (size_t)(naug * NB) * sizeof(double), "alloc panel");
-      alloc(ctx, R->S[b], (size_t)(SUB * NB) * sizeof(double), "alloc S");
     }
+    for (int b = 0; b < 2; ++b) alloc(ctx, R->S[b], (size_t)(SUB * NB) * sizeof(double), "alloc S");
+    if (nslot == 4) build_cross_lists(ctx, *R, naug, steps, world);
     alloc(ctx, R->SW, (size_t)SW_DOUBLES * sizeof(double), "alloc SW");
     alloc(ctx, R->piv, (size_t)npad * sizeof(double), "alloc piv");
     alloc(ctx, R->flag, 16, "alloc flag");
@@ -436,10 +617,10 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
     alloc(ctx, R->augvec, (size_t)(2 * npad + 8) * sizeof(double), "alloc aug vector");
     m->ranks.push_back(std::move(R));
   }
-  if (!m->sim) {
-    m->ev.assign((size_t)(2 * steps + 1), nullptr);
-    for (auto &e : m->ev) ck(ctx, hipEventCreateWithFlags(&e, ACE_SYNC_EVENT_FLAGS), "event");
-  }
+  // lookahead events: the step schedule's 2 steps + 1, the pair schedule's
+  // 4 ngroups + 1
+  m->ev.assign((size_t)std::max(2 * steps + 1, 4 * ((steps + 1) / 2) + 1), nullptr);
+  for (auto &e : m->ev) ck(ctx, hipEventCreateWithFlags(&e, ACE_SYNC_EVENT_FLAGS), "event");
   m->ev_upd.assign((size_t)(2 * steps), nullptr);
   m->upd_flops.assign((size_t)steps, 0.0);
   for (auto &e : m->ev_upd) ck(ctx, hipEventCreateWithFlags(&e, ACE_TIMING_EVENT_FLAGS), "event");

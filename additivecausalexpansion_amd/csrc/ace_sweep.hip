@@ -892,20 +892,23 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
 // written once per two steps.  Tiles of block b take W_b (k_update's copy);
 // tiles of block a take W_a (what step a left there) and then only panel b's
 // product; tiles with I or J in blocks [kx0, kx1) (the lookahead cross,
-// updated on the side stream) are skipped.  Single GPU only (G = 1).
+// updated on the side stream) are skipped.  Sharded (G > 1 or wcol): A's
+// columns are block-cyclic (lcol) and the operands swapped (R = Pn, C = W).
 __device__ __forceinline__ void update_pair_tile(
     int I, int J, double (&sW)[2][BK][LDL], double (&sP)[2][BK][LDL], double *__restrict__ A,
     int64_t ld, const double *__restrict__ Ra, const double *__restrict__ Ca,
     const double *__restrict__ Rb, const double *__restrict__ Cb, int64_t ldp, int64_t ka0,
-    const GatherOut &go) {
+    const GatherOut &go, int G, bool wcol) {
   constexpr int KT = NB / UT;
   const int64_t kb0 = ka0 + NB;
   const int ta0 = (int)(ka0 / UT), tb0 = ta0 + KT;
   const bool Ia = I >= ta0 && I < tb0, Ja = J >= ta0 && J < tb0;
   const bool Ib = I >= tb0 && I < tb0 + KT, Jb = J >= tb0 && J < tb0 + KT;
   const int64_t R0 = (int64_t)I * UT, C0 = (int64_t)J * UT;
+  const int64_t L0 = lcol(C0, G);  // A's local column of the tile (sharded: block-cyclic)
   const int tid = threadIdx.x;
-  const double *Wa = Ra, *Wb = Rb;  // single GPU: R = W
+  // single GPU: R = W, C = Pn; sharded (wcol): R = Pn, C = W (own columns)
+  const double *Wa = wcol ? Ca : Ra, *Wb = wcol ? Cb : Rb;
 
   if (Ib || Jb) {  // block b holds W_b after the pair
     if (Ib && !Jb) {
@@ -921,7 +924,7 @@ __device__ __forceinline__ void update_pair_tile(
           for (int e = tid; e < 4096; e += UTHREADS) {
             const int a = e & 63, c = e >> 6;
             const double v = tileT[a * 65 + c];
-            A[(R0 + 64 * sa + a) + (C0 + 64 * sb + c) * ld] = v;
+            A[(R0 + 64 * sa + a) + (L0 + 64 * sb + c) * ld] = v;
             if (go.k0 >= 0) gput(go, R0 + 64 * sa + a, C0 + 64 * sb + c, v);
           }
         }
@@ -929,7 +932,7 @@ __device__ __forceinline__ void update_pair_tile(
       for (int e = tid; e < UT * UT; e += UTHREADS) {
         const int a = e & (UT - 1), c = e >> 7;
         const double v = Wb[(R0 + a) + (C0 - kb0 + c) * ldp];
-        A[(R0 + a) + (C0 + c) * ld] = v;
+        A[(R0 + a) + (L0 + c) * ld] = v;
         if (go.k0 >= 0) gput(go, R0 + a, C0 + c, v);
       }
     }
@@ -947,10 +950,10 @@ __device__ __forceinline__ void update_pair_tile(
   if (R0 >= ld - AUG) {  // AUG row block: 16 live rows (as k_update)
     d4 acc;
     const int64_t r = R0 + lr;
-    const int64_t c = C0 + 16 * wv + lk;
+    const int64_t c = C0 + 16 * wv + lk, lc = L0 + 16 * wv + lk;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      acc[j] = from_w ? wab[r * wrs + (c + 4 * j) * wcs] : ld_a(&A[r + (c + 4 * j) * ld]);
+      acc[j] = from_w ? wab[r * wrs + (c + 4 * j) * wcs] : ld_a(&A[r + (lc + 4 * j) * ld]);
     for (int pnl = from_w ? 1 : 0; pnl < 2; ++pnl) {
       const double *gr = (pnl ? Rb : Ra) + R0 + lr + (int64_t)lk * ldp;
       const double *gc = (pnl ? Cb : Ca) + C0 + 16 * wv + lr + (int64_t)lk * ldp;
@@ -965,7 +968,7 @@ __device__ __forceinline__ void update_pair_tile(
       }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) st_a(&A[r + (c + 4 * j) * ld], acc[j]);
+    for (int j = 0; j < 4; ++j) st_a(&A[r + (lc + 4 * j) * ld], acc[j]);
     if (go.k0 >= 0) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) gput(go, r, c + 4 * j, acc[j]);
@@ -994,13 +997,13 @@ __device__ __forceinline__ void update_pair_tile(
 #pragma unroll
     for (int ri = 0; ri < 4; ++ri) {
       const int64_t r = R0 + 64 * wr + 16 * ri + lr;
-      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+      const int64_t c = C0 + 32 * wc + 16 * ci + lk, lc = L0 + 32 * wc + 16 * ci + lk;
       if (from_w) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[ci][ri][j] = wab[r * wrs + (c + 4 * j) * wcs];
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[ci][ri][j] = ld_a(&A[r + (c + 4 * j) * ld]);
+        for (int j = 0; j < 4; ++j) acc[ci][ri][j] = ld_a(&A[r + (lc + 4 * j) * ld]);
       }
     }
   *reinterpret_cast<double2 *>(&sW[0][sk][sm]) = rw0;
@@ -1050,9 +1053,9 @@ __device__ __forceinline__ void update_pair_tile(
 #pragma unroll
     for (int ri = 0; ri < 4; ++ri) {
       const int64_t r = R0 + 64 * wr + 16 * ri + lr;
-      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+      const int64_t lc = L0 + 32 * wc + 16 * ci + lk;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) st_a(&A[r + (c + 4 * j) * ld], acc[ci][ri][j]);
+      for (int j = 0; j < 4; ++j) st_a(&A[r + (lc + 4 * j) * ld], acc[ci][ri][j]);
     }
   if (go.k0 >= 0) {
 #pragma unroll
@@ -1076,7 +1079,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
     double *__restrict__ A, int64_t ld, const double *__restrict__ Ra,
     const double *__restrict__ Ca, const double *__restrict__ Rb, const double *__restrict__ Cb,
     int64_t ldp, int64_t ka0, int kx0, int kx1, const Tile *__restrict__ tiles, GatherOut go,
-    int nfront, int *cnt) {
+    int nfront, int *cnt, int G, int wcol) {
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
   constexpr int KT = NB / UT;
@@ -1099,7 +1102,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
     return;
   GatherOut g = go;
   if (nfront >= 0 && !front) g.k0 = -1;
-  update_pair_tile(I, J, sW, sP, A, ld, Ra, Ca, Rb, Cb, ldp, ka0, g);
+  update_pair_tile(I, J, sW, sP, A, ld, Ra, Ca, Rb, Cb, ldp, ka0, g, G, wcol != 0);
   if (front && cnt) {
     // publish (cdna_hip_programming.md §6 Guideline 16, counter form): every
     // wave drains its stores, then one lane releases at agent scope and adds
@@ -1805,13 +1808,13 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
         }
         if (nah > 0) hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nah), dim3(UTHREADS), 0, side, b.A, b.ld,
                            b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0,
-                           -1, -1, b.ptiles + pa, gout(k + 2), -1, nullptr);
+                           -1, -1, b.ptiles + pa, gout(k + 2), -1, nullptr, 1, 0);
         if (xs) {  // the rest of block 2g+2's cross on side2; its panel GEMM waits for E3
           if (na > nah)
             hipLaunchKernelGGL(k_update_pair, dim3((unsigned)(na - nah)), dim3(UTHREADS), 0, side2,
                                b.A, b.ld, b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)],
                                b.P[slot(k + 1)], b.ld, ka0, -1, -1, b.ptiles + pa + nah, gout(k + 2),
-                               -1, nullptr);
+                               -1, nullptr, 1, 0);
           if ((e = hipEventRecord(E3(g + 1), side2)) != hipSuccess) return e;
         }
         if (nb > 0) {
@@ -1821,7 +1824,7 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
           }
           hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nb), dim3(UTHREADS), 0, side2, b.A, b.ld,
                              b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld,
-                             ka0, -1, -1, b.ptiles + pb, no_gather(), -1, nullptr);
+                             ka0, -1, -1, b.ptiles + pb, no_gather(), -1, nullptr, 1, 0);
           if (two2 && (e = hipEventRecord(E2(g + 1), side2)) != hipSuccess) return e;
         }
         if ((e = produce(g + 1, nb > 0)) != hipSuccess) return e;
@@ -1844,7 +1847,7 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
       hipLaunchKernelGGL(k_update_pair, dim3(grid), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[slot(k)],
                          b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0, kx0, kx1,
                          ord, mfront ? gout(k + 2) : no_gather(), mfront ? b.mfront[g] : -1,
-                         mfront ? b.mcnt + g : nullptr);
+                         mfront ? b.mcnt + g : nullptr, 1, 0);
     else
       hipLaunchKernelGGL(k_update, dim3(grid), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[slot(k)],
                          b.P[slot(k)], b.W[slot(k)], b.ld, ka0, -1, ord, 1, no_gather());
@@ -1972,6 +1975,24 @@ hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t s
   hipLaunchKernelGGL(k_update_x, dim3((unsigned)(naug / XT), 2 * (NB / XT)), dim3(256), 0, st,
                      b.A, b.ld, b.P[buf], b.W[buf], b.W[buf], b.ld, (int64_t)k * NB, k + 1, b.G,
                      b.r);
+  return hipGetLastError();
+}
+
+hipError_t shard_update_tiles(const ShardSweep &b, int k, int slot, int kx, const Tile *tiles,
+                              int64_t nt, hipStream_t st) {
+  if (nt > 0)
+    hipLaunchKernelGGL(k_update, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld, b.P[slot],
+                       b.W[slot], b.W[slot], b.ld, (int64_t)k * NB, kx, tiles, b.G, no_gather());
+  return hipGetLastError();
+}
+
+hipError_t shard_update_pair(const ShardSweep &b, int ka, int kx0, int kx1, const Tile *tiles,
+                             int64_t nt, hipStream_t st) {
+  const int sa = ka & 3, sb = (ka + 1) & 3;
+  if (nt > 0)
+    hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld, b.P[sa],
+                       b.W[sa], b.P[sb], b.W[sb], b.ld, (int64_t)ka * NB, kx0, kx1, tiles,
+                       no_gather(), -1, nullptr, b.G, 1);
   return hipGetLastError();
 }
 

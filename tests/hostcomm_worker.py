@@ -7,6 +7,7 @@ block-column-sharded model whose panel exchanges and all-reduces go through
 torch.distributed on host buffers (ace_model_create_sharded_host).  Rank 0
 writes what every check needs to OUT (npz).
 """
+import datetime
 import os
 import sys
 
@@ -18,7 +19,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     out, kind, n, p, B = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
     import torch.distributed as dist
-    dist.init_process_group("gloo")
+    # short timeout: a rank whose collective failed must not hang its peers long
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=60))
     rank, world = dist.get_rank(), dist.get_world_size()
     import additivecausalexpansion_amd as A
     from additivecausalexpansion_amd.hostcomm import HostComm

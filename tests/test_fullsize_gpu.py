@@ -175,3 +175,48 @@ def test_c4_fullsize_sharded8_and_rccl_match_single(A):
     close(g3, g1, 1e-9, 1e-11)
     close(s3, s1, 1e-10, 0)
     rc.close()
+
+
+@pytest.mark.timeout(600)
+def test_c2_fullsize_predict_against_torch(A, tmp_path):
+    """ace_model_predict / ace_model_predict_marginal with ATE, ATT, ATU at
+    n = 16384 (C2), nx = 4096 test points, against the torch restatement of
+    pred_cpp / pred_marginal_cpp (tests/torch_ref.py predict: Cholesky inverse
+    at theta_{T-1}, kernels at theta_T, Q6).  Tolerances 1e-6: map relative
+    (with a floor of 1e-9 of the largest), each variance to 1e-6 of the terms
+    its quadratic form cancels (a form the reference sees as negative gives
+    NaN there; the engine may only disagree on that inside the tolerance)."""
+    kernel, n, p, B, y, X, Z, th, sy = _problem("C2", seed=1000)
+    nx = 4096
+    from additivecausalexpansion_amd.synthetic import make_problem
+    _, X2, Z2, _, _ = make_problem(nx, p, B, seed=77)
+    dZ2 = np.asfortranarray(0.5 * Z2 + 0.05)
+    zx = (np.arange(nx) % 3 == 0).astype(float)
+    m = A.DeviceModel(kernel, n, p, B)
+    m.set_data(y, X, Z, sy)
+    th_prev = th.copy()
+    m.para_update(2, th_prev)  # resident inverse at theta_{T-1}
+    th_T = th + 0.02
+    th_T[1] = 0.07
+    got = m.predict(th_T, X2, Z2, 0.3, 1.7)
+    gm = m.predict_marginal(th_T, X2, dZ2, zx, 1.7, 0.8, True)
+    inp, out = str(tmp_path / "pin.npz"), str(tmp_path / "pout.npz")
+    np.savez(inp, mode="predict", kernel=kernel, y=y, X=X, Z=Z, theta_inv=th, theta=th_T, X2=X2,
+             Z2=Z2, dZ2=dZ2, zx=zx, mean_y=0.3, std_y=1.7, std_Z=0.8)
+    subprocess.run([sys.executable, os.path.join(ROOT, "tests", "torch_ref.py"), inp, out],
+                   check=True, timeout=420)
+    with np.load(out, allow_pickle=False) as d:
+        ref = {k: d[k] for k in d.files}
+    close(got["map"], ref["map"], 1e-6, 1e-9)
+    assert np.all(np.abs(got["var"] - ref["var"]) <= 1e-6 * ref["var_terms"])
+    close(gm["map"], ref["mmap"], 1e-6, 1e-9)
+    assert np.all(np.abs(gm["var"] - ref["mvar"]) <= 1e-6 * ref["mvar_terms"])
+    for j, k in enumerate(("ate", "att", "atu")):
+        close(gm[k]["map"], ref["avg_map"][j], 1e-6, 1e-9)
+        cnt = (nx, zx.sum(), nx - zx.sum())[j]
+        tol = 1e-6 * ref["avg_terms"][j]
+        want = (1.7 / cnt) ** 2 * ref["avg_q"][j]
+        if np.isnan(gm[k]["var"]):
+            assert want < tol, (k, want, tol)
+        else:
+            assert abs(gm[k]["var"] - max(want, 0.0)) <= tol, (k, gm[k]["var"], want, tol)

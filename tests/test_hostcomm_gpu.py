@@ -59,13 +59,38 @@ def _run_group(world, out, kind, n, p, B):
     return dict(np.load(out))
 
 
-@pytest.mark.parametrize("world,kind,n,p,B", [(2, "SE", 700, 3, 4), (3, "Matern32", 900, 5, 5)])
+@pytest.mark.parametrize("world,kind,n,p,B", [(2, "SE", 700, 3, 4), (3, "Matern32", 900, 5, 5),
+                                              (2, "Matern32", 2000, 6, 5)])
 def test_sharded_processes_match_single_gpu_and_oracle(A, O, tmp_path, world, kind, n, p, B):
+    """The pair-step lookahead schedule runs in every rank process: the bulk
+    update of group g is in flight while the rank's host exchanges group
+    g+1's panels (n = 2000: 8 sweep steps, 4 groups).  The processes'
+    inverse equals the in-process simulated group's of the same world size
+    bit for bit (same kernels, same operand order; only the transport and the
+    concurrency differ), the all-reduced sums to the last bits, and the
+    single-GPU model and the oracle to rounding."""
     r = _run_group(world, str(tmp_path / "r.npz"), kind, n, p, B)
     y, X, Z, sy = r["y"], r["X"], r["Z"], float(r["sy"][0])
     # every rank returned the same gradient
     for q in range(1, world):
         assert np.array_equal(r["g2_all_ranks"][q], r["g2_all_ranks"][0])
+    sim = A.DeviceModel(kind, n, p, B, world=world, rank=0, sharded=True)
+    sim.set_data(y, X, Z, sy)
+    th1 = r["theta1"].copy()
+    th1[1] = 0.0
+    gs1, ss1, _ = sim.para_update(1, th1)
+    gs2, ss2, _ = sim.para_update(2, r["theta2"].copy())
+    # the swept matrix has no reduction in it: bitwise; the gradient sums are
+    # all-reduced (gloo's summation order vs the simulated group's rank
+    # order, exact for two ranks): to the last bits
+    assert np.array_equal(np.diag(sim.inverse()), r["inv_diag"])
+    close(gs1, r["g1"], 1e-13, 1e-14)
+    close(ss1, r["st1"], 1e-13, 0)
+    close(gs2, r["g2"], 1e-13, 1e-14)
+    close(ss2, r["st2"], 1e-13, 0)
+    if world == 2:
+        assert np.array_equal(gs2, r["g2"]) and np.array_equal(ss2, r["st2"])
+    sim.close()
     # the single-GPU model on the same data and thetas
     m = A.DeviceModel(kind, n, p, B)
     m.set_data(y, X, Z, sy)

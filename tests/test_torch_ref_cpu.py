@@ -30,3 +30,39 @@ def test_torch_ref_matches_oracle(kernel, it, n, p, B):
     assert np.all(np.abs(r["grad"] - g) <= 1e-10 * np.abs(g) + 1e-12 * scale)
     assert np.allclose(r["stats"], st, rtol=1e-10, atol=0)
     assert r["logdet"] == pytest.approx(float(np.sum(np.log(inv["eigenval"]))), rel=1e-12)
+
+
+@pytest.mark.parametrize("kernel", ["SE", "Matern32"])
+def test_torch_ref_predict_matches_oracle(kernel):
+    """The prediction restatement (pred_cpp / pred_marginal_cpp with the Q6
+    theta mix) against the oracle at small n, to 1e-9."""
+    pytest.importorskip("torch")
+    import torch_ref
+    from additivecausalexpansion_amd.synthetic import make_problem
+    from oracle import ace_oracle as O
+    n, p, B, nx = 220, 3, 5, 60
+    y, X, Z, th_prev, sy = make_problem(n, p, B, seed=7)
+    th = th_prev + 0.02
+    th[1] = 0.1
+    _, X2, Z2, _, _ = make_problem(nx, p, B, seed=8)
+    dZ2 = 0.6 * Z2 + 0.1
+    zx = (np.arange(nx) % 3 == 0).astype(float)
+    r = torch_ref.predict(kernel, y, X, Z, th_prev, th, X2, Z2, dZ2, zx, 0.3, 1.7, 0.8, dev="cpu")
+    sym, cross, _ = O.KERNELS[kernel]
+    inv = O.invkernel_cpp(sym(X, Z, th_prev)["full"], th_prev[0])["inv"]
+    ref = O.pred_cpp(y, th[0], th[1], inv, cross(X2, X, Z2, Z, th)["full"], sym(X2, Z2, th)["full"],
+                     0.3, 1.7)
+    assert np.allclose(r["map"], ref["map"], rtol=1e-9, atol=0)
+    assert np.all(np.abs(r["var"] - ref["var"]) <= 1e-9 * r["var_terms"])
+    rm = O.pred_marginal_cpp(y, zx, th[0], th[1], inv, cross(X2, X, dZ2, Z, th)["elements"],
+                             sym(X2, dZ2, th)["elements"], 0.3, 1.7, 0.8, True)
+    assert np.allclose(r["mmap"], rm["map"], rtol=1e-9, atol=1e-12 * np.abs(rm["map"]).max())
+    assert np.all(np.abs(r["mvar"] - rm["var"]) <= 1e-9 * r["mvar_terms"])
+    for j, k in enumerate(("ate", "att", "atu")):
+        assert r["avg_map"][j] == pytest.approx(rm[k]["map"], rel=1e-9, abs=1e-12)
+        cnt = (nx, zx.sum(), nx - zx.sum())[j]
+        q = r["avg_q"][j]
+        if q >= 0:
+            assert abs((1.7 / cnt) ** 2 * q - rm[k]["var"]) <= 1e-9 * r["avg_terms"][j]
+        else:
+            assert np.isnan(rm[k]["var"])

@@ -25,9 +25,21 @@ The pair sums run over row chunks; sum_rc M d_i^2 is taken as
 sum_r x_ri^2 R_r + sum_c x_ci^2 C_c - 2 sum_r x_ri (M X)_ri (R, C the row /
 column sums of M), one GEMM per slice instead of p elementwise passes.
 
+Prediction (mode "predict"): pred_cpp and pred_marginal_cpp with ATE / ATT /
+ATU (src/pred_cpp.cpp:8-126) with the inverse at theta_inv (the last
+para_update's, Q6: R/kernel_SE_R6.R:37) and the kernels at theta
+(R/kernel_SE_R6.R:75-97): tmp = K_xX A^-1, map = mean_y + std_y (tmp (y - mu)
++ mu), var = std_y^2 |diag(K_xx - tmp K_xX^T) + e^theta0|; marginal over
+slices 1..B-1 with the derivative basis dZ2, the full nx x nx posterior
+matrix for the averaged effects.  Returned beside each variance: the
+quadratic form before the sqrt and the size of the terms it cancels.
+
 usage: python tests/torch_ref.py in.npz out.npz
   in:  kernel ("SE"/"Matern32"), y, X, Z, theta, std_y, it
+       [mode="predict", theta_inv, X2, Z2, dZ2, zx, mean_y, std_Z]
   out: grad, stats, rmse_identity, logdet, mu, alpha_head
+       (predict: map, var, var_q, var_terms, mmap, mvar, mvar_q, mvar_terms,
+        avg_map[3], avg_q[3], avg_terms[3])
 """
 import math
 import sys
@@ -138,10 +150,111 @@ def para_update(kernel, y, X, Z, theta, std_y, it, dev="cuda", chunk=1024):
             "alpha_head": alpha[:64].cpu().numpy()}
 
 
+def _weights(th, B, p, dev):
+    f64 = torch.float64
+    wk = torch.tensor([[math.exp(-th[1 + b + B * (i + 1)]) for i in range(p)] for b in range(B)],
+                      dtype=f64, device=dev)
+    return wk, [float(th[2 + b]) for b in range(B)]
+
+
+def kernel_sum(kernel, Xa, Za, Xb, Zb, th, b0, b1, same=False, dev="cuda"):
+    """sum_{b0 <= b < b1} K_b(Xa, Xb) (src/kernel_SE_cpp.cpp:9-64,
+    src/kernel_Matern_cpp.cpp:52-93), z_0 = 1, z_b = Z[:, b-1]."""
+    f64 = torch.float64
+    p = Xa.shape[1]
+    B = Za.shape[1] + 1
+    wk, lam = _weights(th, B, p, dev)
+    xa = torch.tensor(Xa, dtype=f64, device=dev)
+    xb = torch.tensor(Xb, dtype=f64, device=dev)
+    s3 = math.sqrt(3.0)
+    out = torch.zeros((xa.shape[0], xb.shape[0]), dtype=f64, device=dev)
+    for b in range(b0, b1):
+        w = wk[b]
+        G = torch.addmm(((xa * xa) @ w)[:, None], xa * w, xb.T, alpha=-2.0)
+        G.add_(((xb * xb) @ w)[None, :]).clamp_(min=0.0)
+        if same:
+            G.fill_diagonal_(0.0)
+        if kernel == "SE":
+            K = G.neg_().add_(lam[b]).exp_()
+        else:
+            t = G.sqrt_()
+            e = torch.exp(lam[b] - s3 * t)
+            K = t.mul_(s3).add_(1.0).mul_(e)
+        if b > 0:
+            K.mul_(torch.tensor(Za[:, b - 1], dtype=f64, device=dev)[:, None])
+            K.mul_(torch.tensor(Zb[:, b - 1], dtype=f64, device=dev)[None, :])
+        out.add_(K)
+        del G, K
+    return out
+
+
+def predict(kernel, y, X, Z, theta_inv, theta, X2, Z2, dZ2, zx, mean_y, std_y, std_Z, dev="cuda"):
+    f64 = torch.float64
+    n = X.shape[0]
+    B = Z.shape[1] + 1
+    th = np.array(theta, dtype=np.float64)
+    A = kernel_sum(kernel, X, Z, X, Z, theta_inv, 0, B, same=True, dev=dev)
+    A.diagonal().add_(math.exp(theta_inv[0]))
+    L, info = torch.linalg.cholesky_ex(A)
+    del A
+    if int(info) != 0:
+        raise RuntimeError(f"not positive definite (info {int(info)})")
+    Ainv = torch.cholesky_inverse(L)
+    del L
+    w = torch.tensor(y, dtype=f64, device=dev) - th[1]
+    out = {}
+    # pred_cpp (src/pred_cpp.cpp:8-34)
+    KxX = kernel_sum(kernel, X2, Z2, X, Z, th, 0, B, dev=dev)
+    tmp = KxX @ Ainv
+    out["map"] = (mean_y + std_y * (tmp @ w + th[1])).cpu().numpy()
+    q = (tmp * KxX).sum(1)
+    kxx = torch.diagonal(kernel_sum(kernel, X2, Z2, X2, Z2, th, 0, B, same=True, dev=dev))
+    d = kxx - q + math.exp(th[0])
+    out["var_q"] = d.cpu().numpy()
+    out["var"] = (std_y * torch.sqrt(d.abs())).pow(2).cpu().numpy()
+    out["var_terms"] = (std_y ** 2 * (kxx.abs() + q.abs() + math.exp(th[0]))).cpu().numpy()
+    del KxX, tmp
+    # pred_marginal_cpp (src/pred_cpp.cpp:37-126): slices 1..B-1 (or 0 if B == 1)
+    b0, b1 = (1, B) if B > 1 else (0, 1)
+    KmX = kernel_sum(kernel, X2, dZ2, X, Z, th, b0, b1, dev=dev)
+    Kmx = kernel_sum(kernel, X2, dZ2, X2, dZ2, th, b0, b1, same=True, dev=dev)
+    tmp = KmX @ Ainv
+    yx = std_y * (tmp @ w) / std_Z
+    C = tmp @ KmX.T
+    post = Kmx - C
+    dq = torch.diagonal(post)
+    out["mmap"] = yx.cpu().numpy()
+    out["mvar_q"] = dq.cpu().numpy()
+    out["mvar"] = (std_y * torch.sqrt(dq.abs()) / std_Z).pow(2).cpu().numpy()
+    out["mvar_terms"] = ((std_y / std_Z) ** 2 * (torch.diagonal(Kmx).abs() +
+                                                 torch.diagonal(C).abs())).cpu().numpy()
+    zt = torch.tensor(zx, dtype=f64, device=dev)
+    nx = X2.shape[0]
+    ntx = float(int(zx.sum()))
+    ate = float(yx.mean())
+    att = float(yx @ zt) / ntx
+    atu = (ate * nx - att * ntx) / (nx - ntx)
+    am, aq, at = [ate, att, atu], [], []
+    for wv, cnt in ((torch.ones(nx, dtype=f64, device=dev), nx), (zt, ntx),
+                    ((zt == 0).to(f64), nx - ntx)):
+        aq.append(float(wv @ post @ wv))
+        at.append((std_y / cnt) ** 2 * (abs(float(wv @ Kmx @ wv)) + abs(float(wv @ C @ wv))))
+    out["avg_map"] = np.array(am)
+    out["avg_q"] = np.array(aq)
+    out["avg_terms"] = np.array(at)
+    return out
+
+
 def main():
     inp, out = sys.argv[1], sys.argv[2]
     with np.load(inp, allow_pickle=False) as d:
         args = {k: d[k] for k in d.files}
+    if "mode" in args and str(args["mode"]) == "predict":
+        r = predict(str(args["kernel"]), args["y"], args["X"], args["Z"], args["theta_inv"],
+                    args["theta"], args["X2"], args["Z2"], args["dZ2"], args["zx"],
+                    float(args["mean_y"]), float(args["std_y"]), float(args["std_Z"]))
+        np.savez(out, **r)
+        return
     r = para_update(str(args["kernel"]), args["y"], args["X"], args["Z"], args["theta"],
                     float(args["std_y"]), int(args["it"]))
     np.savez(out, **r)
