@@ -183,7 +183,8 @@ std::vector<Tile> xcd_update_order(const std::vector<Tile> &tl, int S,
 // per group of two steps, the bulk order with each XCD's cheap tiles last
 // (ACE_TAIL_SORT=1): ngroups lists of *len entries
 bool tail_sort();
-std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len);
+// (sharded: rank r's own tiles of G)
+std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len, int G = 1, int r = 0);
 // own lower tiles of size T over [0, ntile*T) in row-major order (ace_shard.cpp)
 std::vector<Tile> own_tiles(int64_t ntile, int T, int G, int r);
 // super-block size S of that order (0: row-major grid); ACE_UPD_ORDER=S

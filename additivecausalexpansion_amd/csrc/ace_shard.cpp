@@ -138,7 +138,7 @@ struct RankState {
   DBuf A[2];  // A[1]: train_stats scratch (keeps A[0]'s inverse, Q6)
   DBuf P[4], W[4], SW, S[2], piv, flag, low, send, recv;  // panel slots k & 3
   DBuf tupd, tasm, tgrad;  // device tile lists
-  int64_t nupd = 0, nasm = 0, ngrad = 0, ndiag = 0;
+  int64_t nupd = 0, nasm = 0, nasm1 = 0, ngrad = 0, ndiag = 0;  // nasm1: first-part tiles
   std::vector<Tile> hupd;  // host copy (flop accounting)
   // pair schedule: own lookahead cross tiles (XCD-dealt), one device list
   // with host offsets -- xoff[k] .. xoff[k + 1]: tiles with I or J in block
@@ -146,6 +146,10 @@ struct RankState {
   // group g's pair cross, block 2 g first, then block 2 g + 1 minus block 2 g
   DBuf tx, tp;
   std::vector<int64_t> xoff, poff;
+  // per group g: the bulk order (pair_bulk_orders: own tiles XCD-dealt with
+  // each XCD's cheap / skipped tiles last), glen entries each (0: use tupd)
+  DBuf tgo;
+  int64_t glen = 0;
   DBuf y, tab, alpha, scal, gpart, gwork, red, sums, augvec;
   SideBufs side;
 };
@@ -291,6 +295,11 @@ void build_cross_lists(ace_ctx *ctx, RankState &R, int64_t naug, int steps, int 
   }
   upload_tiles(ctx, R.tx, x);
   upload_tiles(ctx, R.tp, pr);
+  R.glen = 0;
+  if (tail_sort()) {
+    const std::vector<Tile> o = pair_bulk_orders(naug, steps, &R.glen, G, R.r);
+    upload_tiles(ctx, R.tgo, o);
+  }
 }
 
 // ---- collectives over the local ranks -------------------------------------
@@ -466,7 +475,8 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
          "shard cross update");
     }
   };
-  rec(E_IN, st);  // assembly + AUG rows done
+  // E_IN: recorded by shard_eval after the first two panels' columns, the
+  // AUG rows and the flag (the rest of the assembly runs on under prepare(0))
   wait(side, E_IN);
   prepare(0);
   single_cross(0);
@@ -482,7 +492,11 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
     for (size_t j = 0; j < v.size(); ++j) {
       RankState &R = *m.ranks[j];
       if (tm && j == 0) ck(ctx, hipEventRecord(m.ev_upd[(size_t)m.upd_used], st), "event");
-      if (zsize(g) == 2)
+      if (zsize(g) == 2 && R.glen > 0)
+        ck(ctx, shard_update_pair(v[j], ka, kx0, kx1, (const Tile *)R.tgo.p + (int64_t)g * R.glen,
+                                  R.glen, st),
+           "shard pair update");
+      else if (zsize(g) == 2)
         ck(ctx, shard_update_pair(v[j], ka, kx0, kx1, (const Tile *)R.tupd.p, R.nupd, st),
            "shard pair update");
       else
@@ -595,7 +609,12 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
     if (const int S = update_order_block(); S > 0) R->hupd = xcd_update_order(R->hupd, S);
     R->nupd = (int64_t)R->hupd.size();
     upload_tiles(ctx, R->tupd, R->hupd);
-    const std::vector<Tile> ta = own_tiles(npad / AT, AT, world, R->r);
+    std::vector<Tile> ta = own_tiles(npad / AT, AT, world, R->r);
+    // the first two panels' columns first (the pair schedule's first side
+    // path runs under the rest of the assembly, as model_pipeline's)
+    const int jb = 2 * NB / AT;
+    R->nasm1 = std::stable_partition(ta.begin(), ta.end(), [&](const Tile &t) { return t.J < jb; }) -
+               ta.begin();
     R->nasm = (int64_t)ta.size();
     upload_tiles(ctx, R->tasm, ta);
     std::vector<Tile> tg = own_tiles(m->ntr, AT, world, R->r);
@@ -678,20 +697,27 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
        "upload tables");
   }
   ck(ctx, hipStreamSynchronize(st), "sync tables");  // pageable source
-  // assembly (own tiles) + AUG rows
-  for (size_t j = 0; j < m->ranks.size(); ++j) {
-    RankState &R = *m->ranks[j];
-    const TabView tv = tab_view(R.tab, s);
-    const PairSide ps = R.side.view(n);
-    if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_asm[0], st), "event");
-    ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, npad, s.B, s.ZS, tv, sig, R.A[which].d(),
-                            naug, nullptr, st, R.tasm.p ? (const Tile *)R.tasm.p : nullptr,
-                            R.nasm, m->G),
-       "assembly");
-    if (timed && j == 0) ck(ctx, hipEventRecord(m->ev_asm[1], st), "event");
-    ck(ctx, launch_aug_init(R.A[which].d(), naug, npad, n, R.y.d(), st, m->G, R.r), "aug init");
-    ck(ctx, hipMemsetAsync(R.flag.p, 0, sizeof(int), st), "memset flag");
+  // assembly (own tiles) + AUG rows: the first two panels' columns, the
+  // AUG rows and the flag, then (the sweep's first side path may start) the rest
+  if (timed) ck(ctx, hipEventRecord(m->ev_asm[0], st), "event");
+  for (int part = 0; part < 2; ++part) {
+    for (size_t j = 0; j < m->ranks.size(); ++j) {
+      RankState &R = *m->ranks[j];
+      const TabView tv = tab_view(R.tab, s);
+      const PairSide ps = R.side.view(n);
+      const int64_t t0 = part ? R.nasm1 : 0, nt = part ? R.nasm - R.nasm1 : R.nasm1;
+      if (nt > 0)
+        ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, npad, s.B, s.ZS, tv, sig, R.A[which].d(),
+                                naug, nullptr, st, (const Tile *)R.tasm.p + t0, nt, m->G),
+           "assembly");
+      if (part == 0) {
+        ck(ctx, launch_aug_init(R.A[which].d(), naug, npad, n, R.y.d(), st, m->G, R.r), "aug init");
+        ck(ctx, hipMemsetAsync(R.flag.p, 0, sizeof(int), st), "memset flag");
+      }
+    }
+    if (part == 0) ck(ctx, hipEventRecord(m->ev[0], st), "event");  // the sweep's inputs ready
   }
+  if (timed) ck(ctx, hipEventRecord(m->ev_asm[1], st), "event");
   run_sweep_sharded(*m, which, timed);
   // alpha, mu_solution
   for (auto &R : m->ranks)

@@ -1515,11 +1515,11 @@ bool tail_sort() {
   return v != 0;
 }
 
-std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len) {
+std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len, int G, int r) {
   const int64_t nT = naug / UT;
   constexpr int KT = NB / UT;
   const int ng = (steps + 1) / 2;
-  const std::vector<Tile> base = own_tiles(nT, UT, 1, 0);
+  const std::vector<Tile> base = own_tiles(nT, UT, G, r);
   const int S = std::max(1, update_order_block());
   std::vector<Tile> all;
   *len = 0;
