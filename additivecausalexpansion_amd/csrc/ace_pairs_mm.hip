@@ -276,6 +276,20 @@ __device__ __forceinline__ void tile_of(const Tile *tiles, int64_t t, int64_t &I
 // loops read only LDS and registers, apart from the row values z_r, whose
 // load is issued ahead of each slice's GEMM1.
 // ---------------------------------------------------------------------------
+// LDS pitch of the staged column covariates XJ: GEMM1 reads XJ[(cbase + lr)
+// XP + lk + 4 kk] with ds_read_b64, whose 32-lane halves conflict unless the
+// 16 rows lr land on distinct 4-bank groups, i.e. XP = 2 (mod 4)
+// (ACE_XJ_PAD=1; 0, the default: the dense PM + 1 pitch, 2-way conflicts for
+// odd PM + 1).  Measured neutral at C2 (gradient 4.80 / 4.81 ms, assembly
+// 2.35 / 2.35 ms, profiles/r03_grad_ab.txt): the kernels are bound by the
+// fp64 dependency chains, not by LDS.
+#ifndef ACE_XJ_PAD
+#define ACE_XJ_PAD 0
+#endif
+__host__ __device__ constexpr int xj_pitch(int PM) {
+  return ACE_XJ_PAD ? PM + 1 + ((6 - (PM + 1) % 4) % 4) : PM + 1;
+}
+
 struct MmLayout {
   int etab, xj, xi, z, lz, nc, nr, w, red, red_slices, rv, total;
 };
@@ -291,7 +305,7 @@ __host__ __device__ inline MmLayout mm_layout(int PM, int B, int KIND, bool grad
   o.etab = off;
   off += 32;
   o.xj = off;
-  off += 64 * (PM + 1);
+  off += 64 * xj_pitch(PM);
   o.xi = off;
   if (grad && PM <= 32) off += 64 * (PM + 1);
   o.z = off;  // row 0: slice 0's unit basis factors, rows 1..B-1: Z
@@ -327,7 +341,7 @@ __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS
                                           const double *__restrict__ wk,
                                           const double *__restrict__ wlast, int64_t R0,
                                           int64_t C0, int tid) {
-  constexpr int XP = PM + 1;
+  constexpr int XP = xj_pitch(PM);
   const MmLayout o = mm_layout(PM, B, KIND, GRAD, NT / 64);
   const int NS = (GRAD && KIND == 1) ? B + 1 : B;
   constexpr bool XI = GRAD && PM <= 32;
@@ -495,7 +509,7 @@ __global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 32 ? 3 : 2)) v
   const int64_t R0 = I * AT, C0 = J * AT, n = S.n;
   const int rl = 16 * wr + lr;
   const int64_t r = R0 + rl;
-  constexpr int XP = PM + 1;
+  constexpr int XP = xj_pitch(PM);
   const MmLds L = mm_stage<PM, KIND, false, ASM_NT>(lds, S, B, ZS, tab.wk, tab.wk, R0, C0, tid);
   RowX<PM> xr;
   xr.load(S.X + r * PM, lk);
@@ -648,7 +662,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
     const Tile *__restrict__ tiles, int G, int64_t t0) {
   constexpr int NT = 64 * 4 * (4 / CB);      // threads
   constexpr int NWV = NT / 64;               // waves
-  constexpr int XP = PM + 1;
+  constexpr int XP = xj_pitch(PM);
   constexpr bool XIL = PM <= 32;             // row covariates staged in LDS
   constexpr int NV = PM + 1;
   constexpr int NQ = (PM + 15) / 16;         // GEMM2 16-wide column blocks

@@ -453,13 +453,15 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
   auto zsize = [&](int g) { return std::min(2, steps - 2 * g); };
   std::vector<ShardSweep> v;
   for (auto &R : m.ranks) v.push_back(sweep_view(m, *R, which));
-  // events: [0] inputs, ready(g) 1.., bulkdone(g) 1+ng.., side2 start / done
+  // events: [0] inputs, ready(g) 1.., bulkdone(g) 1+ng.., side2 start / done,
+  // [4 ng + 1] the assembly done
   auto EV = [&](int i) { return m.ev[(size_t)i]; };
   const int E_IN = 0;
   auto E_READY = [&](int g) { return 1 + g; };
   auto E_BULK = [&](int g) { return 1 + ng + g; };
   auto E_S2A = [&](int g) { return 1 + 2 * ng + g; };
   auto E_S2B = [&](int g) { return 1 + 3 * ng + g; };
+  const int E_ASM = 1 + 4 * ng;  // the whole assembly (part 2 included) done
   auto rec = [&](int i, hipStream_t s_) { ck(ctx, hipEventRecord(EV(i), s_), "event"); };
   auto wait = [&](hipStream_t s_, int i) { ck(ctx, hipStreamWaitEvent(s_, EV(i), 0), "event wait"); };
   auto prepare = [&](int k) {  // panel k into slot k & 3, on `side`
@@ -483,6 +485,7 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
   prepare(1);
   rec(E_READY(0), side);
   m.upd_used = 0;
+  rec(E_ASM, st);  // group 1's cross tiles include assembly part-2 tiles
   for (int g = 0; g < ng; ++g) {
     const int ka = 2 * g;
     const bool more = g + 1 < ng;
@@ -513,7 +516,7 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
     if (!more) break;
     // side path of group g + 1 (its cross tiles were last touched by bulk g-1)
     const int kb = ka + 2;  // first block of group g + 1
-    if (g > 0) wait(side, E_BULK(g - 1));
+    wait(side, g > 0 ? E_BULK(g - 1) : E_ASM);
     const bool two = zsize(g + 1) == 2;
     if (two) {  // block kb + 1's share of the pair cross on side2, concurrently
       rec(E_S2A(g + 1), side);
@@ -637,8 +640,8 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
     m->ranks.push_back(std::move(R));
   }
   // lookahead events: the step schedule's 2 steps + 1, the pair schedule's
-  // 4 ngroups + 1
-  m->ev.assign((size_t)std::max(2 * steps + 1, 4 * ((steps + 1) / 2) + 1), nullptr);
+  // 4 ngroups + 2
+  m->ev.assign((size_t)std::max(2 * steps + 1, 4 * ((steps + 1) / 2) + 2), nullptr);
   for (auto &e : m->ev) ck(ctx, hipEventCreateWithFlags(&e, ACE_SYNC_EVENT_FLAGS), "event");
   m->ev_upd.assign((size_t)(2 * steps), nullptr);
   m->upd_flops.assign((size_t)steps, 0.0);
