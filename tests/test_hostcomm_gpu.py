@@ -97,13 +97,15 @@ def test_sharded_processes_match_single_gpu_and_oracle(A, O, tmp_path, world, ki
     th1 = r["theta1"].copy()
     th1[1] = 0.0  # para_update(1) overwrote theta[1] with mu: restart from the input
     g1, st1, mu1 = m.para_update(1, th1)
-    close(th1, r["theta1"], 1e-8, 1e-12)
-    close(g1, r["g1"], 1e-8, 1e-9)
-    close(st1, r["st1"], 1e-8, 1e-9)
-    assert mu1 == pytest.approx(float(r["mu1"][0]), rel=1e-8)
+    # the sharded sweep's operand order differs from the single GPU's (R = Pn,
+    # C = W): gradient and stats agree to 1e-9
+    close(th1, r["theta1"], 1e-9, 1e-12)
+    close(g1, r["g1"], 1e-9, 1e-11)
+    close(st1, r["st1"], 1e-9, 1e-12)
+    assert mu1 == pytest.approx(float(r["mu1"][0]), rel=1e-9)
     g2, st2, _ = m.para_update(2, r["theta2"].copy())
-    close(g2, r["g2"], 1e-8, 1e-9)
-    close(st2, r["st2"], 1e-8, 1e-9)
+    close(g2, r["g2"], 1e-9, 1e-11)
+    close(st2, r["st2"], 1e-9, 1e-12)
     # the sharded sweep forms W with the operands swapped:
     # inverse entries agree to a few 1e-9 of the largest one
     close(m.apply_inverse(r["V"]), r["AinvV"], 1e-7, 1e-8)
