@@ -1,3 +1,5 @@
+# Handle-path (unchanged R6 sequence) GPU tests, then the bench with the
+# round-3 direct path (ACE_DMAT_DIRECT=1) against the round-2 one (0).
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_r6_handles_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/r6t.log 2>&1 || { tail -30 gpurun_out/r6t.log; exit 1; }

@@ -1,3 +1,5 @@
+# Sharded GPU tests, the 1-rank pair-schedule A/B (tools/ab_shard_pair.sh)
+# and a rocprofv3 kernel trace of one sharded C2 run (tools/shard_trace.py).
 set -o pipefail
 mkdir -p gpurun_out/shp
 timeout -k 10 600 python -u -m pytest tests/test_shard_gpu.py tests/test_hostcomm_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/shp/tests.log 2>&1 || { tail -30 gpurun_out/shp/tests.log; exit 1; }
