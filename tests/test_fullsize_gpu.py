@@ -220,3 +220,28 @@ def test_c2_fullsize_predict_against_torch(A, tmp_path):
             assert want < tol, (k, want, tol)
         else:
             assert abs(gm[k]["var"] - max(want, 0.0)) <= tol, (k, gm[k]["var"], want, tol)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("cfg,seed", [("C1", 1100), ("C3", 3300)])
+def test_single_gpu_fullsize_against_torch(A, tmp_path, cfg, seed):
+    """The other BASELINE configurations on one GPU against the same
+    independent torch fp64 restatement as C2: C1 (n = 4096, d = 10, SE,
+    B = 6) and C3 (n = 32768, d = 32, SE, B = 12 -- its A fits one MI355X;
+    the 4-rank sharded model is compared with this single-GPU model in
+    test_c3_fullsize_sharded4_matches_single).  Iteration 1 (the mu_solution
+    overwrite, Q4) and 2; gradient / stats 1e-6 relative (north star), the
+    RMSE against the reference's explicit residual."""
+    kernel, n, p, B, y, X, Z, th, sy = _problem(cfg, seed=seed)
+    m = A.DeviceModel(kernel, n, p, B)
+    m.set_data(y, X, Z, sy)
+    for it in (1, 2):
+        t = th.copy() if it == 1 else th + 0.03
+        t0 = t.copy()
+        g, st, _ = m.para_update(it, t)
+        ref = _torch_reference(tmp_path, kernel, y, X, Z, t0, sy, it)
+        if it == 1:
+            assert t[1] == pytest.approx(float(ref["mu"]), rel=1e-7, abs=1e-10)
+        close(g, ref["grad"])
+        assert st[1] == pytest.approx(float(ref["stats"][1]), rel=1e-9)
+        assert abs(st[0] - ref["stats"][0]) / ref["stats"][0] < 1e-6
