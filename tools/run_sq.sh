@@ -10,6 +10,6 @@ for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA 
             "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_TRANS_F64" \
             "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_MFMA_F64 SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_ACTIVE_INST_SCA"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $pass --output-format csv -d $out/p$i -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --no-cpu-baseline "${@:2}" > $out/p$i.log 2>&1 || exit 1
+  timeout -s KILL 90 rocprofv3 --pmc $pass --output-format csv -d $out/p$i -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-r6 "${@:2}" > $out/p$i.log 2>&1 || exit 1
 done
 python3 $GRAFT_REPO_ROOT/tools/sq_counters.py $out/p1 $out/p2 $out/p3 | tee $out/sq.txt
