@@ -240,14 +240,17 @@ hipError_t shard_unpack_chain(const ShardSweep &b, int k, int buf, hipStream_t s
 hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t st);
 // every own tile except the cross of block kx (kx < 0: none)
 hipError_t shard_update_main(const ShardSweep &b, int k, int buf, int kx, hipStream_t st);
-// step k with panel slot `slot` on a tile list (skip rule kx as k_update)
+// step k with panel slot `slot` on a tile list (skip rule kx as k_update);
+// kpack >= 0: the launch also writes the exchange buffers of step kpack
+// (what shard_pack(kpack) would copy) from the values it stores -- the list
+// must then hold every own tile with I or J in block kpack
 hipError_t shard_update_tiles(const ShardSweep &b, int k, int slot, int kx, const Tile *tiles,
-                              int64_t nt, hipStream_t st);
+                              int64_t nt, hipStream_t st, int kpack = -1);
 // steps ka, ka + 1 in one launch (k_update_pair, panels in slots ka & 3 and
 // (ka + 1) & 3, operands swapped: R = Pn, C = W) on a tile list, skipping the
-// tiles with I or J in blocks [kx0, kx1)
+// tiles with I or J in blocks [kx0, kx1); kpack as shard_update_tiles
 hipError_t shard_update_pair(const ShardSweep &b, int ka, int kx0, int kx1, const Tile *tiles,
-                             int64_t nt, hipStream_t st);
+                             int64_t nt, hipStream_t st, int kpack = -1);
 
 // ---- small helpers -----------------------------------------------------------
 // AUG rows of columns j < n: row 0 = y (zeros if y is null), row 1 = 1

@@ -368,6 +368,14 @@ void allreduce(ShardModel &m, int which, int64_t count, hipStream_t st) {
 }
 
 // ---- the sharded sweep -------------------------------------------------------
+bool fuse_pack() {
+  static const bool v = [] {
+    const char *e = getenv("ACE_FUSE_PACK");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+
 // One step per update launch, lookahead only over RCCL (ACE_PAIR=0: the
 // round-2 schedule, kept for A/B and for npad < 2 NB).
 void run_sweep_sharded_steps(ShardModel &m, int which, bool timed) {
@@ -464,8 +472,12 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
   const int E_ASM = 1 + 4 * ng;  // the whole assembly (part 2 included) done
   auto rec = [&](int i, hipStream_t s_) { ck(ctx, hipEventRecord(EV(i), s_), "event"); };
   auto wait = [&](hipStream_t s_, int i) { ck(ctx, hipStreamWaitEvent(s_, EV(i), 0), "event wait"); };
-  auto prepare = [&](int k) {  // panel k into slot k & 3, on `side`
-    for (auto &b : v) ck(ctx, shard_pack(b, k, side), "shard pack");
+  // the cross launch that finalises block k's tiles also writes the exchange
+  // buffers of step k (ACE_FUSE_PACK=0: separate k_pack_* launches)
+  const bool fuse = fuse_pack();
+  auto prepare = [&](int k, bool packed) {  // panel k into slot k & 3, on `side`
+    if (!packed)
+      for (auto &b : v) ck(ctx, shard_pack(b, k, side), "shard pack");
     exchange(m, k, side);
     for (auto &b : v) ck(ctx, shard_unpack_chain(b, k, k & 3, side), "shard panel");
   };
@@ -473,16 +485,17 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
     for (size_t j = 0; j < v.size(); ++j) {
       RankState &R = *m.ranks[j];
       const int64_t x0 = R.xoff[(size_t)k], nx = R.xoff[(size_t)k + 1] - x0;
-      ck(ctx, shard_update_tiles(v[j], k, k & 3, -1, (const Tile *)R.tx.p + x0, nx, side),
+      ck(ctx, shard_update_tiles(v[j], k, k & 3, -1, (const Tile *)R.tx.p + x0, nx, side,
+                                 fuse ? k + 1 : -1),
          "shard cross update");
     }
   };
   // E_IN: recorded by shard_eval after the first two panels' columns, the
   // AUG rows and the flag (the rest of the assembly runs on under prepare(0))
   wait(side, E_IN);
-  prepare(0);
+  prepare(0, false);
   single_cross(0);
-  prepare(1);
+  prepare(1, fuse);
   rec(E_READY(0), side);
   m.upd_used = 0;
   rec(E_ASM, st);  // group 1's cross tiles include assembly part-2 tiles
@@ -532,14 +545,15 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
     for (size_t j = 0; j < v.size(); ++j) {
       RankState &R = *m.ranks[j];
       const int64_t p0 = R.poff[(size_t)(2 * (g + 1))], np = R.poff[(size_t)(2 * (g + 1) + 1)] - p0;
-      ck(ctx, shard_update_pair(v[j], ka, -1, -1, (const Tile *)R.tp.p + p0, np, side),
+      ck(ctx, shard_update_pair(v[j], ka, -1, -1, (const Tile *)R.tp.p + p0, np, side,
+                                fuse ? kb : -1),
          "shard pair cross");
     }
-    prepare(kb);
+    prepare(kb, fuse);
     if (two) {
       wait(side, E_S2B(g + 1));
       single_cross(kb);
-      prepare(kb + 1);
+      prepare(kb + 1, fuse);
     }
     rec(E_READY(g + 1), side);
   }

@@ -586,14 +586,39 @@ __device__ __forceinline__ double ld_a(const double *p) { return __builtin_nonte
 struct GatherOut {
   double *P, *W, *S0;
   int64_t k0, ldp;
+  // pack mode (sharded, low != null): instead of P / W / S0, write what
+  // shard_pack would read back for the exchange of step k0 / NB -- the
+  // owner's column block rows >= k0 into low (ld h, the pivot block's upper
+  // part mirrored) and the rank's row pieces A[k-block, j-block], j < k,
+  // into send (slot = local block index)
+  double *low = nullptr, *send = nullptr;
+  int64_t h = 0;
+  int G = 1;
 };
 static inline GatherOut no_gather() { return GatherOut{nullptr, nullptr, nullptr, -1, 0}; }
+static inline GatherOut pack_out(double *low, double *send, int64_t k0, int64_t naug, int G) {
+  GatherOut g{nullptr, nullptr, nullptr, k0, 0};
+  g.low = low;
+  g.send = send;
+  g.h = naug - k0;
+  g.G = G;
+  return g;
+}
 
 // the value v stored at lower position (r, c) of A (r >= c; entries above
 // the diagonal of a diagonal tile are not part of the lower storage)
 __device__ __forceinline__ void gput(const GatherOut &g, int64_t r, int64_t c, double v) {
   if (r < c) return;
   const int64_t cc = c - g.k0, rr = r - g.k0;
+  if (g.low) {  // pack mode (k_pack_lower / k_pack_rows layouts)
+    if ((uint64_t)cc < (uint64_t)NB) {  // column block k: rows >= k0 (r >= c >= k0)
+      g.low[rr + cc * g.h] = v;
+      if ((uint64_t)rr < (uint64_t)NB && r != c) g.low[cc + rr * g.h] = v;  // mirror
+    } else if ((uint64_t)rr < (uint64_t)NB) {  // row block k, an own column c < k0
+      g.send[(lcol(c, g.G) / NB) * NB * NB + rr + (c % NB) * NB] = v;
+    }
+    return;
+  }
   if ((uint64_t)cc < (uint64_t)NB) {  // column block kg: row r of the panel
     g.P[r + cc * g.ldp] = -v;
     if ((uint64_t)rr < (uint64_t)NB) {
@@ -613,9 +638,18 @@ __device__ __forceinline__ void gput(const GatherOut &g, int64_t r, int64_t c, d
 // the AUG row block's dead rows (16 .. 127: zero padding, not computed):
 // k_gather copies them too
 __device__ __forceinline__ void gput_aug_dead(const GatherOut &g, const double *A, int64_t ld,
-                                              int64_t R0, int64_t C0, int tid, int nthr) {
+                                              int64_t R0, int64_t C0, int tid, int nthr,
+                                              int64_t L0 = -1) {
   const int64_t cc0 = C0 - g.k0;
   if ((uint64_t)cc0 >= (uint64_t)NB) return;
+  if (g.low) {  // pack mode: the dead AUG rows of column block k (zeros) into low
+    const int64_t lc0 = L0 >= 0 ? L0 : C0;
+    for (int e = tid; e < (UT - 16) * UT; e += nthr) {
+      const int a = 16 + e % (UT - 16), c = e / (UT - 16);
+      g.low[(R0 + a - g.k0) + (cc0 + c) * g.h] = A[(R0 + a) + (lc0 + c) * ld];
+    }
+    return;
+  }
   for (int e = tid; e < (UT - 16) * UT; e += nthr) {
     const int a = 16 + e % (UT - 16), c = e / (UT - 16);
     g.P[(R0 + a) + (cc0 + c) * g.ldp] = -A[(R0 + a) + (C0 + c) * ld];
@@ -717,7 +751,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
     if (go.k0 >= 0) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) gput(go, r, C0 + 16 * wv + lk + 4 * j, acc[j]);
-      gput_aug_dead(go, A, ld, R0, C0, tid, UTHREADS);
+      gput_aug_dead(go, A, ld, R0, C0, tid, UTHREADS, L0);
     }
     return;
   }
@@ -972,7 +1006,7 @@ __device__ __forceinline__ void update_pair_tile(
     if (go.k0 >= 0) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) gput(go, r, c + 4 * j, acc[j]);
-      gput_aug_dead(go, A, ld, R0, C0, tid, UTHREADS);
+      gput_aug_dead(go, A, ld, R0, C0, tid, UTHREADS, L0);
     }
     return;
   }
@@ -1979,20 +2013,24 @@ hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t s
 }
 
 hipError_t shard_update_tiles(const ShardSweep &b, int k, int slot, int kx, const Tile *tiles,
-                              int64_t nt, hipStream_t st) {
+                              int64_t nt, hipStream_t st, int kpack) {
+  const GatherOut go = kpack >= 0 ? pack_out(b.low, b.send, (int64_t)kpack * NB, b.ld, b.G)
+                                  : no_gather();
   if (nt > 0)
     hipLaunchKernelGGL(k_update, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld, b.P[slot],
-                       b.W[slot], b.W[slot], b.ld, (int64_t)k * NB, kx, tiles, b.G, no_gather());
+                       b.W[slot], b.W[slot], b.ld, (int64_t)k * NB, kx, tiles, b.G, go);
   return hipGetLastError();
 }
 
 hipError_t shard_update_pair(const ShardSweep &b, int ka, int kx0, int kx1, const Tile *tiles,
-                             int64_t nt, hipStream_t st) {
+                             int64_t nt, hipStream_t st, int kpack) {
   const int sa = ka & 3, sb = (ka + 1) & 3;
+  const GatherOut go = kpack >= 0 ? pack_out(b.low, b.send, (int64_t)kpack * NB, b.ld, b.G)
+                                  : no_gather();
   if (nt > 0)
     hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld, b.P[sa],
-                       b.W[sa], b.P[sb], b.W[sb], b.ld, (int64_t)ka * NB, kx0, kx1, tiles,
-                       no_gather(), -1, nullptr, b.G, 1);
+                       b.W[sa], b.P[sb], b.W[sb], b.ld, (int64_t)ka * NB, kx0, kx1, tiles, go,
+                       -1, nullptr, b.G, 1);
   return hipGetLastError();
 }
 

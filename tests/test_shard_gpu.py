@@ -163,7 +163,9 @@ def test_sharded_pair_schedule_is_bitwise_neutral(tmp_path, world, n):
     """The sharded sweep's pair-step lookahead schedule (two steps per bulk
     launch, second side stream, single-step cross on 128-tiles; ACE_PAIR=1,
     default) and the one-step schedule (ACE_PAIR=0) give bit-identical
-    results: every tile sees the same MFMA chains in the same order.  n
+    results: every tile sees the same MFMA chains in the same order; and so
+    does the exchange packing fused into the cross launches (default)
+    against separate pack launches (ACE_FUSE_PACK=0).  n
     gives 8, 7 (an odd last group) and 9 sweep steps; the simulated group
     runs the lookahead with all ranks on the shared streams."""
     import os
@@ -171,11 +173,13 @@ def test_sharded_pair_schedule_is_bitwise_neutral(tmp_path, world, n):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
-    for v in ("0", "1"):
+    variants = {"step": {"ACE_PAIR": "0"}, "pair": {"ACE_FUSE_PACK": "0"}, "fused": {}}
+    for v, extra in variants.items():
         out = str(tmp_path / f"s{v}.npz")
-        env = dict(os.environ, ACE_PAIR=v)
+        env = dict(os.environ, **extra)
         subprocess.run([sys.executable, "-c", _SCHED.format(root=root, n=n, world=world, out=out)],
                        env=env, check=True, timeout=100)
         outs[v] = np.load(out)
-    for k in ("g1", "s1", "g2", "s2", "inv"):
-        assert np.array_equal(outs["0"][k], outs["1"][k]), k
+    for v in ("pair", "fused"):
+        for k in ("g1", "s1", "g2", "s2", "inv"):
+            assert np.array_equal(outs["step"][k], outs[v][k]), (v, k)
