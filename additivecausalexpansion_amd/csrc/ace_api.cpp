@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -734,10 +735,25 @@ int ace_model_set_data(ace_model *m, const double *y, const double *X, const dou
   ACE_CATCH
 }
 
+#ifdef ACE_HOST_TRACE
+// diagnostic builds only (tools/build_variant.sh TAG -DACE_HOST_TRACE): host
+// timestamps of one para_update on stderr -- entry, enqueue done, results
+// synchronised, exit -- and the time since the previous call's exit
+static double host_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+static double g_ht_exit = 0.0;
+#define ACE_HT(name) const double name = host_us()
+#else
+#define ACE_HT(name)
+#endif
+
 int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, double *stats,
                           double *mu_post) {
   if (!m) return ACE_ERR_ARG;
   ace_ctx *ctx = m->ctx;
+  ACE_HT(t_in);
   ACE_TRY
   int stop = (ctx->poll && ctx->poll(ctx->poll_user)) ? 1 : 0;
   // sharded over RCCL: every rank votes (also ranks without a poll), so that
@@ -761,6 +777,7 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, d
     if (timed) shard_collect_timing(m->shard, m->t_ms, m->t_launch, m->t_work);
   } else {
     model_pipeline(m, m->sw, theta, iter == 1 ? 1 : 0, timed);
+    ACE_HT(t_enq);
     // the previous timed evaluation's events completed before its results
     // were read: read them back while this evaluation runs
     if (m->pend >= 0) {
@@ -784,6 +801,11 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, d
       m->pend = m->tset;
       m->tset ^= 1;
     }
+#ifdef ACE_HOST_TRACE
+    const double t_sync = host_us();
+    fprintf(stderr, "ace_host_trace it %d: since last exit %.1f us, enqueue %.1f us, wait %.1f us\n",
+            iter, g_ht_exit > 0 ? t_in - g_ht_exit : -1.0, t_enq - t_in, t_sync - t_enq);
+#endif
   }
   m->has_inverse = true;
   if (iter == 1) theta[1] = scal[3];  // mean_solution before the gradient (R/kernel_SE_R6.R:45)
@@ -797,6 +819,9 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, d
     stats[0] = stats[1] = kNaN;
     if (mu_post) *mu_post = kNaN;
   }
+#ifdef ACE_HOST_TRACE
+  g_ht_exit = host_us();
+#endif
   return ACE_OK;
   ACE_CATCH
 }

@@ -215,7 +215,7 @@ double update_gemm_tiles(int64_t naug, int64_t k0, int kx, bool look);
 
 // ---- sharded sweep (one rank's view; ace_shard.cpp drives the steps) --------
 // Step k on rank r:  shard_pack -> [exchange: broadcast `low` from rank k%G,
-// all-gather `send` -> `recv`] -> shard_unpack_chain (panel k on every rank,
+// all-gather recv slot r -> recv] -> shard_unpack_chain (panel k on every rank,
 // pivot chain run redundantly, W for the rows r consumes) -> updates.
 struct ShardSweep {
   double *A;          // local column blocks, naug x (nloc * NB), ld = naug
@@ -228,22 +228,25 @@ struct ShardSweep {
   double *piv;        // npad pivots (every rank records all of them)
   int *flag;
   double *low;        // (naug - k0) x NB broadcast block
-  double *send;       // shard_row_slots(k, G) x NB x NB own row pieces
-  double *recv;       // G x shard_row_slots(k, G) x NB x NB
+  double *recv;       // G x shard_row_slots(k, G) x NB x NB; slot r holds the own
+                      // row pieces (the in-place all-gather operand)
   const Tile *tiles;  // own 128-tiles (row-major lower), device
   int64_t ntiles;
 };
 int shard_row_slots(int k, int G);
 hipError_t shard_pack(const ShardSweep &b, int k, hipStream_t st);
-hipError_t shard_unpack_chain(const ShardSweep &b, int k, int buf, hipStream_t st);
+// own_done: the packing cross launch already wrote the rank's own panel rows
+hipError_t shard_unpack_chain(const ShardSweep &b, int k, int buf, hipStream_t st,
+                              bool own_done = false);
 // cross tiles of block k+1 with panel k (buffer buf)
 hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t st);
 // every own tile except the cross of block kx (kx < 0: none)
 hipError_t shard_update_main(const ShardSweep &b, int k, int buf, int kx, hipStream_t st);
 // step k with panel slot `slot` on a tile list (skip rule kx as k_update);
 // kpack >= 0: the launch also writes the exchange buffers of step kpack
-// (what shard_pack(kpack) would copy) from the values it stores -- the list
-// must then hold every own tile with I or J in block kpack
+// (what shard_pack(kpack) would copy; G > 1) and the rank's own rows of panel
+// kpack (slot kpack & 3) from the values it stores -- the list must then hold
+// every own tile with I or J in block kpack
 hipError_t shard_update_tiles(const ShardSweep &b, int k, int slot, int kx, const Tile *tiles,
                               int64_t nt, hipStream_t st, int kpack = -1);
 // steps ka, ka + 1 in one launch (k_update_pair, panels in slots ka & 3 and

@@ -31,6 +31,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstring>
 #include <memory>
 #include <stdexcept>
 
@@ -136,7 +137,7 @@ void host_allreduce(ace_ctx *ctx, const ace_comm_ops &o, double *dbuf, size_t co
 struct RankState {
   int r = 0;
   DBuf A[2];  // A[1]: train_stats scratch (keeps A[0]'s inverse, Q6)
-  DBuf P[4], W[4], SW, S[2], piv, flag, low, send, recv;  // panel slots k & 3
+  DBuf P[4], W[4], SW, S[2], piv, flag, low, recv;  // panel slots k & 3
   DBuf tupd, tasm, tgrad;  // device tile lists
   int64_t nupd = 0, nasm = 0, nasm1 = 0, ngrad = 0, ndiag = 0;  // nasm1: first-part tiles
   std::vector<Tile> hupd;  // host copy (flop accounting)
@@ -173,6 +174,7 @@ struct ShardModel {
   std::vector<double> upd_flops;
   hipEvent_t ev_asm[2] = {nullptr, nullptr}, ev_grad[2] = {nullptr, nullptr};
   int upd_used = 0;
+  PinnedBuf hio;  // [tables | gsum | sums | scal | one flag per local rank] host staging
   ~ShardModel() {
     for (auto e : ev) (void)hipEventDestroy(e);
     for (auto e : ev_upd) (void)hipEventDestroy(e);
@@ -217,7 +219,6 @@ ShardSweep sweep_view(const ShardModel &m, RankState &R, int which) {
   b.piv = R.piv.d();
   b.flag = R.flag.i();
   b.low = R.low.d();
-  b.send = R.send.d();
   b.recv = R.recv.d();
   b.tiles = reinterpret_cast<const Tile *>(R.tupd.p);
   b.ntiles = R.nupd;
@@ -306,15 +307,18 @@ void build_cross_lists(ace_ctx *ctx, RankState &R, int64_t naug, int steps, int 
 // Panel exchange of step k on stream st.
 void exchange(ShardModel &m, int k, hipStream_t st) {
   ace_ctx *ctx = m.ctx;
+  if (m.G == 1) return;  // one rank: both collectives are the identity
   const int64_t k0 = (int64_t)k * NB;
   const size_t nlow = (size_t)((m.naug - k0) * NB);
   const int slots = shard_row_slots(k, m.G);
   const size_t nrow = (size_t)slots * NB * NB;
   const int root = k % m.G;
+  // the all-gather operand of rank r is slot r of recv (in place)
+  auto own = [&](RankState &R) { return R.recv.d() + (size_t)R.r * nrow; };
   if (m.host) {
     RankState &R = *m.ranks[0];
     host_bcast(ctx, m.ops, R.low.d(), nlow, root, st);
-    if (nrow > 0) host_allgather(ctx, m.ops, R.send.d(), R.recv.d(), nrow, m.G, st);
+    if (nrow > 0) host_allgather(ctx, m.ops, own(R), R.recv.d(), nrow, m.G, st);
     return;
   }
   if (!m.sim) {
@@ -323,8 +327,7 @@ void exchange(ShardModel &m, int k, hipStream_t st) {
     nck(ctx, rccl().Broadcast(R.low.p, R.low.p, nlow, ncclDouble, root, m.comm, st),
         "ncclBroadcast");
     if (nrow > 0)
-      nck(ctx, rccl().AllGather(R.send.p, R.recv.p, nrow, ncclDouble, m.comm, st),
-          "ncclAllGather");
+      nck(ctx, rccl().AllGather(own(R), R.recv.p, nrow, ncclDouble, m.comm, st), "ncclAllGather");
     nck(ctx, rccl().GroupEnd(), "ncclGroupEnd");
     return;
   }
@@ -336,9 +339,10 @@ void exchange(ShardModel &m, int k, hipStream_t st) {
          "sim broadcast");
     if (nrow > 0)
       for (auto &Sp : m.ranks)
-        ck(ctx, hipMemcpyAsync(R.recv.d() + (size_t)Sp->r * nrow, Sp->send.p, nrow * sizeof(double),
-                               hipMemcpyDeviceToDevice, st),
-           "sim all-gather");
+        if (Sp->r != R.r)
+          ck(ctx, hipMemcpyAsync(R.recv.d() + (size_t)Sp->r * nrow, own(*Sp), nrow * sizeof(double),
+                                 hipMemcpyDeviceToDevice, st),
+             "sim all-gather");
   }
 }
 
@@ -346,6 +350,7 @@ void exchange(ShardModel &m, int k, hipStream_t st) {
 // (0: augvec, 1: red).
 void allreduce(ShardModel &m, int which, int64_t count, hipStream_t st) {
   ace_ctx *ctx = m.ctx;
+  if (m.G == 1) return;  // one rank: the identity
   auto buf = [&](RankState &R) { return which == 0 ? R.augvec.d() : R.red.d(); };
   if (m.host) {
     host_allreduce(ctx, m.ops, buf(*m.ranks[0]), (size_t)count, 0, st);
@@ -357,7 +362,6 @@ void allreduce(ShardModel &m, int which, int64_t count, hipStream_t st) {
         "ncclAllReduce");
     return;
   }
-  if (m.G == 1) return;
   double *acc = buf(*m.ranks[0]);
   for (size_t j = 1; j < m.ranks.size(); ++j)
     ck(ctx, launch_add(buf(*m.ranks[j]), acc, count, st), "sim all-reduce");
@@ -479,7 +483,7 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
     if (!packed)
       for (auto &b : v) ck(ctx, shard_pack(b, k, side), "shard pack");
     exchange(m, k, side);
-    for (auto &b : v) ck(ctx, shard_unpack_chain(b, k, k & 3, side), "shard panel");
+    for (auto &b : v) ck(ctx, shard_unpack_chain(b, k, k & 3, side, packed), "shard panel");
   };
   auto single_cross = [&](int k) {  // cross of block k + 1 with panel k, on `side`
     for (size_t j = 0; j < v.size(); ++j) {
@@ -619,7 +623,6 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
     alloc(ctx, R->piv, (size_t)npad * sizeof(double), "alloc piv");
     alloc(ctx, R->flag, 16, "alloc flag");
     alloc(ctx, R->low, (size_t)(naug * NB) * sizeof(double), "alloc exchange");
-    alloc(ctx, R->send, (size_t)std::max(1, maxslots) * NB * NB * sizeof(double), "alloc exchange");
     alloc(ctx, R->recv, (size_t)world * std::max(1, maxslots) * NB * NB * sizeof(double),
           "alloc exchange");
     R->hupd = own_tiles(naug / UT, UT, world, R->r);
@@ -704,16 +707,19 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
   const int64_t naug = m->naug, npad = m->npad, n = m->n;
   std::vector<double> tab = make_tab(theta, s);
   const double sig = std::exp(theta[0]);
+  // pinned staging, async on the stream: the previous evaluation's results
+  // were synchronised before this one started, so the region is free
+  const size_t nl = m->ranks.size();
+  double *h = m->hio.ensure(ctx, tab.size() + (size_t)(ncol + 1) + 4 + 5 + nl);
+  std::copy(tab.begin(), tab.end(), h);
   for (auto &R : m->ranks) {
     if (which == 1) {
       alloc(ctx, R->A[1], R->A[0].bytes, "alloc local A (train stats)");
       ck(ctx, hipMemsetAsync(R->A[1].p, 0, R->A[1].bytes, st), "memset A");
     }
-    ck(ctx, hipMemcpyAsync(R->tab.p, tab.data(), tab.size() * sizeof(double),
-                           hipMemcpyHostToDevice, st),
+    ck(ctx, hipMemcpyAsync(R->tab.p, h, tab.size() * sizeof(double), hipMemcpyHostToDevice, st),
        "upload tables");
   }
-  ck(ctx, hipStreamSynchronize(st), "sync tables");  // pageable source
   // assembly (own tiles) + AUG rows: the first two panels' columns, the
   // AUG rows and the flag, then (the sweep's first side path may start) the rest
   if (timed) ck(ctx, hipEventRecord(m->ev_asm[0], st), "event");
@@ -766,22 +772,28 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
     ck(ctx, launch_final_sums(R->y.d(), R->scal.d() + 4, R->alpha.d(), nullptr, sig, n,
                               R->piv.d(), npad, R->sums.d(), st),
        "final sums");
+  // into the pinned region behind the tables, one synchronisation
   RankState &R0 = *m->ranks[0];
-  ck(ctx, hipMemcpyAsync(gsum, R0.red.p, (size_t)(ncol + 1) * sizeof(double),
-                         hipMemcpyDeviceToHost, st),
+  double *hg = h + tab.size(), *hs = hg + ncol + 1, *hc = hs + 4, *hf = hc + 5;
+  ck(ctx, hipMemcpyAsync(hg, R0.red.p, (size_t)(ncol + 1) * sizeof(double), hipMemcpyDeviceToHost, st),
      "download gsum");
-  ck(ctx, hipMemcpyAsync(sums, R0.sums.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st),
+  ck(ctx, hipMemcpyAsync(hs, R0.sums.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st),
      "download sums");
-  ck(ctx, hipMemcpyAsync(scal, R0.scal.p, 5 * sizeof(double), hipMemcpyDeviceToHost, st),
+  ck(ctx, hipMemcpyAsync(hc, R0.scal.p, 5 * sizeof(double), hipMemcpyDeviceToHost, st),
      "download scal");
+  for (size_t j = 0; j < nl; ++j)
+    ck(ctx, hipMemcpyAsync(hf + j, m->ranks[j]->flag.p, sizeof(int), hipMemcpyDeviceToHost, st),
+       "download flag");
+  sync(ctx);
+  std::copy(hg, hg + ncol + 1, gsum);
+  std::copy(hs, hs + 4, sums);
+  std::copy(hc, hc + 5, scal);
   *flag = 0;
-  for (auto &R : m->ranks) {
-    int f = 0;
-    ck(ctx, hipMemcpyAsync(&f, R->flag.p, sizeof(int), hipMemcpyDeviceToHost, st), "download flag");
-    ck(ctx, hipStreamSynchronize(st), "sync");
+  for (size_t j = 0; j < nl; ++j) {
+    int f;
+    std::memcpy(&f, hf + j, sizeof(int));
     *flag |= f;
   }
-  sync(ctx);
 }
 
 // Full symmetric inverse (n x n) of the resident A[0] on every rank.  The
@@ -843,7 +855,7 @@ void shard_collect_timing(ShardModel *m, double *t_ms, int64_t *t_launch, double
 // leave the others blocked in the next sweep's collectives.  Simulated
 // groups share the process's poll, so the local value is already common.
 int shard_any(ShardModel *m, int local) {
-  if (m->sim) return local;
+  if (m->sim || m->G == 1) return local;
   ace_ctx *ctx = m->ctx;
   hipStream_t st = ctx->stream;
   if (m->host) {
@@ -871,7 +883,7 @@ int shard_rank_of(const ShardModel *m, int j) { return m->ranks[(size_t)j]->r; }
 // Sum over ranks of `count` doubles (in place, device).  Simulated groups
 // sum their local partials themselves, so only RCCL has work to do.
 void shard_allreduce_sum(ShardModel *m, double *buf, int64_t count) {
-  if (m->sim || count <= 0) return;
+  if (m->sim || m->G == 1 || count <= 0) return;
   if (m->host) {
     host_allreduce(m->ctx, m->ops, buf, (size_t)count, 0, m->ctx->stream);
     return;

@@ -586,20 +586,24 @@ __device__ __forceinline__ double ld_a(const double *p) { return __builtin_nonte
 struct GatherOut {
   double *P, *W, *S0;
   int64_t k0, ldp;
-  // pack mode (sharded, low != null): instead of P / W / S0, write what
-  // shard_pack would read back for the exchange of step k0 / NB -- the
-  // owner's column block rows >= k0 into low (ld h, the pivot block's upper
-  // part mirrored) and the rank's row pieces A[k-block, j-block], j < k,
-  // into send (slot = local block index)
+  // pack mode (sharded, low != null, G > 1): also write what shard_pack
+  // would read back for the exchange of step k0 / NB -- the owner's column
+  // block rows >= k0 into low (ld h, the pivot block's upper part mirrored)
+  // and the rank's row pieces A[k-block, j-block], j < k, into send (slot =
+  // local block index).  P / W / S0 (when set) receive the panel rows the
+  // rank owns, so that shard_unpack_chain only fills the rows of other ranks.
   double *low = nullptr, *send = nullptr;
   int64_t h = 0;
   int G = 1;
 };
 static inline GatherOut no_gather() { return GatherOut{nullptr, nullptr, nullptr, -1, 0}; }
-static inline GatherOut pack_out(double *low, double *send, int64_t k0, int64_t naug, int G) {
-  GatherOut g{nullptr, nullptr, nullptr, k0, 0};
-  g.low = low;
-  g.send = send;
+static inline GatherOut pack_out(double *low, double *send, double *P, double *W, double *S0,
+                                 int64_t k0, int64_t naug, int G) {
+  GatherOut g{P, W, S0, k0, naug};
+  if (G > 1) {
+    g.low = low;
+    g.send = send;
+  }
   g.h = naug - k0;
   g.G = G;
   return g;
@@ -617,8 +621,8 @@ __device__ __forceinline__ void gput(const GatherOut &g, int64_t r, int64_t c, d
     } else if ((uint64_t)rr < (uint64_t)NB) {  // row block k, an own column c < k0
       g.send[(lcol(c, g.G) / NB) * NB * NB + rr + (c % NB) * NB] = v;
     }
-    return;
   }
+  if (!g.P) return;
   if ((uint64_t)cc < (uint64_t)NB) {  // column block kg: row r of the panel
     g.P[r + cc * g.ldp] = -v;
     if ((uint64_t)rr < (uint64_t)NB) {
@@ -636,23 +640,18 @@ __device__ __forceinline__ void gput(const GatherOut &g, int64_t r, int64_t c, d
 }
 
 // the AUG row block's dead rows (16 .. 127: zero padding, not computed):
-// k_gather copies them too
+// k_gather copies them too.  L0: the local column of C0 (sharded).
 __device__ __forceinline__ void gput_aug_dead(const GatherOut &g, const double *A, int64_t ld,
                                               int64_t R0, int64_t C0, int tid, int nthr,
                                               int64_t L0 = -1) {
   const int64_t cc0 = C0 - g.k0;
   if ((uint64_t)cc0 >= (uint64_t)NB) return;
-  if (g.low) {  // pack mode: the dead AUG rows of column block k (zeros) into low
-    const int64_t lc0 = L0 >= 0 ? L0 : C0;
-    for (int e = tid; e < (UT - 16) * UT; e += nthr) {
-      const int a = 16 + e % (UT - 16), c = e / (UT - 16);
-      g.low[(R0 + a - g.k0) + (cc0 + c) * g.h] = A[(R0 + a) + (lc0 + c) * ld];
-    }
-    return;
-  }
+  const int64_t lc0 = L0 >= 0 ? L0 : C0;
   for (int e = tid; e < (UT - 16) * UT; e += nthr) {
     const int a = 16 + e % (UT - 16), c = e / (UT - 16);
-    g.P[(R0 + a) + (cc0 + c) * g.ldp] = -A[(R0 + a) + (C0 + c) * ld];
+    const double v = A[(R0 + a) + (lc0 + c) * ld];
+    if (g.low) g.low[(R0 + a - g.k0) + (cc0 + c) * g.h] = v;
+    if (g.P) g.P[(R0 + a) + (cc0 + c) * g.ldp] = -v;
   }
 }
 
@@ -1337,17 +1336,23 @@ __global__ __launch_bounds__(256) void k_pack_rows(const double *__restrict__ A,
 // Rebuilds panel k on every rank: Pn = -P for every row, W = P on the pivot
 // rows, S0 = pivot rows of sub-block 0 (k_pivot's input).  Rows >= k0 come
 // from the broadcast block, rows i < k0 (block j = i / NB) from all-gather
-// slot (j % G, j / G), transposed: P[i, c] = A[k0 + c, i].
+// slot (j % G, j / G), transposed: P[i, c] = A[k0 + c, i].  skip_own: the
+// rows of rank r's own blocks are already in place (packing cross launch).
 __global__ __launch_bounds__(256) void k_unpack_panel(const double *__restrict__ low,
                                                       const double *__restrict__ recv, int m,
                                                       int G, int64_t k0, int64_t naug,
                                                       double *__restrict__ Pn,
                                                       double *__restrict__ W, int64_t ldp,
-                                                      double *__restrict__ S0) {
+                                                      double *__restrict__ S0, int skip_own,
+                                                      int r) {
   __shared__ double tile[64][65];
   const int64_t i0 = (int64_t)blockIdx.x * 64;
   const int j0 = blockIdx.y * 64;
   const int tid = threadIdx.x;
+  if (skip_own) {  // rows the rank's own (packing) cross launch wrote
+    const int64_t kb = k0 / NB;
+    if (i0 >= k0 ? kb % G == r : (i0 / NB) % G == r) return;
+  }
   if (i0 >= k0) {
     const int64_t h = naug - k0;
     for (int e = tid; e < 4096; e += 256) {
@@ -1983,6 +1988,12 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
 // ---- sharded step pieces (driven by ace_shard.cpp) --------------------------
 int shard_row_slots(int k, int G) { return (k + G - 1) / G; }
 
+// Rank r's all-gather operand of step k lies in place in recv (slot r), so
+// the collective needs no local copy (and none at all for one rank).
+static double *send_of(const ShardSweep &b, int k) {
+  return b.recv + (int64_t)b.r * shard_row_slots(k, b.G) * NB * NB;
+}
+
 hipError_t shard_pack(const ShardSweep &b, int k, hipStream_t st) {
   const int64_t k0 = (int64_t)k * NB, naug = b.ld;
   if (k % b.G == b.r)
@@ -1991,15 +2002,16 @@ hipError_t shard_pack(const ShardSweep &b, int k, hipStream_t st) {
   const int own = k > b.r ? (k - b.r + b.G - 1) / b.G : 0;  // own blocks j < k
   if (own > 0)
     hipLaunchKernelGGL(k_pack_rows, dim3(NB / 64, NB / 64, (unsigned)own), dim3(256), 0, st, b.A,
-                       b.ld, k0, b.send);
+                       b.ld, k0, send_of(b, k));
   return hipGetLastError();
 }
 
-hipError_t shard_unpack_chain(const ShardSweep &b, int k, int buf, hipStream_t st) {
+hipError_t shard_unpack_chain(const ShardSweep &b, int k, int buf, hipStream_t st, bool own_done) {
   const int64_t k0 = (int64_t)k * NB, naug = b.ld;
-  hipLaunchKernelGGL(k_unpack_panel, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st,
-                     b.low, b.recv, shard_row_slots(k, b.G), b.G, k0, naug, b.P[buf], b.W[buf],
-                     b.ld, b.S[0]);
+  if (!(own_done && b.G == 1))
+    hipLaunchKernelGGL(k_unpack_panel, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st,
+                       b.low, b.recv, shard_row_slots(k, b.G), b.G, k0, naug, b.P[buf], b.W[buf],
+                       b.ld, b.S[0], own_done ? 1 : 0, b.r);
   panel_chain(b.P[buf], b.W[buf], b.ld, k0, b.SW, b.S, b.piv, b.flag, b.G, b.r, st);
   return hipGetLastError();
 }
@@ -2014,7 +2026,9 @@ hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t s
 
 hipError_t shard_update_tiles(const ShardSweep &b, int k, int slot, int kx, const Tile *tiles,
                               int64_t nt, hipStream_t st, int kpack) {
-  const GatherOut go = kpack >= 0 ? pack_out(b.low, b.send, (int64_t)kpack * NB, b.ld, b.G)
+  const int sp = kpack & 3;
+  const GatherOut go = kpack >= 0 ? pack_out(b.low, send_of(b, kpack), b.P[sp], b.W[sp], b.S[0],
+                                             (int64_t)kpack * NB, b.ld, b.G)
                                   : no_gather();
   if (nt > 0)
     hipLaunchKernelGGL(k_update, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld, b.P[slot],
@@ -2025,7 +2039,9 @@ hipError_t shard_update_tiles(const ShardSweep &b, int k, int slot, int kx, cons
 hipError_t shard_update_pair(const ShardSweep &b, int ka, int kx0, int kx1, const Tile *tiles,
                              int64_t nt, hipStream_t st, int kpack) {
   const int sa = ka & 3, sb = (ka + 1) & 3;
-  const GatherOut go = kpack >= 0 ? pack_out(b.low, b.send, (int64_t)kpack * NB, b.ld, b.G)
+  const int sp = kpack & 3;
+  const GatherOut go = kpack >= 0 ? pack_out(b.low, send_of(b, kpack), b.P[sp], b.W[sp], b.S[0],
+                                             (int64_t)kpack * NB, b.ld, b.G)
                                   : no_gather();
   if (nt > 0)
     hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld, b.P[sa],

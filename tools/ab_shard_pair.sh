@@ -1,6 +1,6 @@
 # Sharded (1-rank RCCL) rates, same box: one-step schedule (ACE_PAIR=0),
-# pair schedule with the plain own-tile order (ACE_TAIL_SORT=0) and with the
-# cost-sorted per-group bulk orders (default).  Args: configs (default C2).
+# pair schedule with separate pack launches and full unpack (ACE_FUSE_PACK=0) and the
+# default (ACE_X=1 is a no-op switch).  AB_ENVS overrides the list.  Args: configs (default C2).
 set -o pipefail
 mkdir -p gpurun_out/sp
 port=29531
@@ -8,7 +8,7 @@ cfgs=${@:-C2}
 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-r6 > gpurun_out/sp/single.json 2> gpurun_out/sp/single.err || exit 1
 python -c "import json;d=json.load(open('gpurun_out/sp/single.json'));print('single C2', round(d['value'],3), round(d['ms_per_step'],1))"
 for cfg in $cfgs; do
-  for env in "ACE_PAIR=0" "ACE_TAIL_SORT=0" "ACE_X=1"; do
+  for env in ${AB_ENVS:-"ACE_PAIR=0" "ACE_FUSE_PACK=0" "ACE_X=1"}; do
     port=$((port + 1))
     st=3; [ $cfg = C4 ] && st=2
     tag=${cfg}_${env%%=*}
