@@ -411,9 +411,9 @@ int ace_pred_marginal(ace_ctx *ctx, int64_t nX, int64_t nx, int B, const double 
 }  // extern "C"
 
 // A = Kfull + sig I (lower 64-tiles, assembly mode 0) into w.A with the AUG
-// rows [y; 1] (y null: the 1 row only), then the sweep.  The first two
-// panels' columns are assembled first: the sweep's first pivot chains and the
-// cross of block 1 (side stream) then run under the rest of the assembly.
+// rows [y; 1] (y null: the 1 row only), then the sweep.  The first sweep
+// group's panels' columns are assembled first: that group's pivot chains and
+// lookahead crosses (side stream) then run under the rest of the assembly.
 // ev_asm (optional): two timing events around the assembly.
 void assemble_and_sweep(ace_ctx *ctx, SweepWork &w, const Shape &s, const PairSide &ps,
                         const TabView &tv, double sig, const double *y, int64_t n,

@@ -125,8 +125,9 @@ struct SweepBufs {
   double *A;      // Naug x Naug, col-major, ld = Naug, lower triangle used
   int64_t ld;     // Naug
   int64_t npad;   // multiple of NB
-  double *P[4];   // Naug x NB : -panel (negated copy), slot k & 1 (k & 3 with pair steps)
-  double *W[4];   // Naug x NB : panel being swept, same slots; [2], [3] null unless pairs
+  double *P[8];   // Naug x NB : -panel (negated copy), slot k & 1 (k % 2Z with Z steps per group)
+  double *W[8];   // Naug x NB : panel being swept, same slots; [2] .. null unless used
+  int Z = 2;      // steps per bulk launch (sweep_group()); the lists below follow it
   double *SW;     // SW_DOUBLES: 2 SUB x SUB sub-pivot inverses + split-panel chunks
   double *S[2];   // SUB x NB col-major: pivot rows before their sub-sweep (ping-pong)
   double *piv;    // npad pivots
@@ -168,8 +169,16 @@ bool pair_steps();
 // ngroups-1 (each list dealt to the XCDs): [off[2g], off[2g+1]) the lower
 // 128-tiles with I or J in block 2g, [off[2g+1], off[2g+2]) those with I or
 // J in block 2g + 1 and not in block 2g (empty for a one-step group).
-std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t> &off);
+// Z steps per group (sweep_group()): off[2g] .. off[2g+1] the tiles with I
+// or J in the group's first block, off[2g+1] .. off[2g+2] those in its other
+// blocks and not in the first.
+std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t> &off,
+                                   int Z = 2);
 double update_gemm_tiles_pair(int64_t naug, int64_t ka0, int kx0, int kx1);
+// Steps per bulk launch: 2 (k_update_pair, default), ACE_GROUP=3 or 4 selects
+// k_update_multi groups (run_sweep_groups).
+int sweep_group();
+double update_gemm_tiles_group(int64_t naug, int64_t ka0, int npan, int kx0, int kx1);
 // The lower 128-tiles with I or J in block k+1, for k = 0 .. steps-2,
 // concatenated (each step's list dealt to the XCDs like the bulk order);
 // off[k] .. off[k+1] is step k's range.  ACE_XUPD=0 selects k_update_x.
@@ -184,7 +193,9 @@ std::vector<Tile> xcd_update_order(const std::vector<Tile> &tl, int S,
 // (ACE_TAIL_SORT=1): ngroups lists of *len entries
 bool tail_sort();
 // (sharded: rank r's own tiles of G)
-std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len, int G = 1, int r = 0);
+// (Z: steps per group, sweep_group())
+std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len, int G = 1, int r = 0,
+                                   int Z = 2);
 // own lower tiles of size T over [0, ntile*T) in row-major order (ace_shard.cpp)
 std::vector<Tile> own_tiles(int64_t ntile, int T, int G, int r);
 // super-block size S of that order (0: row-major grid); ACE_UPD_ORDER=S

@@ -8,8 +8,8 @@
 
 // Buffers of one Gauss-Jordan sweep and its lookahead events.
 struct SweepWork {
-  DBuf A, P0, P1, W0, W1, P2, P3, W2, W3, SW, S0, S1, piv, flag, order, xtiles, ptiles, gorder,
-      morder, mcnt;
+  DBuf A, Ps[8], Ws[8], SW, S0, S1, piv, flag, order, xtiles, ptiles, gorder, morder, mcnt;
+  int Z = 2;  // steps per bulk launch (sweep_group()), panel slots k % 2Z
   DBuf gtiles;                          // handle path: the gradient's tile list (build_grad_tiles)
   DBuf gpart, gwork, gsum;              // handle path: gradient partial-sum scratch
   int64_t ngtiles = 0, ngdiag = -2;     // -2: not built yet
@@ -28,7 +28,10 @@ struct SweepWork {
     npad = round_up(n, NB);
     naug = npad + AUG;
     alloc(ctx, A, (size_t)(naug * naug) * sizeof(double), "alloc A");
-    for (DBuf *b : {&P0, &P1, &W0, &W1}) alloc(ctx, *b, (size_t)(naug * NB) * sizeof(double), "alloc panel");
+    for (int j = 0; j < 2; ++j) {
+      alloc(ctx, Ps[j], (size_t)(naug * NB) * sizeof(double), "alloc panel");
+      alloc(ctx, Ws[j], (size_t)(naug * NB) * sizeof(double), "alloc panel");
+    }
     alloc(ctx, SW, (size_t)SW_DOUBLES * sizeof(double), "alloc SW");
     alloc(ctx, S0, (size_t)(SUB * NB) * sizeof(double), "alloc S");
     alloc(ctx, S1, (size_t)(SUB * NB) * sizeof(double), "alloc S");
@@ -44,21 +47,25 @@ struct SweepWork {
     }
     poff.clear();
     if (pair_steps() && cross_update_on_tiles() && npad / NB >= 2) {
-      for (DBuf *b : {&P2, &P3, &W2, &W3}) alloc(ctx, *b, (size_t)(naug * NB) * sizeof(double), "alloc panel");
-      const std::vector<Tile> t = pair_cross_tiles(naug, (int)(npad / NB), poff);
+      Z = sweep_group();
+      for (int j = 2; j < 2 * Z; ++j) {
+        alloc(ctx, Ps[j], (size_t)(naug * NB) * sizeof(double), "alloc panel");
+        alloc(ctx, Ws[j], (size_t)(naug * NB) * sizeof(double), "alloc panel");
+      }
+      const std::vector<Tile> t = pair_cross_tiles(naug, (int)(npad / NB), poff, Z);
       alloc(ctx, ptiles, std::max<size_t>(t.size(), 1) * sizeof(Tile), "alloc pair cross tiles");
       if (!t.empty())
         ck(ctx, hipMemcpy(ptiles.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
            "upload pair cross tiles");
       glen = 0;
       if (tail_sort()) {
-        const std::vector<Tile> o = pair_bulk_orders(naug, (int)(npad / NB), &glen);
+        const std::vector<Tile> o = pair_bulk_orders(naug, (int)(npad / NB), &glen, 1, 0, Z);
         alloc(ctx, gorder, o.size() * sizeof(Tile), "alloc bulk orders");
         ck(ctx, hipMemcpy(gorder.p, o.data(), o.size() * sizeof(Tile), hipMemcpyHostToDevice),
            "upload bulk orders");
       }
       moff.clear();
-      if (glen > 0 && merge_cross()) {
+      if (glen > 0 && merge_cross() && Z == 2) {
         const std::vector<Tile> m = merged_bulk_orders(naug, (int)(npad / NB), moff, mfront, mtarget);
         alloc(ctx, morder, m.size() * sizeof(Tile), "alloc merged orders");
         ck(ctx, hipMemcpy(morder.p, m.data(), m.size() * sizeof(Tile), hipMemcpyHostToDevice),
@@ -86,14 +93,11 @@ struct SweepWork {
     b.A = A.d();
     b.ld = naug;
     b.npad = npad;
-    b.P[0] = P0.d();
-    b.P[1] = P1.d();
-    b.W[0] = W0.d();
-    b.W[1] = W1.d();
-    b.P[2] = P2.p ? P2.d() : nullptr;
-    b.P[3] = P3.p ? P3.d() : nullptr;
-    b.W[2] = W2.p ? W2.d() : nullptr;
-    b.W[3] = W3.p ? W3.d() : nullptr;
+    for (int j = 0; j < 8; ++j) {
+      b.P[j] = Ps[j].p ? Ps[j].d() : nullptr;
+      b.W[j] = Ws[j].p ? Ws[j].d() : nullptr;
+    }
+    b.Z = Z;
     if (!poff.empty()) {
       b.ptiles = reinterpret_cast<const Tile *>(ptiles.p);
       b.poff = poff.data();

@@ -457,9 +457,12 @@ __device__ __forceinline__ void gemm1_mm(const double *sXJ, const RowX<PM, FP> &
 // identity on padding) and of the Kfull copy; same outputs as
 // k_assembly<PM, KIND, 0>.
 // ---------------------------------------------------------------------------
-// tile columns of the assembly's first part (model_pipeline): the first two
-// panels' columns, at most all of them
-__host__ __device__ inline int asm_first_cols(int nt) { return 2 * NB / AT < nt ? 2 * NB / AT : nt; }
+// tile columns of the assembly's first part (model_pipeline): the first
+// sweep group's panels' columns (sweep_group() blocks), at most all of them
+static int asm_first_cols(int nt) {
+  const int jb = sweep_group() * NB / AT;
+  return jb < nt ? jb : nt;
+}
 
 // Column blocks per wave of the assembly: ACE_ASM_CB = 4 (256 threads, 16
 // pairs per lane) or 2 (512 threads, wave w: rows 16 (w & 3).., columns
@@ -473,15 +476,14 @@ __global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 32 ? 3 : 2)) v
                                                 double sig, double *__restrict__ out, int64_t ld,
                                                 double *__restrict__ kcopy,
                                                 const Tile *__restrict__ tiles, int G, int part,
-                                                int nt) {
+                                                int nt, int JB) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const double sg = tab.sig ? *tab.sig : sig;  // exp(theta[0]) on the diagonal
   int64_t I, J;
-  // part 1: the tiles of the first two panels' columns (J < JB = 2 NB / AT,
-  // column by column) -- what the sweep's first group (two pivot chains and
-  // the cross of block 1) needs; part 2: the rest (the lower triangle of
-  // tiles >= JB); 0: every lower tile / the list
-  const int JB = asm_first_cols(nt);
+  // part 1: the tiles of the first sweep group's panels' columns (J < JB =
+  // Z NB / AT, column by column) -- what that group's pivot chains and
+  // lookahead crosses need; part 2: the rest (the lower triangle of tiles >=
+  // JB); 0: every lower tile / the list
   if (tiles || part == 0) {
     tile_of(tiles, blockIdx.x, I, J);
   } else if (part == 1) {
@@ -1113,10 +1115,10 @@ static hipError_t asm_mm_pm(int kind, PairSide S, int64_t npad, int B, int ZS, T
   }
   if (kind == 0)
     hipLaunchKernelGGL((k_asm_mm<PM, 0>), dim3((unsigned)nblk), dim3(ASM_NT), lds, st, S, B, ZS,
-                       tab, sig, out, ld, kcopy, tiles, G, part, (int)nt);
+                       tab, sig, out, ld, kcopy, tiles, G, part, (int)nt, (int)JB);
   else
     hipLaunchKernelGGL((k_asm_mm<PM, 1>), dim3((unsigned)nblk), dim3(ASM_NT), lds, st, S, B, ZS,
-                       tab, sig, out, ld, kcopy, tiles, G, part, (int)nt);
+                       tab, sig, out, ld, kcopy, tiles, G, part, (int)nt, (int)JB);
   return hipGetLastError();
 }
 

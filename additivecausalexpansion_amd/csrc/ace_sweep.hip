@@ -757,13 +757,13 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
   // staging: each thread moves 4 doubles of each operand per chunk (issued
   // before the C tile, so chunk 0 reaches LDS without waiting for C)
   const int sk = tid >> 5, sm = (tid & 31) * 4;
-  const double *gW = Rop + (R0 + sm) + (int64_t)sk * ldp;
-  const double *gP = Cop + (C0 + sm) + (int64_t)sk * ldp;
+  // scalar panel bases + 32-bit element offsets (as k_update_multi)
+  const int roff = (int)((R0 + sm) + (int64_t)sk * ldp), coff = (int)((C0 + sm) + (int64_t)sk * ldp);
   double2 rw[2], rp[2];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    rw[e] = *reinterpret_cast<const double2 *>(gW + 2 * e);
-    rp[e] = *reinterpret_cast<const double2 *>(gP + 2 * e);
+    rw[e] = *reinterpret_cast<const double2 *>(Rop + roff + 2 * e);
+    rp[e] = *reinterpret_cast<const double2 *>(Cop + coff + 2 * e);
   }
   __builtin_amdgcn_sched_barrier(0);  // keep the C-tile loads behind them
   const int wr = wv & 1, wc = wv >> 1;  // rows 64*wr.., cols 32*wc..
@@ -787,10 +787,11 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
     const int cur = ch & 1;
     if (ch + 1 < NCH) {
       const int64_t off = (int64_t)(ch + 1) * BK * ldp;
+      const double *nw = Rop + off, *np = Cop + off;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        rw[e] = *reinterpret_cast<const double2 *>(gW + off + 2 * e);
-        rp[e] = *reinterpret_cast<const double2 *>(gP + off + 2 * e);
+        rw[e] = *reinterpret_cast<const double2 *>(nw + roff + 2 * e);
+        rp[e] = *reinterpret_cast<const double2 *>(np + coff + 2 * e);
       }
     }
 #pragma unroll
@@ -1010,13 +1011,13 @@ __device__ __forceinline__ void update_pair_tile(
     return;
   }
   const int sk = tid >> 5, sm = (tid & 31) * 4;
-  const double *gWa = Ra + (R0 + sm) + (int64_t)sk * ldp;
-  const double *gPa = Ca + (C0 + sm) + (int64_t)sk * ldp;
-  const double *gWb = Rb + (R0 + sm) + (int64_t)sk * ldp;
-  const double *gPb = Cb + (C0 + sm) + (int64_t)sk * ldp;
+  // 32-bit element offsets from the (scalar) panel bases: the loads take a
+  // scalar base + vector offset (no 64-bit address VGPRs; -1 ms per C2
+  // evaluation, profiles/r03_v4_group_ab.txt)
+  const int roff = (int)((R0 + sm) + (int64_t)sk * ldp), coff = (int)((C0 + sm) + (int64_t)sk * ldp);
   double2 rw0, rw1, rp0, rp1;
   {
-    const double *w = from_w ? gWb : gWa, *pp = from_w ? gPb : gPa;
+    const double *w = (from_w ? Rb : Ra) + roff, *pp = (from_w ? Cb : Ca) + coff;
     rw0 = *reinterpret_cast<const double2 *>(w);
     rw1 = *reinterpret_cast<const double2 *>(w + 2);
     rp0 = *reinterpret_cast<const double2 *>(pp);
@@ -1047,13 +1048,13 @@ __device__ __forceinline__ void update_pair_tile(
   // chunk ch of segment seg (0: panel a, 1: panel b) uses LDS buffer ch & 1
   // (NCH is even, so the parity runs on across the two segments)
   for (int seg = from_w ? 1 : 0; seg < 2; ++seg) {
-    const double *sw = seg ? gWb : gWa, *sp = seg ? gPb : gPa;
+    const double *sw = seg ? Rb : Ra, *sp = seg ? Cb : Ca;
     for (int ch = 0; ch < NCH; ++ch) {
       const int cur = ch & 1;
       const bool more = ch + 1 < NCH || seg == 0;
       if (more) {
-        const double *nw = ch + 1 < NCH ? sw + (int64_t)(ch + 1) * BK * ldp : gWb;
-        const double *np = ch + 1 < NCH ? sp + (int64_t)(ch + 1) * BK * ldp : gPb;
+        const double *nw = (ch + 1 < NCH ? sw + (int64_t)(ch + 1) * BK * ldp : Rb) + roff;
+        const double *np = (ch + 1 < NCH ? sp + (int64_t)(ch + 1) * BK * ldp : Cb) + coff;
         rw0 = *reinterpret_cast<const double2 *>(nw);
         rw1 = *reinterpret_cast<const double2 *>(nw + 2);
         rp0 = *reinterpret_cast<const double2 *>(np);
@@ -1147,6 +1148,236 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
       __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+// Z sweep steps per launch (sweep_group() = 3 or 4; k_update_pair is Z = 2):
+// npan panels j = 0 .. npan-1 of blocks ka0 / NB + j, operands R[j] = W_j,
+// C[j] = Pn_j (single GPU), K = npan NB per tile.  A tile whose row or
+// column lies in one of those blocks is overwritten by the step of the
+// latest such block jm: it starts from W_jm and takes only panels jm+1 ..
+// npan-1 (jm = npan-1: a copy of W_jm); any other tile takes every panel.
+// Each accumulator runs the single-step schedule's MFMA chain in the same k
+// order (fp64 in registers between panels), so the results are
+// bit-identical to npan k_update launches.
+struct PanelSet {
+  const double *R[4];
+  const double *C[4];
+};
+// panel j's pointer (j wave-uniform: scalar selects, no indexed kernarg)
+__device__ __forceinline__ const double *psel(const double *const (&p)[4], int j) {
+  return j == 0 ? p[0] : j == 1 ? p[1] : j == 2 ? p[2] : p[3];
+}
+
+// SH (sharded): A holds the rank's block-cyclic columns (tile column C0 at
+// local column lcol(C0, G)) and the operands are swapped, R = Pn, C = W (W
+// is only computed for the rows the rank consumes, its own columns).
+template <bool SH>
+__device__ __forceinline__ void update_multi_tile(int I, int J, double (&sW)[2][BK][LDL],
+                                                  double (&sP)[2][BK][LDL], double *__restrict__ A,
+                                                  int64_t ld, const PanelSet &ps, int npan,
+                                                  int64_t ldp, int64_t ka0, const GatherOut &go,
+                                                  int G) {
+  constexpr int KT = NB / UT;
+  const int ta0 = (int)(ka0 / UT);
+  const int di = I - ta0, dj = J - ta0;
+  const int bi = (di >= 0 && di < npan * KT) ? di / KT : -1;
+  const int bj = (dj >= 0 && dj < npan * KT) ? dj / KT : -1;
+  const int jm = bi > bj ? bi : bj;  // the latest group block holding the tile
+  const int64_t R0 = (int64_t)I * UT, C0 = (int64_t)J * UT;
+  const int64_t L0 = SH ? lcol(C0, G) : C0;  // A's local column of the tile
+  const int tid = threadIdx.x;
+  const double *const(&WS)[4] = SH ? ps.C : ps.R;  // the W operands
+
+  if (jm == npan - 1) {  // the last block: W of the last step
+    const double *Wl = psel(WS, jm);
+    const int64_t kl0 = ka0 + (int64_t)jm * NB;
+    if (bi == jm && bj != jm) {
+      double *tileT = &sW[0][0][0];  // 64 x 65 scratch
+      for (int sa = 0; sa < 2; ++sa)
+        for (int sb = 0; sb < 2; ++sb) {
+          __syncthreads();
+          for (int e = tid; e < 4096; e += UTHREADS) {
+            const int c = e & 63, a = e >> 6;
+            tileT[a * 65 + c] = Wl[(C0 + 64 * sb + c) + (R0 - kl0 + 64 * sa + a) * ldp];
+          }
+          __syncthreads();
+          for (int e = tid; e < 4096; e += UTHREADS) {
+            const int a = e & 63, c = e >> 6;
+            const double v = tileT[a * 65 + c];
+            A[(R0 + 64 * sa + a) + (L0 + 64 * sb + c) * ld] = v;
+            if (go.k0 >= 0) gput(go, R0 + 64 * sa + a, C0 + 64 * sb + c, v);
+          }
+        }
+    } else {
+      for (int e = tid; e < UT * UT; e += UTHREADS) {
+        const int a = e & (UT - 1), c = e >> 7;
+        const double v = Wl[(R0 + a) + (C0 - kl0 + c) * ldp];
+        A[(R0 + a) + (L0 + c) * ld] = v;
+        if (go.k0 >= 0) gput(go, R0 + a, C0 + c, v);
+      }
+    }
+    return;
+  }
+  const bool from_w = jm >= 0;
+  const int seg0 = from_w ? jm + 1 : 0;
+  // W_jm at (row r, column c): column block jm (and its diagonal block)
+  // W_jm[r, c - kj0], row block jm W_jm[c, r - kj0] (transposed)
+  const bool jin = bj == jm;
+  const int64_t wrs = jin ? 1 : ldp, wcs = jin ? ldp : 1;
+  const double *wab = from_w ? psel(WS, jm) - (ka0 + (int64_t)jm * NB) * ldp : nullptr;
+
+  const int lane = tid & 63, wv = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  if (R0 >= ld - AUG) {  // AUG row block: 16 live rows (as k_update)
+    d4 acc;
+    const int64_t r = R0 + lr;
+    const int64_t c = C0 + 16 * wv + lk, lc = L0 + 16 * wv + lk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      acc[j] = from_w ? wab[r * wrs + (c + 4 * j) * wcs] : ld_a(&A[r + (lc + 4 * j) * ld]);
+    for (int pnl = seg0; pnl < npan; ++pnl) {
+      const double *gr = psel(ps.R, pnl) + R0 + lr + (int64_t)lk * ldp;
+      const double *gc = psel(ps.C, pnl) + C0 + 16 * wv + lr + (int64_t)lk * ldp;
+      double an = gc[0], bn = gr[0];
+      for (int kk = 0; kk < NB / 4; ++kk) {
+        const double a = an, bb = bn;
+        if (kk + 1 < NB / 4) {
+          an = gc[(int64_t)(4 * (kk + 1)) * ldp];
+          bn = gr[(int64_t)(4 * (kk + 1)) * ldp];
+        }
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st_a(&A[r + (lc + 4 * j) * ld], acc[j]);
+    if (go.k0 >= 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gput(go, r, c + 4 * j, acc[j]);
+      gput_aug_dead(go, A, ld, R0, C0, tid, UTHREADS, L0);
+    }
+    return;
+  }
+  const int sk = tid >> 5, sm = (tid & 31) * 4;
+  // 32-bit element offsets from the (scalar) panel bases: the loads take a
+  // scalar base + vector offset, so the segment pointers cost no VGPRs
+  const int roff = (int)((R0 + sm) + (int64_t)sk * ldp), coff = (int)((C0 + sm) + (int64_t)sk * ldp);
+  double2 rw0, rw1, rp0, rp1;
+  {
+    const double *w = psel(ps.R, seg0) + roff, *pp = psel(ps.C, seg0) + coff;
+    rw0 = *reinterpret_cast<const double2 *>(w);
+    rw1 = *reinterpret_cast<const double2 *>(w + 2);
+    rp0 = *reinterpret_cast<const double2 *>(pp);
+    rp1 = *reinterpret_cast<const double2 *>(pp + 2);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the C-tile loads behind them
+  const int wr = wv & 1, wc = wv >> 1;
+  d4 acc[2][4];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 4; ++ri) {
+      const int64_t r = R0 + 64 * wr + 16 * ri + lr;
+      const int64_t c = C0 + 32 * wc + 16 * ci + lk, lc = L0 + 32 * wc + 16 * ci + lk;
+      if (from_w) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[ci][ri][j] = wab[r * wrs + (c + 4 * j) * wcs];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[ci][ri][j] = ld_a(&A[r + (lc + 4 * j) * ld]);
+      }
+    }
+  *reinterpret_cast<double2 *>(&sW[0][sk][sm]) = rw0;
+  *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2]) = rw1;
+  *reinterpret_cast<double2 *>(&sP[0][sk][sm]) = rp0;
+  *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2]) = rp1;
+  __syncthreads();
+  // chunk ch of every segment uses LDS buffer ch & 1 (NCH is even, so the
+  // parity runs on across segments)
+  for (int seg = seg0; seg < npan; ++seg) {
+    const double *sw = psel(ps.R, seg), *sp = psel(ps.C, seg);
+    const bool last = seg + 1 == npan;
+    const double *nxw = last ? sw : psel(ps.R, seg + 1);
+    const double *nxp = last ? sp : psel(ps.C, seg + 1);
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int cur = ch & 1;
+      const bool more = ch + 1 < NCH || !last;
+      if (more) {
+        const double *nw = (ch + 1 < NCH ? sw + (int64_t)(ch + 1) * BK * ldp : nxw) + roff;
+        const double *np = (ch + 1 < NCH ? sp + (int64_t)(ch + 1) * BK * ldp : nxp) + coff;
+        rw0 = *reinterpret_cast<const double2 *>(nw);
+        rw1 = *reinterpret_cast<const double2 *>(nw + 2);
+        rp0 = *reinterpret_cast<const double2 *>(np);
+        rp1 = *reinterpret_cast<const double2 *>(np + 2);
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        double a[2], b[4];
+#pragma unroll
+        for (int ci = 0; ci < 2; ++ci) a[ci] = sP[cur][4 * kk + lk][32 * wc + 16 * ci + lr];
+#pragma unroll
+        for (int ri = 0; ri < 4; ++ri) b[ri] = sW[cur][4 * kk + lk][64 * wr + 16 * ri + lr];
+#pragma unroll
+        for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+          for (int ri = 0; ri < 4; ++ri)
+            acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
+      }
+      if (more) {
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm]) = rw0;
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2]) = rw1;
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm]) = rp0;
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2]) = rp1;
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 4; ++ri) {
+      const int64_t r = R0 + 64 * wr + 16 * ri + lr;
+      const int64_t lc = L0 + 32 * wc + 16 * ci + lk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st_a(&A[r + (lc + 4 * j) * ld], acc[ci][ri][j]);
+    }
+  if (go.k0 >= 0) {
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int ri = 0; ri < 4; ++ri)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          gput(go, R0 + 64 * wr + 16 * ri + lr, C0 + 32 * wc + 16 * ci + lk + 4 * j, acc[ci][ri][j]);
+  }
+}
+
+// npan (1 .. 4) steps in one launch on a tile list (null: every lower tile,
+// row-major grid), skipping the tiles with I or J in blocks [kx0, kx1).
+template <bool SH>
+__global__ __launch_bounds__(UTHREADS, 2) void k_update_multi(double *__restrict__ A, int64_t ld,
+                                                              PanelSet ps, int npan, int64_t ldp,
+                                                              int64_t ka0, int kx0, int kx1,
+                                                              const Tile *__restrict__ tiles,
+                                                              GatherOut go, int G) {
+  __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
+  __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
+  constexpr int KT = NB / UT;
+  int I, J;
+  if (tiles) {
+    const Tile tt = tiles[blockIdx.x];
+    I = tt.I;
+    J = tt.J;
+    if (I < 0) return;  // padding of the XCD order
+  } else {
+    const int t = blockIdx.x;
+    int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((i + 1) * (i + 2) / 2 <= t) ++i;
+    while (i * (i + 1) / 2 > t) --i;
+    I = i;
+    J = t - i * (i + 1) / 2;
+  }
+  if (kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT))) return;
+  update_multi_tile<SH>(I, J, sW, sP, A, ld, ps, npan, ldp, ka0, go, G);
 }
 
 // Side stream, merged schedule: wait until *cnt >= target (the merged bulk
@@ -1554,31 +1785,47 @@ bool tail_sort() {
   return v != 0;
 }
 
-std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len, int G, int r) {
+std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len, int G, int r, int Z) {
   const int64_t nT = naug / UT;
   constexpr int KT = NB / UT;
-  const int ng = (steps + 1) / 2;
+  const int ng = (steps + Z - 1) / Z;
   const std::vector<Tile> base = own_tiles(nT, UT, G, r);
   const int S = std::max(1, update_order_block());
   std::vector<Tile> all;
   *len = 0;
   for (int g = 0; g < ng; ++g) {
-    const int64_t ta0 = (int64_t)2 * g * KT, tb0 = ta0 + KT;
+    const int z = std::min(Z, steps - Z * g);
+    const int64_t ta0 = (int64_t)Z * g * KT;
     const bool more = g + 1 < ng;
-    const int64_t x0 = more ? (int64_t)2 * (g + 1) * KT : -1;
-    const int64_t x1 = more ? (int64_t)std::min(2 * (g + 1) + 2, steps) * KT : -1;
+    const int64_t x0 = more ? (int64_t)Z * (g + 1) * KT : -1;
+    const int64_t x1 = more ? (int64_t)std::min(Z * (g + 1) + Z, steps) * KT : -1;
+    // segments the tile runs: every panel, or those after its latest group
+    // block (a copy for the last one)
     auto cost = [&](const Tile &t) -> double {
       const int64_t I = t.I, J = t.J;
       if (more && ((I >= x0 && I < x1) || (J >= x0 && J < x1))) return 0.0;  // skipped
-      if ((I >= tb0 && I < tb0 + KT) || (J >= tb0 && J < tb0 + KT)) return 0.05;  // copy
+      const int64_t di = I - ta0, dj = J - ta0;
+      const int bi = (di >= 0 && di < z * KT) ? (int)(di / KT) : -1;
+      const int bj = (dj >= 0 && dj < z * KT) ? (int)(dj / KT) : -1;
+      const int jm = std::max(bi, bj);
+      if (jm == z - 1) return 0.05;  // copy
       const double rows = (I == nT - 1) ? 16.0 / UT : 1.0;
-      return rows * (((I >= ta0 && I < tb0) || (J >= ta0 && J < tb0)) ? 1.0 : 2.0);
+      return rows * (jm >= 0 ? z - 1 - jm : z);
     };
     const std::vector<Tile> o = xcd_update_order(base, S, cost);
     *len = (int64_t)o.size();
     all.insert(all.end(), o.begin(), o.end());
   }
   return all;
+}
+
+int sweep_group() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_GROUP");
+    v = e ? std::min(4, std::max(2, atoi(e))) : 2;
+  }
+  return v;
 }
 
 bool merge_cross() {
@@ -1649,23 +1896,31 @@ bool xsplit_cross() {
   return v != 0;
 }
 
-std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t> &off) {
+std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t> &off, int Z) {
   const int64_t nT = naug / UT;
   constexpr int KT = NB / UT;
-  const int ng = (steps + 1) / 2;
+  const int ng = (steps + Z - 1) / Z;
   const int S = update_order_block();
+  const bool xs = Z == 2 && xsplit_cross();
   std::vector<Tile> all;
   off.assign(3, 0);  // group 0 has no cross lists
   auto in_blk = [&](int64_t t, int blk) { return t >= (int64_t)blk * KT && t < (int64_t)(blk + 1) * KT; };
   for (int g = 1; g < ng; ++g) {
-    const int b0 = 2 * g, b1 = 2 * g + 1;
+    const int b0 = Z * g, b1 = std::min(Z * g + Z, steps);  // the group's blocks [b0, b1)
     std::vector<Tile> ta, tb;
     for (int64_t I = 0; I < nT; ++I)
       for (int64_t J = 0; J <= I; ++J) {
-        if (in_blk(I, b0) || in_blk(J, b0)) ta.push_back(Tile{(int)I, (int)J});
-        else if (b1 < steps && (in_blk(I, b1) || in_blk(J, b1))) tb.push_back(Tile{(int)I, (int)J});
+        if (in_blk(I, b0) || in_blk(J, b0)) {
+          ta.push_back(Tile{(int)I, (int)J});
+          continue;
+        }
+        for (int bb = b0 + 1; bb < b1; ++bb)
+          if (in_blk(I, bb) || in_blk(J, bb)) {
+            tb.push_back(Tile{(int)I, (int)J});
+            break;
+          }
       }
-    if (xsplit_cross()) {
+    if (xs) {
       // the pivot block's own tiles (I and J in block b0) lead block b0's
       // list, padded to XSPLIT_HEAD entries: the split schedule launches
       // them alone so the pivot chain can start before the rest is done
@@ -1678,13 +1933,35 @@ std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t>
     }
     bool first = true;
     for (auto *t : {&ta, &tb}) {
-      const std::vector<Tile> o = (S > 0 && !(first && xsplit_cross())) ? xcd_update_order(*t, S) : *t;
+      const std::vector<Tile> o = (S > 0 && !(first && xs)) ? xcd_update_order(*t, S) : *t;
       first = false;
       all.insert(all.end(), o.begin(), o.end());
       off.push_back((int64_t)all.size());
     }
   }
   return all;
+}
+
+// GEMM tiles of one launch of npan steps from block ka0 / NB (k_update_multi's
+// rule) over every lower tile outside blocks [kx0, kx1), in units of one full
+// tile x NB (a tile of the AUG row block computes 16 of 128 rows).
+double update_gemm_tiles_group(int64_t naug, int64_t ka0, int npan, int kx0, int kx1) {
+  const int64_t nT = naug / UT;
+  constexpr int KT = NB / UT;
+  const int64_t ta0 = ka0 / UT;
+  double cnt = 0.0;
+  for (int64_t I = 0; I < nT; ++I)
+    for (int64_t J = 0; J <= I; ++J) {
+      if (kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT)))
+        continue;
+      const int64_t di = I - ta0, dj = J - ta0;
+      const int bi = (di >= 0 && di < npan * KT) ? (int)(di / KT) : -1;
+      const int bj = (dj >= 0 && dj < npan * KT) ? (int)(dj / KT) : -1;
+      const int jm = std::max(bi, bj);
+      if (jm == npan - 1) continue;
+      cnt += ((I == nT - 1) ? 16.0 / UT : 1.0) * (jm >= 0 ? npan - 1 - jm : npan);
+    }
+  return cnt;
 }
 
 // GEMM tiles of one k_update_pair launch over every lower tile, in units of
@@ -1905,10 +2182,159 @@ static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const Swee
   return hipSuccess;
 }
 
+// Two-panel launches on k_update_multi (default; ACE_MULTI2=0: k_update_pair)
+static bool multi2_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_MULTI2");
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
+// Z = b.Z sweep steps per bulk launch (run_sweep_pairs: the round-2 Z = 2 form).
+// Group g = steps Z g .. Z g + z_g - 1 (the last one may be shorter), panels
+// in slots k % 2Z.
+//   side:  wait(bulk g-1 done) -> cross of group g+1's first block kb with
+//          group g's panels (gathers panel kb) -> its chain; side2
+//          meanwhile: the cross of the group's other blocks (not in kb) with
+//          group g's panels.  Then for j = 1 .. z-1: the cross of block
+//          kb + j with panels kb .. kb + j - 1 (gathers panel kb + j) -> its
+//          chain.  -> ready(g+1)
+//   main:  wait(ready g) -> the bulk launch of group g's panels over every
+//          tile outside group g+1's cross.
+// Launches of 1 / 2 panels run k_update / k_update_pair, 3 / 4 k_update_multi;
+// every element sees the single-step schedule's MFMA chains in the same
+// order, so the result is bit-identical to it (tests/test_gpu.py).
+static hipError_t run_sweep_groups(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
+                                   const SweepTiming *tm) {
+  const int64_t naug = b.ld;
+  const unsigned nT = (unsigned)(naug / UT);
+  const int steps = (int)(b.npad / NB);
+  const int Z = b.Z;
+  const int ng = (steps + Z - 1) / Z;
+  const bool two = sy && sy->side && sy->nev >= 2 * steps + 1;
+  hipStream_t side = two ? sy->side : st;
+  const bool two2 = two && side2_on() && sy->side2 && sy->nev >= 4 * steps + 4;
+  hipStream_t side2 = two2 ? sy->side2 : side;
+  auto zsize = [&](int g) { return std::min(Z, steps - Z * g); };
+  auto slot = [&](int k) { return k % (2 * Z); };
+  auto E1 = [&](int g) { return sy->ev[2 * steps + 1 + 2 * g]; };
+  auto E2 = [&](int g) { return sy->ev[2 * steps + 2 + 2 * g]; };
+  const bool xg = xgather();
+  auto gout = [&](int k) {
+    return xg ? GatherOut{b.P[slot(k)], b.W[slot(k)], b.S[0], (int64_t)k * NB, b.ld} : no_gather();
+  };
+  // npan steps from block kb on a tile list (null: the row-major grid of nt
+  // tiles), skipping blocks [kx0, kx1).  Two panels run k_update_multi too
+  // (77.1 against 78.1 ms per C2 evaluation with k_update_pair, same box, 3
+  // rounds, profiles/r03_v4_group_ab.txt); ACE_MULTI2=0 selects k_update_pair
+  const bool multi2 = multi2_on();
+  auto upd = [&](int npan, int kb, int kx0, int kx1, const Tile *tl, int64_t nt, GatherOut go,
+                 hipStream_t s_) {
+    if (nt <= 0) return;
+    const int64_t ka0 = (int64_t)kb * NB;
+    if (npan == 1) {  // (only ever without a skip range)
+      hipLaunchKernelGGL(k_update, dim3((unsigned)nt), dim3(UTHREADS), 0, s_, b.A, b.ld,
+                         b.W[slot(kb)], b.P[slot(kb)], b.W[slot(kb)], b.ld, ka0, -1, tl, 1, go);
+    } else if (npan == 2 && !multi2) {
+      hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nt), dim3(UTHREADS), 0, s_, b.A, b.ld,
+                         b.W[slot(kb)], b.P[slot(kb)], b.W[slot(kb + 1)], b.P[slot(kb + 1)], b.ld,
+                         ka0, kx0, kx1, tl, go, -1, nullptr, 1, 0);
+    } else {
+      PanelSet ps;
+      for (int j = 0; j < 4; ++j) {
+        ps.R[j] = j < npan ? b.W[slot(kb + j)] : nullptr;
+        ps.C[j] = j < npan ? b.P[slot(kb + j)] : nullptr;
+      }
+      hipLaunchKernelGGL(k_update_multi<false>, dim3((unsigned)nt), dim3(UTHREADS), 0, s_, b.A,
+                         b.ld, ps, npan, b.ld, ka0, kx0, kx1, tl, go, 1);
+    }
+  };
+  // blocks kb + 1 .. kb + z - 1 of a group from its own panels, each followed
+  // by its chain (on `side`)
+  auto inner = [&](int kb, int z) -> hipError_t {
+    for (int j = 1; j < z; ++j) {
+      const int k = kb + j - 1;  // xoff list k: the tiles with I or J in block k + 1
+      const int64_t x0 = b.xoff[k], nx = b.xoff[k + 1] - x0;
+      upd(j, kb, -1, -1, b.xtiles + x0, nx, gout(kb + j), side);
+      const hipError_t r = panel_sweep(b, slot(kb + j), (int64_t)(kb + j) * NB, side, xg);
+      if (r != hipSuccess) return r;
+    }
+    return hipSuccess;
+  };
+  hipError_t e;
+  if (two) {
+    if (!sy->ready_recorded) {
+      e = hipEventRecord(sy->ev[2 * steps], st);  // inputs ready
+      if (e != hipSuccess) return e;
+    }
+    if ((e = hipStreamWaitEvent(side, sy->ev[2 * steps], 0)) != hipSuccess) return e;
+  }
+  // group 0: its first panel is gathered by its chain (nothing wrote it yet)
+  if ((e = panel_sweep(b, slot(0), 0, side)) != hipSuccess) return e;
+  if ((e = inner(0, zsize(0))) != hipSuccess) return e;
+  if (two && (e = hipEventRecord(sy->ev[0], side)) != hipSuccess) return e;
+  int used = 0;
+  for (int g = 0; g < ng; ++g) {
+    const int kg = Z * g;
+    const bool more = g + 1 < ng;
+    const int kb = Z * (g + 1), zb = more ? zsize(g + 1) : 0;
+    if (two && (e = hipStreamWaitEvent(st, sy->ev[2 * g], 0)) != hipSuccess) return e;
+    if (more) {
+      if (two) {
+        if ((e = hipEventRecord(sy->ev[2 * g + 1], st)) != hipSuccess) return e;  // bulk g-1 done
+        if ((e = hipStreamWaitEvent(side, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
+      }
+      const int64_t pa = b.poff[2 * (g + 1)], na = b.poff[2 * (g + 1) + 1] - pa;
+      const int64_t pb = b.poff[2 * (g + 1) + 1], nb = b.poff[2 * (g + 1) + 2] - pb;
+      if (nb > 0 && two2) {
+        if ((e = hipEventRecord(E1(g + 1), side)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(side2, E1(g + 1), 0)) != hipSuccess) return e;
+      }
+      upd(zsize(g), kg, -1, -1, b.ptiles + pa, na, gout(kb), side);
+      if (nb > 0) {
+        upd(zsize(g), kg, -1, -1, b.ptiles + pb, nb, no_gather(), side2);
+        if (two2 && (e = hipEventRecord(E2(g + 1), side2)) != hipSuccess) return e;
+      }
+      if ((e = panel_sweep(b, slot(kb), (int64_t)kb * NB, side, xg)) != hipSuccess) return e;
+      if (nb > 0 && two2 && (e = hipStreamWaitEvent(side, E2(g + 1), 0)) != hipSuccess) return e;
+      if ((e = inner(kb, zb)) != hipSuccess) return e;
+      if (two && (e = hipEventRecord(sy->ev[2 * (g + 1)], side)) != hipSuccess) return e;
+    }
+    const bool timed = tm && tm->ev && used + 2 <= tm->nev;
+    if (timed) (void)hipEventRecord(tm->ev[used], st);
+    const int64_t grid = b.gorder ? b.glen : (b.order ? b.norder : (int64_t)nT * (nT + 1) / 2);
+    const Tile *ord = b.gorder ? b.gorder + (int64_t)g * b.glen : b.order;
+    const int kx0 = more ? kb : -1, kx1 = more ? kb + zb : -1;
+    upd(zsize(g), kg, kx0, kx1, ord, grid, no_gather(), st);
+    if (timed) {
+      (void)hipEventRecord(tm->ev[used + 1], st);
+      if (tm->flops)
+        tm->flops[used / 2] =
+            update_gemm_tiles_group(naug, (int64_t)kg * NB, zsize(g), kx0, kx1) * 2.0 * UT * UT * NB;
+      used += 2;
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (tm && tm->used) *tm->used = used;
+  return hipSuccess;
+}
+
 hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
                      const SweepTiming *tm) {
-  if (pair_steps() && b.ptiles && b.xtiles && b.P[2] && b.npad / NB >= 2)
+  if (pair_steps() && b.ptiles && b.xtiles && b.P[2] && b.npad / NB >= 2) {
+    // the group schedule (any Z); ACE_GROUP_SCHED=0 -- and the merged /
+    // split-cross variants, which only it implements -- select the round-2
+    // pair schedule (Z = 2, k_update_pair)
+    static const bool gs = [] {
+      const char *e = getenv("ACE_GROUP_SCHED");
+      return !(e && atoi(e) == 0);
+    }();
+    if (b.P[2 * b.Z - 1] && (b.Z > 2 || (gs && !b.morder && !xsplit_cross())))
+      return run_sweep_groups(b, st, sy, tm);
     return run_sweep_pairs(b, st, sy, tm);
+  }
   const int64_t naug = b.ld;
   const unsigned nT = (unsigned)(naug / UT);
   const int steps = (int)(b.npad / NB);
@@ -2043,10 +2469,16 @@ hipError_t shard_update_pair(const ShardSweep &b, int ka, int kx0, int kx1, cons
   const GatherOut go = kpack >= 0 ? pack_out(b.low, send_of(b, kpack), b.P[sp], b.W[sp], b.S[0],
                                              (int64_t)kpack * NB, b.ld, b.G)
                                   : no_gather();
-  if (nt > 0)
+  if (nt <= 0) return hipGetLastError();
+  if (multi2_on()) {
+    PanelSet ps{{b.P[sa], b.P[sb], nullptr, nullptr}, {b.W[sa], b.W[sb], nullptr, nullptr}};
+    hipLaunchKernelGGL(k_update_multi<true>, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld,
+                       ps, 2, b.ld, (int64_t)ka * NB, kx0, kx1, tiles, go, b.G);
+  } else {
     hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld, b.P[sa],
                        b.W[sa], b.P[sb], b.W[sb], b.ld, (int64_t)ka * NB, kx0, kx1, tiles, go,
                        -1, nullptr, b.G, 1);
+  }
   return hipGetLastError();
 }
 

@@ -108,7 +108,8 @@ def pmc_traffic(kernel="k_update"):
 
 
 def rocprof_bulk_avg():
-    """Average duration (ms) of the bulk k_update_pair launch in the newest
+    """Average duration (ms) of the bulk update launch (k_update_multi; older
+    summaries: k_update_pair) in the newest
     committed rocprofv3 kernel-trace summary (profiles/rNN_vMM_kernel_stats_split.csv,
     tools/kernel_stats_split.py: the bulk launches on their own line), for the
     cross-check against this run's HIP-event average."""
@@ -119,7 +120,7 @@ def rocprof_bulk_avg():
         return None, None
     try:
         for row in csv.DictReader(open(files[-1])):
-            if row["Name"] == "ace::k_update_pair[bulk]":
+            if row["Name"] in ("ace::k_update_multi[bulk]", "ace::k_update_pair[bulk]"):
                 return float(row["AverageNs"]) / 1e6, os.path.relpath(files[-1], ROOT)
     except (KeyError, ValueError, OSError):
         pass
@@ -384,7 +385,9 @@ def main():
 
     line = None
     if rank == 0:
-        traffic, traffic_src = pmc_traffic("k_update_pair_bulk")
+        traffic, traffic_src = pmc_traffic("k_update_multi_bulk")
+        if traffic is None:  # a summary from before the multi-panel kernel
+            traffic, traffic_src = pmc_traffic("k_update_pair_bulk")
         rp_ms, rp_src = rocprof_bulk_avg()
         naug = -(-n // 256) * 256 + 128
         nt = naug // 128
@@ -415,7 +418,7 @@ def main():
                 "parallelism": "single" if world == 1 else f"replicas x{world}",
             },
             "roofline": {
-                "kernel": ("k_update_pair (bulk sweep update, two Gauss-Jordan steps per launch, "
+                "kernel": ("k_update_multi (bulk sweep update, two Gauss-Jordan steps per launch, "
                            "K = 512 per 128x128 tile, v_mfma_f64_16x16x4_f64)"),
                 "bound": "mfma",
                 "achieved": achieved,

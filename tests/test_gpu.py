@@ -476,7 +476,7 @@ def test_cross_update_on_tiles_is_bitwise_neutral(A, tmp_path):
     assert np.array_equal(A.invkernel_cpp(K, th[0])["inv"], outs["0"])
 
 
-@pytest.mark.parametrize("n", [1100, 1500])
+@pytest.mark.parametrize("n", [1100, 1500, 2600])
 def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     """Two sweep steps per bulk launch (k_update_pair, ACE_PAIR=1) run every
     element's MFMA chain over the same k order as one step per launch: the
@@ -487,7 +487,10 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     stream for everything (ACE_LOOKAHEAD=0), the panel GEMM on 128-tiles
     (ACE_PGEMM_TILES=0: the 64-row k_panel_gemm) and the next group's cross
     tiles at the head of the bulk launch (ACE_XMERGE=1, with and without the
-    fused gather) instead of side-stream launches."""
+    fused gather) instead of side-stream launches.  Three and four steps per
+    bulk launch (ACE_GROUP=3 / 4, k_update_multi; groups 3+2 / 4+1 at n =
+    1100, 3+3 / 4+2 at 1500, 3+3+3+2 / 4+4+3 at 2600) are bit-identical too,
+    with and without the fused gather, the second side stream and lookahead."""
     import os
     import subprocess
     import sys
@@ -508,7 +511,13 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
                 "merged": {"ACE_PAIR": "1", "ACE_XMERGE": "1"},
                 "merged_gather": {"ACE_PAIR": "1", "ACE_XMERGE": "1", "ACE_XGATHER": "0"},
                 "unmerged": {"ACE_PAIR": "1", "ACE_XMERGE": "0"},
-                "xsplit": {"ACE_PAIR": "1", "ACE_XSPLIT": "1"}}
+                "xsplit": {"ACE_PAIR": "1", "ACE_XSPLIT": "1"},
+                "pair_kernel": {"ACE_MULTI2": "0"}, "pair_schedule": {"ACE_GROUP_SCHED": "0"},
+                "group3": {"ACE_GROUP": "3"}, "group4": {"ACE_GROUP": "4"},
+                "group4_gather": {"ACE_GROUP": "4", "ACE_XGATHER": "0"},
+                "group4_one_side": {"ACE_GROUP": "4", "ACE_SIDE2": "0"},
+                "group4_one_stream": {"ACE_GROUP": "4", "ACE_LOOKAHEAD": "0"},
+                "group3_untail": {"ACE_GROUP": "3", "ACE_TAIL_SORT": "0"}}
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)
@@ -588,12 +597,16 @@ def test_merged_cross_model_is_bitwise_neutral(tmp_path, n):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
-    for v in ("0", "1", "split"):
+    for v in ("0", "1", "split", "group4"):
         out = str(tmp_path / f"m{v}.npy")
-        env = dict(os.environ, ACE_XMERGE=v) if v != "split" else dict(os.environ, ACE_XSPLIT="1")
+        env = (dict(os.environ, ACE_XSPLIT="1") if v == "split" else
+               dict(os.environ, ACE_GROUP="4") if v == "group4" else dict(os.environ, ACE_XMERGE=v))
         subprocess.run([sys.executable, "-c", _MODEL_SNIPPET.format(root=root, n=n, out=out)],
                        env=env, check=True, timeout=100)
         outs[v] = np.load(out)
     assert np.all(np.isfinite(outs["1"]))
     assert np.array_equal(outs["0"], outs["1"])
     assert np.array_equal(outs["0"], outs["split"])  # the split cross (ACE_XSPLIT=1)
+    # four steps per bulk launch: the assembly's first part covers the first
+    # group's four panels, its side path runs under the rest
+    assert np.array_equal(outs["0"], outs["group4"])

@@ -165,7 +165,8 @@ def test_sharded_pair_schedule_is_bitwise_neutral(tmp_path, world, n):
     default) and the one-step schedule (ACE_PAIR=0) give bit-identical
     results: every tile sees the same MFMA chains in the same order; and so
     does the exchange packing fused into the cross launches (default)
-    against separate pack launches (ACE_FUSE_PACK=0).  n
+    against separate pack launches (ACE_FUSE_PACK=0), and the pair launches
+    on k_update_multi (default) against k_update_pair (ACE_MULTI2=0).  n
     gives 8, 7 (an odd last group) and 9 sweep steps; the simulated group
     runs the lookahead with all ranks on the shared streams."""
     import os
@@ -173,7 +174,8 @@ def test_sharded_pair_schedule_is_bitwise_neutral(tmp_path, world, n):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
-    variants = {"step": {"ACE_PAIR": "0"}, "pair": {"ACE_FUSE_PACK": "0"}, "fused": {}}
+    variants = {"step": {"ACE_PAIR": "0"}, "pair": {"ACE_FUSE_PACK": "0"}, "fused": {},
+                "pair_kernel": {"ACE_MULTI2": "0"}}
     for v, extra in variants.items():
         out = str(tmp_path / f"s{v}.npz")
         env = dict(os.environ, **extra)

@@ -8,7 +8,7 @@ cfgs=${@:-C2}
 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-r6 > gpurun_out/sp/single.json 2> gpurun_out/sp/single.err || exit 1
 python -c "import json;d=json.load(open('gpurun_out/sp/single.json'));print('single C2', round(d['value'],3), round(d['ms_per_step'],1))"
 for cfg in $cfgs; do
-  for env in ${AB_ENVS:-"ACE_PAIR=0" "ACE_FUSE_PACK=0" "ACE_X=1"}; do
+  for env in ${AB_ENVS:-ACE_PAIR=0 ACE_FUSE_PACK=0 ACE_X=1}; do
     port=$((port + 1))
     st=3; [ $cfg = C4 ] && st=2
     tag=${cfg}_${env%%=*}

@@ -1,11 +1,11 @@
-"""rocprofv3 kernel stats with k_update_pair split by role.
+"""rocprofv3 kernel stats with the two-step update kernel split by role.
 
-k_update_pair runs as the bulk sweep update (every lower tile: the largest
-grid) and as the side stream's lookahead cross (a few hundred tiles), so the
---stats line of k_update_pair averages two different launch sizes.  This
-recomputes the per-kernel summary from the --kernel-trace CSV with the bulk
-launches on their own line (`k_update_pair[bulk]`), which is the launch the
-bench's roofline times with HIP events.
+k_update_multi (round 3; k_update_pair before) runs as the bulk sweep update
+(every lower tile: the largest grid) and as the side stream's lookahead cross
+(a few hundred tiles), so its --stats line averages two different launch
+sizes.  This recomputes the per-kernel summary from the --kernel-trace CSV
+with the bulk launches on their own line (`k_update_multi[bulk]`), which is
+the launch the bench's roofline times with HIP events.
 
 usage: python tools/kernel_stats_split.py DIR > profiles/rNN_kernel_stats_split.csv
 """
@@ -19,12 +19,15 @@ from collections import defaultdict
 def main():
     f = glob.glob(os.path.join(sys.argv[1], "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = [r for r in csv.DictReader(open(f)) if r.get("Kind", "KERNEL_DISPATCH") == "KERNEL_DISPATCH"]
-    gmax = max((int(r["Grid_Size_X"]) for r in rows if "k_update_pair(" in r["Kernel_Name"]), default=0)
+    split = {"k_update_multi<false>(": "ace::k_update_multi", "k_update_pair(": "ace::k_update_pair"}
+    gmax = {key: max((int(r["Grid_Size_X"]) for r in rows if key in r["Kernel_Name"]), default=0)
+            for key in split}
     dur = defaultdict(list)
     for r in rows:
         name = r["Kernel_Name"]
-        if "k_update_pair(" in name:
-            name = "ace::k_update_pair[bulk]" if int(r["Grid_Size_X"]) == gmax else "ace::k_update_pair[cross]"
+        for key, short in split.items():
+            if key in name:
+                name = short + ("[bulk]" if int(r["Grid_Size_X"]) == gmax[key] else "[cross]")
         dur[name].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     total = sum(sum(v) for v in dur.values())
     w = csv.writer(sys.stdout)

@@ -22,6 +22,7 @@ from collections import defaultdict
 KERNELS = {
     "k_update": "ace::k_update(",
     "k_update_pair": "ace::k_update_pair(",
+    "k_update_multi": "ace::k_update_multi<false>(",
     "k_update_x": "ace::k_update_x(",
     "k_gather": "ace::k_gather(",
     "k_panel_gemm": "ace::k_panel_gemm(",
@@ -47,14 +48,15 @@ def read(d, counter):
                         per[short][k] = per[short].get(k, 0.0) + float(row["Counter_Value"])
                         grid[short][k] = int(row.get("Grid_Size", 0) or 0)
     vals = {s: [v for _, v in sorted(m.items())] for s, m in per.items()}
-    # k_update_pair runs both as the bulk update (every lower tile: the
-    # largest grid) and as the side stream's lookahead cross (a few hundred
-    # tiles): report the bulk launches, selected by grid size, on their own
-    if "k_update_pair" in per:
-        g = grid["k_update_pair"]
-        gmax = max(g.values())
-        vals["k_update_pair_bulk"] = [v for k, v in sorted(per["k_update_pair"].items())
-                                      if g[k] == gmax]
+    # the two-step update kernel runs both as the bulk update (every lower
+    # tile: the largest grid) and as the side stream's lookahead cross (a few
+    # hundred tiles): report the bulk launches, selected by grid size, on
+    # their own
+    for kn in ("k_update_pair", "k_update_multi"):
+        if kn in per:
+            g = grid[kn]
+            gmax = max(g.values())
+            vals[kn + "_bulk"] = [v for k, v in sorted(per[kn].items()) if g[k] == gmax]
     return vals
 
 
@@ -63,7 +65,7 @@ def main():
     fetch = read(fdir, "FETCH_SIZE")
     write = read(wdir, "WRITE_SIZE")
     out = {"unit": "bytes per launch", "fetch_correction": 2.0, "kernels": {}}
-    for k in list(KERNELS) + ["k_update_pair_bulk"]:
+    for k in list(KERNELS) + ["k_update_pair_bulk", "k_update_multi_bulk"]:
         if not fetch.get(k) or not write.get(k):
             continue
         f = sum(fetch[k]) / len(fetch[k]) * 1024.0

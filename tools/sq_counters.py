@@ -7,7 +7,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("k_grad_mm", "k_asm_mm", "k_grad2", "k_assembly", "k_update(", "k_update_x")
+KERNELS = ("k_grad_mm", "k_asm_mm", "k_grad2", "k_assembly", "k_update(", "k_update_x", "k_update_multi")
 
 
 def main():
