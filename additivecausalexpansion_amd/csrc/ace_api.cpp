@@ -52,13 +52,14 @@ int ace_create(int device, ace_ctx **out) {
   if (e == hipSuccess) {
     // the lookahead panel chain is latency-bound: give it the highest priority
     // so its workgroups take the first free CU slots next to the update kernel
-    // (ACE_SIDE_PRIO=0: default priority, A/B switch; ACE_SIDE2_PRIO=0: the
-    // second side stream only)
+    // (ACE_SIDE_PRIO=0: the least priority, A/B switch; ACE_SIDE2_PRIO=0: the
+    // second side stream only; =2: the main stream's (default) priority.
+    // The range on the box: least 1, greatest -1, default 0)
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
     auto prio = [&](const char *var) {
       const char *v = getenv(var);
-      return (v && atoi(v) == 0) ? lo : hi;
+      return (v && atoi(v) == 0) ? lo : (v && atoi(v) == 2) ? 0 : hi;
     };
     const int p1 = prio("ACE_SIDE_PRIO"), p2 = p1 == lo ? lo : prio("ACE_SIDE2_PRIO");
     e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, p1);

@@ -144,6 +144,8 @@ struct SweepBufs {
   const Tile *ptiles = nullptr;
   const int64_t *poff = nullptr;
   const Tile *gorder = nullptr;  // per-group bulk orders (tail_sort), glen each
+  const Tile *htiles = nullptr;  // group_head_tiles lists (run_sweep_heads), offsets hoff
+  const int64_t *hoff = nullptr;
   int64_t glen = 0;
   // merged schedule (merge_cross()): group g's bulk launch runs the list
   // morder[moff[g], moff[g+1]) = [group g+1's cross tiles (mfront[g]
@@ -175,6 +177,11 @@ bool pair_steps();
 std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t> &off,
                                    int Z = 2);
 double update_gemm_tiles_pair(int64_t naug, int64_t ka0, int kx0, int kx1);
+// Head / tail lists of the group schedule's lookahead (run_sweep_heads):
+// 2Z lists per group at off[G 2Z + m] (see ace_sweep.hip).  heads_on():
+// ACE_HEADS switch.
+std::vector<Tile> group_head_tiles(int64_t naug, int steps, int Z, std::vector<int64_t> &off);
+bool heads_on();
 // Steps per bulk launch: 2 (k_update_pair, default), ACE_GROUP=3 or 4 selects
 // k_update_multi groups (run_sweep_groups).
 int sweep_group();

@@ -8,12 +8,12 @@
 
 // Buffers of one Gauss-Jordan sweep and its lookahead events.
 struct SweepWork {
-  DBuf A, Ps[8], Ws[8], SW, S0, S1, piv, flag, order, xtiles, ptiles, gorder, morder, mcnt;
+  DBuf A, Ps[8], Ws[8], SW, S0, S1, piv, flag, order, xtiles, ptiles, gorder, morder, mcnt, htiles;
   int Z = 2;  // steps per bulk launch (sweep_group()), panel slots k % 2Z
   DBuf gtiles;                          // handle path: the gradient's tile list (build_grad_tiles)
   DBuf gpart, gwork, gsum;              // handle path: gradient partial-sum scratch
   int64_t ngtiles = 0, ngdiag = -2;     // -2: not built yet
-  std::vector<int64_t> xoff, poff, moff;
+  std::vector<int64_t> xoff, poff, moff, hoff;
   std::vector<int> mfront, mtarget;
   int64_t glen = 0;
   std::vector<hipEvent_t> ev;
@@ -64,6 +64,14 @@ struct SweepWork {
         ck(ctx, hipMemcpy(gorder.p, o.data(), o.size() * sizeof(Tile), hipMemcpyHostToDevice),
            "upload bulk orders");
       }
+      hoff.clear();
+      if (heads_on()) {
+        const std::vector<Tile> h = group_head_tiles(naug, (int)(npad / NB), Z, hoff);
+        alloc(ctx, htiles, std::max<size_t>(h.size(), 1) * sizeof(Tile), "alloc head tiles");
+        if (!h.empty())
+          ck(ctx, hipMemcpy(htiles.p, h.data(), h.size() * sizeof(Tile), hipMemcpyHostToDevice),
+             "upload head tiles");
+      }
       moff.clear();
       if (glen > 0 && merge_cross() && Z == 2) {
         const std::vector<Tile> m = merged_bulk_orders(naug, (int)(npad / NB), moff, mfront, mtarget);
@@ -105,6 +113,10 @@ struct SweepWork {
     if (glen > 0) {
       b.gorder = reinterpret_cast<const Tile *>(gorder.p);
       b.glen = glen;
+    }
+    if (!hoff.empty()) {
+      b.htiles = reinterpret_cast<const Tile *>(htiles.p);
+      b.hoff = hoff.data();
     }
     if (!moff.empty()) {
       b.morder = reinterpret_cast<const Tile *>(morder.p);

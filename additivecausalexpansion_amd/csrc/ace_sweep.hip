@@ -846,10 +846,15 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
 __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict__ W,
                                                               const double *__restrict__ Pn,
                                                               int64_t ldp, int64_t k0, int G,
-                                                              int r) {
+                                                              int r, int rt0 = 0,
+                                                              int rs0 = 1 << 30, int rs1 = 1 << 30) {
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];  // Pn rows of the tile
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];  // W_kk rows c
-  const int64_t R0 = (int64_t)blockIdx.x * UT, C0 = (int64_t)blockIdx.y * UT;
+  // row tile rt0 + blockIdx.x, skipping row tiles [rs0, rs1) (the head/tail
+  // split of run_sweep_heads; default: every row tile)
+  int rt = rt0 + (int)blockIdx.x;
+  if (rt >= rs0) rt += rs1 - rs0;
+  const int64_t R0 = (int64_t)rt * UT, C0 = (int64_t)blockIdx.y * UT;
   if (R0 >= k0 && R0 < k0 + NB) return;  // pivot rows are already final
   if (G > 1 && !owns_col(R0, G, r) && !(owns_col(k0, G, r) && R0 >= k0)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1524,6 +1529,101 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
     }
 }
 
+// Latency-critical lookahead updates of the head path (run_sweep_heads): npan
+// panels from ps on a list of 128-tiles none of which lies in a panel's
+// block (so no copies), as 64 x 64 quarters (blockIdx.x = 4 t + quarter;
+// the upper quarter of a diagonal tile too, as k_update computes it) with
+// k_update_x's 4-wave MFMA chain per panel and the accumulators kept across
+// panels: per element the same chain as k_update / k_update_multi, a quarter
+// of a 128-tile's work per workgroup.  go: the gather fused into the launch.
+__global__ __launch_bounds__(256) void k_update_q(double *__restrict__ A, int64_t ld, PanelSet ps,
+                                                  int npan, int64_t ldp,
+                                                  const Tile *__restrict__ tiles, GatherOut go) {
+  __shared__ __attribute__((aligned(16))) double sW[2][BK][XL];
+  __shared__ __attribute__((aligned(16))) double sP[2][BK][XL];
+  const Tile tt = tiles[blockIdx.x >> 2];
+  if (tt.I < 0) return;  // padding of the XCD order
+  const int q = blockIdx.x & 3;
+  const int64_t R0 = (int64_t)tt.I * UT + XT * (q & 1), C0 = (int64_t)tt.J * UT + XT * (q >> 1);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int wr = wv & 1, wc = wv >> 1;  // rows 32*wr.., cols 32*wc..
+  const int lr = lane & 15, lk = lane >> 4;
+  d4 acc[2][2];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) {
+      const int64_t r = R0 + 32 * wr + 16 * ri + lr;
+      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[ci][ri][j] = A[r + (c + 4 * j) * ld];
+    }
+  const int sk = tid >> 4, sm = (tid & 15) * 4;
+  for (int pj = 0; pj < npan; ++pj) {
+    const double *gW = psel(ps.R, pj) + (R0 + sm) + (int64_t)sk * ldp;
+    const double *gP = psel(ps.C, pj) + (C0 + sm) + (int64_t)sk * ldp;
+    double2 rw[2], rp[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      rw[e] = *reinterpret_cast<const double2 *>(gW + 2 * e);
+      rp[e] = *reinterpret_cast<const double2 *>(gP + 2 * e);
+    }
+    __syncthreads();  // the previous panel's last chunk is consumed
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2 * e]) = rw[e];
+      *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2 * e]) = rp[e];
+    }
+    __syncthreads();
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int cur = ch & 1;
+      if (ch + 1 < NCH) {
+        const int64_t off = (int64_t)(ch + 1) * BK * ldp;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          rw[e] = *reinterpret_cast<const double2 *>(gW + off + 2 * e);
+          rp[e] = *reinterpret_cast<const double2 *>(gP + off + 2 * e);
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        double a[2], b[2];
+#pragma unroll
+        for (int ci = 0; ci < 2; ++ci) a[ci] = sP[cur][4 * kk + lk][32 * wc + 16 * ci + lr];
+#pragma unroll
+        for (int ri = 0; ri < 2; ++ri) b[ri] = sW[cur][4 * kk + lk][32 * wr + 16 * ri + lr];
+#pragma unroll
+        for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+          for (int ri = 0; ri < 2; ++ri)
+            acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
+      }
+      if (ch + 1 < NCH) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2 * e]) = rw[e];
+          *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2 * e]) = rp[e];
+        }
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) {
+      const int64_t r = R0 + 32 * wr + 16 * ri + lr;
+      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double v = acc[ci][ri][j];
+        A[r + (c + 4 * j) * ld] = v;
+        if (go.k0 >= 0) gput(go, r, c + 4 * j, v);
+      }
+    }
+}
+
 // ---------------------------------------------------------------- sharded panel
 // Packing for the panel exchange of step k (sharded model).  The owner of
 // block k sends rows [k0, naug) of its column block (contiguous, ld naug-k0)
@@ -1643,7 +1743,8 @@ static bool pgemm_tiles() {
 #endif
 static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, double *SW,
                         double *const S[2], double *piv, int *flag, int G, int r,
-                        hipStream_t st, bool pivot0 = false, hipEvent_t before_gemm = nullptr) {
+                        hipStream_t st, bool pivot0 = false, hipEvent_t before_gemm = nullptr,
+                        bool no_gemm = false) {
   const bool split = panel_split();
   double *const SWb[2] = {SW, SW + SUB * SUB};  // ping-pong by sub-step
   for (int s = 0; s < ((ACE_DIAG_SKIP & 1) ? 0 : NB / SUB); ++s) {
@@ -1657,13 +1758,13 @@ static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, dou
       hipLaunchKernelGGL(k_panel, dim3(NB / SUB), dim3(256), 0, st, W, ld, k0, s, SWb[s & 1],
                          S[s & 1], S[(s + 1) & 1], k0);
   }
-  if (ACE_DIAG_SKIP & 2) return;
+  if ((ACE_DIAG_SKIP & 2) || no_gemm) return;
   // (split cross: the panel rows outside the pivot block come from a launch
   // on the second side stream)
   if (before_gemm) (void)hipStreamWaitEvent(st, before_gemm, 0);
   if (pgemm_tiles())
     hipLaunchKernelGGL(k_panel_gemm_t, dim3((unsigned)(ld / UT), NB / UT), dim3(UTHREADS), 0, st,
-                       W, Pn, ld, k0, G, r);
+                       W, Pn, ld, k0, G, r, 0, 1 << 30, 1 << 30);
   else
     hipLaunchKernelGGL(k_panel_gemm, dim3((unsigned)(ld / SUB)), dim3(512), 0, st, W, Pn, ld, k0,
                        G, r);
@@ -1823,7 +1924,10 @@ int sweep_group() {
   static int v = -1;
   if (v < 0) {
     const char *e = getenv("ACE_GROUP");
-    v = e ? std::min(4, std::max(2, atoi(e))) : 2;
+    // 4 with the head / tail lookahead (run_sweep_heads, default): 75.9
+    // against 76.6 ms per C2 evaluation at 2 (same box, 4 runs each,
+    // profiles/r03_v5_heads_ab.txt)
+    v = e ? std::min(4, std::max(2, atoi(e))) : 4;
   }
   return v;
 }
@@ -1937,6 +2041,55 @@ std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t>
       first = false;
       all.insert(all.end(), o.begin(), o.end());
       off.push_back((int64_t)all.size());
+    }
+  }
+  return all;
+}
+
+// Head / tail split of the group schedule's lookahead (run_sweep_heads).
+// Group G >= 1 (blocks [kb, kb + z)), lists at off[G 2Z + m]:
+//   m = 0          Q: the lower tiles with I and J in the group's blocks
+//   m = 1          the rest of the group's cross (I or J in the group, not in Q)
+//   m = 2 + i      Q_{i+1}: the tiles of Q with J in block kb + i + 1 or later
+//                  (panel kb + i is applied to them as soon as it is final), i < z - 1
+//   m = z + j      T_j: the tiles with I or J in block kb + j minus the head
+//                  H_j = {J in block kb + j, I in blocks [kb + j, kb + z)}, 1 <= j < z
+// Every list is XCD-dealt like the cross lists.
+std::vector<Tile> group_head_tiles(int64_t naug, int steps, int Z, std::vector<int64_t> &off) {
+  const int64_t nT = naug / UT;
+  constexpr int KT = NB / UT;
+  const int ng = (steps + Z - 1) / Z;
+  const int S = update_order_block();
+  std::vector<Tile> all;
+  off.assign((size_t)ng * 2 * Z + 1, 0);
+  auto blk = [&](int64_t t) { return (int)(t / KT); };
+  for (int G = 0; G < ng; ++G) {
+    const int kb = Z * G, z = std::min(Z, steps - kb);
+    std::vector<std::vector<Tile>> L((size_t)2 * Z);
+    if (G > 0) {
+      for (int64_t I = 0; I < nT; ++I)
+        for (int64_t J = 0; J <= I; ++J) {
+          const int bi = blk(I) - kb, bj = blk(J) - kb;  // relative blocks
+          const bool ii = bi >= 0 && bi < z, ij = bj >= 0 && bj < z;
+          const Tile t{(int)I, (int)J};
+          if (ii && ij) {
+            L[0].push_back(t);
+            for (int i = 0; i + 1 < z; ++i)
+              if (bj >= i + 1) L[(size_t)(2 + i)].push_back(t);
+          } else if (ii || ij) {
+            L[1].push_back(t);
+          }
+          for (int j = 1; j < z; ++j) {
+            if (bi != j && bj != j) continue;
+            const bool head = bj == j && bi >= j && bi < z;
+            if (!head) L[(size_t)(z + j)].push_back(t);
+          }
+        }
+    }
+    for (int m = 0; m < 2 * Z; ++m) {
+      const std::vector<Tile> o = S > 0 ? xcd_update_order(L[(size_t)m], S) : L[(size_t)m];
+      all.insert(all.end(), o.begin(), o.end());
+      off[(size_t)G * 2 * Z + m + 1] = (int64_t)all.size();
     }
   }
   return all;
@@ -2321,6 +2474,185 @@ static hipError_t run_sweep_groups(const SweepBufs &b, hipStream_t st, const Swe
   return hipSuccess;
 }
 
+// ACE_HEADS=1: the group schedule with its lookahead split into a head path
+// and a tail path (run_sweep_heads)
+bool heads_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_HEADS");
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
+// The group schedule with the lookahead split by what the next chain needs
+// (lists from group_head_tiles; group g+1 = blocks [kb, kb + z)):
+//   side (head path, the critical one): group g's panels on Q (gathers panel
+//     kb's head rows) -> for each panel k = kb + j: pivot + sub-steps ->
+//     panel GEMM of the rows in blocks (k, kb + z) -> panel k on Q_{j+1}
+//     (gathers panel k + 1's head rows) -> ...  -> ready(g+1)
+//   side2 (tail path): group g's panels on the rest of the cross -> for each
+//     panel k: [after k's sub-steps] the panel GEMM of the other rows ->
+//     [after k's head GEMM] T_{j+1}: panels kb .. k on block k + 1's cross
+//     minus its head -> ... -> ready2(g+1)
+//   main:  wait(ready g, ready2 g) -> the bulk launch of group g.
+// Every tile sees the same panels in the same order with the same per-launch
+// rule as run_sweep_groups, so the result is bit-identical to it; the head
+// path is a chain of small launches (Q: z(z KT + 1) KT / 2 tiles) instead of
+// whole block-column crosses.
+static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
+                                  const SweepTiming *tm) {
+  const int64_t naug = b.ld;
+  const unsigned nT = (unsigned)(naug / UT);
+  constexpr int KT = NB / UT;
+  const int steps = (int)(b.npad / NB);
+  const int Z = b.Z;
+  const int ng = (steps + Z - 1) / Z;
+  hipStream_t side = sy->side, side2 = sy->side2;
+  auto zsize = [&](int g) { return std::min(Z, steps - Z * g); };
+  auto slot = [&](int k) { return k % (2 * Z); };
+  auto E2 = [&](int g) { return sy->ev[2 * steps + 2 + 2 * g]; };     // ready2(g)
+  auto Egh = [&](int k) { return sy->ev[3 * steps + 3 + 2 * k]; };    // panel k's head GEMM done
+  auto Esp = [&](int k) { return sy->ev[3 * steps + 4 + 2 * k]; };    // panel k's sub-steps done
+  auto gout = [&](int k) {
+    return GatherOut{b.P[slot(k)], b.W[slot(k)], b.S[0], (int64_t)k * NB, b.ld};
+  };
+  auto list = [&](int G, int m, const Tile *&p, int64_t &n) {
+    const int64_t i = (int64_t)G * 2 * Z + m;
+    p = b.htiles + b.hoff[i];
+    n = b.hoff[i + 1] - b.hoff[i];
+  };
+  const bool multi2 = multi2_on();
+  auto upd = [&](int npan, int kb, int kx0, int kx1, const Tile *tl, int64_t nt, GatherOut go,
+                 hipStream_t s_) {
+    if (nt <= 0) return;
+    const int64_t ka0 = (int64_t)kb * NB;
+    if (npan == 1) {
+      hipLaunchKernelGGL(k_update, dim3((unsigned)nt), dim3(UTHREADS), 0, s_, b.A, b.ld,
+                         b.W[slot(kb)], b.P[slot(kb)], b.W[slot(kb)], b.ld, ka0, -1, tl, 1, go);
+    } else if (npan == 2 && !multi2) {
+      hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nt), dim3(UTHREADS), 0, s_, b.A, b.ld,
+                         b.W[slot(kb)], b.P[slot(kb)], b.W[slot(kb + 1)], b.P[slot(kb + 1)], b.ld,
+                         ka0, kx0, kx1, tl, go, -1, nullptr, 1, 0);
+    } else {
+      PanelSet ps;
+      for (int j = 0; j < 4; ++j) {
+        ps.R[j] = j < npan ? b.W[slot(kb + j)] : nullptr;
+        ps.C[j] = j < npan ? b.P[slot(kb + j)] : nullptr;
+      }
+      hipLaunchKernelGGL(k_update_multi<false>, dim3((unsigned)nt), dim3(UTHREADS), 0, s_, b.A,
+                         b.ld, ps, npan, b.ld, ka0, kx0, kx1, tl, go, 1);
+    }
+  };
+  // head-path launches on Q lists: 64 x 64 quarters (k_update_q, ACE_HEADQ=1,
+  // default) or the 128-tile kernels
+  static const bool hq = [] {
+    const char *e = getenv("ACE_HEADQ");
+    return !(e && atoi(e) == 0);
+  }();
+  auto qupd = [&](int npan, int kb, const Tile *tl, int64_t nt, GatherOut go, hipStream_t s_) {
+    if (nt <= 0) return;
+    if (!hq) {
+      upd(npan, kb, -1, -1, tl, nt, go, s_);
+      return;
+    }
+    PanelSet ps;
+    for (int j = 0; j < 4; ++j) {
+      ps.R[j] = j < npan ? b.W[slot(kb + j)] : nullptr;
+      ps.C[j] = j < npan ? b.P[slot(kb + j)] : nullptr;
+    }
+    hipLaunchKernelGGL(k_update_q, dim3((unsigned)(4 * nt)), dim3(256), 0, s_, b.A, b.ld, ps, npan,
+                       b.ld, tl, go);
+  };
+  // panel k's GEMM W_i = Pn_i W_kk over row tiles [r0, r1) (head) or all the
+  // others (tail); the kernel itself skips the pivot block's rows
+  auto pgemm = [&](int k, int r0, int r1, bool head, hipStream_t s_) {
+    const int n = head ? r1 - r0 : (int)nT - (r1 - r0);
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_panel_gemm_t, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, s_,
+                       b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, 1, 0, head ? r0 : 0,
+                       head ? 1 << 30 : r0, head ? 1 << 30 : r1);
+  };
+  auto chain = [&](int k, hipStream_t s_) {  // pivot + sub-steps of panel k (gathered)
+    panel_chain(b.P[slot(k)], b.W[slot(k)], b.ld, (int64_t)k * NB, b.SW, b.S, b.piv, b.flag, 1, 0,
+                s_, false, nullptr, true);
+  };
+  hipError_t e;
+  if (!sy->ready_recorded) {
+    e = hipEventRecord(sy->ev[2 * steps], st);  // inputs ready
+    if (e != hipSuccess) return e;
+  }
+  if ((e = hipStreamWaitEvent(side, sy->ev[2 * steps], 0)) != hipSuccess) return e;
+  // group 0 as in run_sweep_groups: its first panel gathered by k_gather,
+  // then each block's full cross and chain
+  {
+    const bool xg = xgather();
+    auto goutx = [&](int k) { return xg ? gout(k) : no_gather(); };
+    if ((e = panel_sweep(b, slot(0), 0, side)) != hipSuccess) return e;
+    for (int j = 1; j < zsize(0); ++j) {
+      const int k = j - 1;
+      const int64_t x0 = b.xoff[k], nx = b.xoff[k + 1] - x0;
+      upd(j, 0, -1, -1, b.xtiles + x0, nx, goutx(j), side);
+      if ((e = panel_sweep(b, slot(j), (int64_t)j * NB, side, xg)) != hipSuccess) return e;
+    }
+    if ((e = hipEventRecord(sy->ev[0], side)) != hipSuccess) return e;
+  }
+  int used = 0;
+  for (int g = 0; g < ng; ++g) {
+    const int kg = Z * g;
+    const bool more = g + 1 < ng;
+    const int kb = Z * (g + 1), zb = more ? zsize(g + 1) : 0;
+    if ((e = hipStreamWaitEvent(st, sy->ev[2 * g], 0)) != hipSuccess) return e;
+    if (g > 0 && (e = hipStreamWaitEvent(st, E2(g), 0)) != hipSuccess) return e;
+    if (more) {
+      if ((e = hipEventRecord(sy->ev[2 * g + 1], st)) != hipSuccess) return e;  // bulk g-1 done
+      if ((e = hipStreamWaitEvent(side, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(side2, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
+      const Tile *tl;
+      int64_t nt;
+      list(g + 1, 0, tl, nt);
+      qupd(zsize(g), kg, tl, nt, gout(kb), side);  // Q
+      list(g + 1, 1, tl, nt);
+      upd(zsize(g), kg, -1, -1, tl, nt, gout(kb), side2);  // the rest of the cross
+      const int hend = (kb + zb) * KT;  // head rows end (row tiles)
+      for (int j = 0; j < zb; ++j) {
+        const int k = kb + j;
+        chain(k, side);
+        if ((e = hipEventRecord(Esp(k), side)) != hipSuccess) return e;
+        pgemm(k, (k + 1) * KT, hend, true, side);
+        if ((e = hipEventRecord(Egh(k), side)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(side2, Esp(k), 0)) != hipSuccess) return e;
+        pgemm(k, (k + 1) * KT, hend, false, side2);
+        if (j + 1 < zb) {
+          list(g + 1, 2 + j, tl, nt);
+          qupd(1, k, tl, nt, gout(k + 1), side);  // panel k on Q_{j+1}
+          if ((e = hipStreamWaitEvent(side2, Egh(k), 0)) != hipSuccess) return e;
+          list(g + 1, zb + j + 1, tl, nt);
+          upd(j + 1, kb, -1, -1, tl, nt, gout(k + 1), side2);  // T_{j+1}
+        }
+      }
+      if ((e = hipEventRecord(sy->ev[2 * (g + 1)], side)) != hipSuccess) return e;
+      if ((e = hipEventRecord(E2(g + 1), side2)) != hipSuccess) return e;
+    }
+    const bool timed = tm && tm->ev && used + 2 <= tm->nev;
+    if (timed) (void)hipEventRecord(tm->ev[used], st);
+    const int64_t grid = b.gorder ? b.glen : (b.order ? b.norder : (int64_t)nT * (nT + 1) / 2);
+    const Tile *ord = b.gorder ? b.gorder + (int64_t)g * b.glen : b.order;
+    const int kx0 = more ? kb : -1, kx1 = more ? kb + zb : -1;
+    upd(zsize(g), kg, kx0, kx1, ord, grid, no_gather(), st);
+    if (timed) {
+      (void)hipEventRecord(tm->ev[used + 1], st);
+      if (tm->flops)
+        tm->flops[used / 2] =
+            update_gemm_tiles_group(naug, (int64_t)kg * NB, zsize(g), kx0, kx1) * 2.0 * UT * UT * NB;
+      used += 2;
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (tm && tm->used) *tm->used = used;
+  return hipSuccess;
+}
+
 hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
                      const SweepTiming *tm) {
   if (pair_steps() && b.ptiles && b.xtiles && b.P[2] && b.npad / NB >= 2) {
@@ -2331,6 +2663,9 @@ hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
       const char *e = getenv("ACE_GROUP_SCHED");
       return !(e && atoi(e) == 0);
     }();
+    if (b.P[2 * b.Z - 1] && b.htiles && heads_on() && sy && sy->side && sy->side2 &&
+        sy->nev >= 5 * (int)(b.npad / NB) + 3)
+      return run_sweep_heads(b, st, sy, tm);
     if (b.P[2 * b.Z - 1] && (b.Z > 2 || (gs && !b.morder && !xsplit_cross())))
       return run_sweep_groups(b, st, sy, tm);
     return run_sweep_pairs(b, st, sy, tm);

@@ -391,9 +391,12 @@ def main():
         rp_ms, rp_src = rocprof_bulk_avg()
         naug = -(-n // 256) * 256 + 128
         nt = naug // 128
+        # sweep steps per bulk launch, from the launch count (steps / groups)
+        nsteps = -(-n // 256)
+        zst = max(1, round(nsteps / (upd_n / a.steps))) if upd_n else 4
         # compulsory bytes of one bulk launch: every lower 128-tile of A read
-        # and written once, plus the two steps' W and Pn panels
-        alg_bytes = nt * (nt + 1) // 2 * 128 * 128 * 8 * 2 + 4 * naug * 256 * 8
+        # and written once, plus the Z steps' W and Pn panels
+        alg_bytes = nt * (nt + 1) // 2 * 128 * 128 * 8 * 2 + 2 * zst * naug * 256 * 8
         evals = a.steps * world
         value = evals / dt_max
         achieved = upd_work / (upd_ms * 1e-3) / 1e12 if upd_ms > 0 else None
@@ -418,8 +421,8 @@ def main():
                 "parallelism": "single" if world == 1 else f"replicas x{world}",
             },
             "roofline": {
-                "kernel": ("k_update_multi (bulk sweep update, two Gauss-Jordan steps per launch, "
-                           "K = 512 per 128x128 tile, v_mfma_f64_16x16x4_f64)"),
+                "kernel": (f"k_update_multi (bulk sweep update, {zst} Gauss-Jordan steps per launch, "
+                           f"K = {256 * zst} per 128x128 tile, v_mfma_f64_16x16x4_f64)"),
                 "bound": "mfma",
                 "achieved": achieved,
                 "peak": FP64_MFMA_PEAK_TFLOPS,

@@ -490,7 +490,9 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     fused gather) instead of side-stream launches.  Three and four steps per
     bulk launch (ACE_GROUP=3 / 4, k_update_multi; groups 3+2 / 4+1 at n =
     1100, 3+3 / 4+2 at 1500, 3+3+3+2 / 4+4+3 at 2600) are bit-identical too,
-    with and without the fused gather, the second side stream and lookahead."""
+    with and without the fused gather, the second side stream and lookahead,
+    and so is the head / tail split of the group lookahead (ACE_HEADS=1 at
+    Z = 2, 3, 4)."""
     import os
     import subprocess
     import sys
@@ -501,23 +503,32 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     inp = str(tmp_path / "k.npz")
     np.savez(inp, K=K, s=th[0])
     outs = {}
-    variants = {"single": {"ACE_PAIR": "0"}, "pair": {"ACE_PAIR": "1"},
-                "one_side": {"ACE_PAIR": "1", "ACE_SIDE2": "0"},
-                "tail": {"ACE_PAIR": "1", "ACE_TAIL_SORT": "1"},
-                "gather": {"ACE_PAIR": "1", "ACE_XGATHER": "0"},
-                "one_stream": {"ACE_PAIR": "1", "ACE_LOOKAHEAD": "0"},
-                "pgemm_rows": {"ACE_PAIR": "1", "ACE_PGEMM_TILES": "0"},
+    z2 = {"ACE_GROUP": "2", "ACE_HEADS": "0"}  # the round-2 / round-3 Z = 2 schedules
+    variants = {"single": {"ACE_PAIR": "0"}, "pair": {"ACE_PAIR": "1", **z2},
+                "one_side": {"ACE_PAIR": "1", "ACE_SIDE2": "0", **z2},
+                "tail": {"ACE_PAIR": "1", "ACE_TAIL_SORT": "1", **z2},
+                "gather": {"ACE_PAIR": "1", "ACE_XGATHER": "0", **z2},
+                "one_stream": {"ACE_PAIR": "1", "ACE_LOOKAHEAD": "0", **z2},
+                "pgemm_rows": {"ACE_PAIR": "1", "ACE_PGEMM_TILES": "0", **z2},
                 "single_pgemm_rows": {"ACE_PAIR": "0", "ACE_PGEMM_TILES": "0"},
-                "merged": {"ACE_PAIR": "1", "ACE_XMERGE": "1"},
-                "merged_gather": {"ACE_PAIR": "1", "ACE_XMERGE": "1", "ACE_XGATHER": "0"},
-                "unmerged": {"ACE_PAIR": "1", "ACE_XMERGE": "0"},
-                "xsplit": {"ACE_PAIR": "1", "ACE_XSPLIT": "1"},
-                "pair_kernel": {"ACE_MULTI2": "0"}, "pair_schedule": {"ACE_GROUP_SCHED": "0"},
-                "group3": {"ACE_GROUP": "3"}, "group4": {"ACE_GROUP": "4"},
-                "group4_gather": {"ACE_GROUP": "4", "ACE_XGATHER": "0"},
-                "group4_one_side": {"ACE_GROUP": "4", "ACE_SIDE2": "0"},
-                "group4_one_stream": {"ACE_GROUP": "4", "ACE_LOOKAHEAD": "0"},
-                "group3_untail": {"ACE_GROUP": "3", "ACE_TAIL_SORT": "0"}}
+                "merged": {"ACE_PAIR": "1", "ACE_XMERGE": "1", **z2},
+                "merged_gather": {"ACE_PAIR": "1", "ACE_XMERGE": "1", "ACE_XGATHER": "0", **z2},
+                "unmerged": {"ACE_PAIR": "1", "ACE_XMERGE": "0", **z2},
+                "xsplit": {"ACE_PAIR": "1", "ACE_XSPLIT": "1", **z2},
+                "pair_kernel": {"ACE_MULTI2": "0", **z2},
+                "pair_schedule": {"ACE_GROUP_SCHED": "0", **z2},
+                "group3": {"ACE_GROUP": "3", "ACE_HEADS": "0"},
+                "group4": {"ACE_GROUP": "4", "ACE_HEADS": "0"},
+                "group4_gather": {"ACE_GROUP": "4", "ACE_HEADS": "0", "ACE_XGATHER": "0"},
+                "group4_one_side": {"ACE_GROUP": "4", "ACE_HEADS": "0", "ACE_SIDE2": "0"},
+                "group4_one_stream": {"ACE_GROUP": "4", "ACE_HEADS": "0", "ACE_LOOKAHEAD": "0"},
+                "group3_untail": {"ACE_GROUP": "3", "ACE_HEADS": "0", "ACE_TAIL_SORT": "0"},
+                "heads2": {"ACE_GROUP": "2", "ACE_HEADS": "1"},
+                "heads3": {"ACE_GROUP": "3", "ACE_HEADS": "1"},
+                "heads4": {"ACE_GROUP": "4", "ACE_HEADS": "1"}, "default": {},
+                "heads4_pair": {"ACE_GROUP": "4", "ACE_HEADS": "1", "ACE_MULTI2": "0"},
+                "heads4_q128": {"ACE_GROUP": "4", "ACE_HEADS": "1", "ACE_HEADQ": "0"},
+                "heads3_q128": {"ACE_GROUP": "3", "ACE_HEADS": "1", "ACE_HEADQ": "0"}}
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)
@@ -597,10 +608,14 @@ def test_merged_cross_model_is_bitwise_neutral(tmp_path, n):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
-    for v in ("0", "1", "split", "group4"):
+    z2 = dict(ACE_GROUP="2", ACE_HEADS="0")  # the merged / split cross are Z = 2 schedules
+    for v in ("0", "1", "split", "group4", "heads4", "heads2"):
         out = str(tmp_path / f"m{v}.npy")
-        env = (dict(os.environ, ACE_XSPLIT="1") if v == "split" else
-               dict(os.environ, ACE_GROUP="4") if v == "group4" else dict(os.environ, ACE_XMERGE=v))
+        env = (dict(os.environ, ACE_XSPLIT="1", **z2) if v == "split" else
+               dict(os.environ, ACE_GROUP="4", ACE_HEADS="0") if v == "group4" else
+               dict(os.environ, ACE_GROUP="4", ACE_HEADS="1") if v == "heads4" else
+               dict(os.environ, ACE_GROUP="2", ACE_HEADS="1") if v == "heads2" else
+               dict(os.environ, ACE_XMERGE=v, **z2))
         subprocess.run([sys.executable, "-c", _MODEL_SNIPPET.format(root=root, n=n, out=out)],
                        env=env, check=True, timeout=100)
         outs[v] = np.load(out)
@@ -610,3 +625,6 @@ def test_merged_cross_model_is_bitwise_neutral(tmp_path, n):
     # four steps per bulk launch: the assembly's first part covers the first
     # group's four panels, its side path runs under the rest
     assert np.array_equal(outs["0"], outs["group4"])
+    # the head / tail lookahead split (ACE_HEADS=1) at four and two steps
+    assert np.array_equal(outs["0"], outs["heads4"])
+    assert np.array_equal(outs["0"], outs["heads2"])
