@@ -1560,31 +1560,30 @@ __global__ __launch_bounds__(256) void k_update_q(double *__restrict__ A, int64_
       for (int j = 0; j < 4; ++j) acc[ci][ri][j] = A[r + (c + 4 * j) * ld];
     }
   const int sk = tid >> 4, sm = (tid & 15) * 4;
+  // staging registers as named values (an array here was kept in scratch)
+  double2 w0, w1, p0, p1;
   for (int pj = 0; pj < npan; ++pj) {
     const double *gW = psel(ps.R, pj) + (R0 + sm) + (int64_t)sk * ldp;
     const double *gP = psel(ps.C, pj) + (C0 + sm) + (int64_t)sk * ldp;
-    double2 rw[2], rp[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      rw[e] = *reinterpret_cast<const double2 *>(gW + 2 * e);
-      rp[e] = *reinterpret_cast<const double2 *>(gP + 2 * e);
-    }
+    w0 = *reinterpret_cast<const double2 *>(gW);
+    w1 = *reinterpret_cast<const double2 *>(gW + 2);
+    p0 = *reinterpret_cast<const double2 *>(gP);
+    p1 = *reinterpret_cast<const double2 *>(gP + 2);
     __syncthreads();  // the previous panel's last chunk is consumed
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2 * e]) = rw[e];
-      *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2 * e]) = rp[e];
-    }
+    *reinterpret_cast<double2 *>(&sW[0][sk][sm]) = w0;
+    *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2]) = w1;
+    *reinterpret_cast<double2 *>(&sP[0][sk][sm]) = p0;
+    *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2]) = p1;
     __syncthreads();
+#pragma unroll 2
     for (int ch = 0; ch < NCH; ++ch) {
       const int cur = ch & 1;
       if (ch + 1 < NCH) {
         const int64_t off = (int64_t)(ch + 1) * BK * ldp;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          rw[e] = *reinterpret_cast<const double2 *>(gW + off + 2 * e);
-          rp[e] = *reinterpret_cast<const double2 *>(gP + off + 2 * e);
-        }
+        w0 = *reinterpret_cast<const double2 *>(gW + off);
+        w1 = *reinterpret_cast<const double2 *>(gW + off + 2);
+        p0 = *reinterpret_cast<const double2 *>(gP + off);
+        p1 = *reinterpret_cast<const double2 *>(gP + off + 2);
       }
 #pragma unroll
       for (int kk = 0; kk < BK / 4; ++kk) {
@@ -1600,11 +1599,10 @@ __global__ __launch_bounds__(256) void k_update_q(double *__restrict__ A, int64_
             acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
       }
       if (ch + 1 < NCH) {
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2 * e]) = rw[e];
-          *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2 * e]) = rp[e];
-        }
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm]) = w0;
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2]) = w1;
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm]) = p0;
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2]) = p1;
       }
       __syncthreads();
     }
@@ -2585,6 +2583,9 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   if ((e = hipStreamWaitEvent(side, sy->ev[2 * steps], 0)) != hipSuccess) return e;
   // group 0 as in run_sweep_groups: its first panel gathered by k_gather,
   // then each block's full cross and chain
+  // (a non-fused split kernel -- k_pivot for every sub-step, 112 registers,
+  // 73 KB of LDS -- did not get these chains beside the assembly's second
+  // part either: neutral, profiles/r03_v5_heads_ab.txt)
   {
     const bool xg = xgather();
     auto goutx = [&](int k) { return xg ? gout(k) : no_gather(); };
