@@ -258,7 +258,13 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
 // Wave w owns rows 16w..16w+15.  Phase 1 forms Vn^T = -V^T = SW W_is^T
 // (SW is symmetric) so that its accumulator fragments are directly the B
 // operands of phase 2's D = S_chunk^T Vn^T + W_chunk^T (no LDS round trip).
-constexpr int PLD = 80;  // LDS pitch for sSW: 64 + 16 doubles, conflict-free fragment reads
+// LDS pitch for sSW: 64 + 16 doubles, conflict-free fragment reads
+// (ACE_PLD=72: the split kernel's LDS fits 72 KB, the hole one finished
+// bulk-update workgroup leaves -- A/B switch)
+#ifndef ACE_PLD
+#define ACE_PLD 80
+#endif
+constexpr int PLD = ACE_PLD;
 constexpr int SLD = 66;  // LDS pitch for the transposed S chunk (c-major)
 
 __global__ __launch_bounds__(256) void k_panel(double *__restrict__ W, int64_t ldp, int64_t k0,
