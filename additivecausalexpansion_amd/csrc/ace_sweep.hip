@@ -2051,7 +2051,7 @@ std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t>
 }
 
 // Head / tail split of the group schedule's lookahead (run_sweep_heads).
-// Group G >= 1 (blocks [kb, kb + z)), lists at off[G 2Z + m]:
+// Group G (blocks [kb, kb + z)), lists at off[G 2Z + m] (m = 0, 1 unused for G = 0):
 //   m = 0          Q: the lower tiles with I and J in the group's blocks
 //   m = 1          the rest of the group's cross (I or J in the group, not in Q)
 //   m = 2 + i      Q_{i+1}: the tiles of Q with J in block kb + i + 1 or later
@@ -2070,7 +2070,7 @@ std::vector<Tile> group_head_tiles(int64_t naug, int steps, int Z, std::vector<i
   for (int G = 0; G < ng; ++G) {
     const int kb = Z * G, z = std::min(Z, steps - kb);
     std::vector<std::vector<Tile>> L((size_t)2 * Z);
-    if (G > 0) {
+    {  // (group 0 uses only m >= 2)
       for (int64_t I = 0; I < nT; ++I)
         for (int64_t J = 0; J <= I; ++J) {
           const int bi = blk(I) - kb, bj = blk(J) - kb;  // relative blocks
@@ -2587,59 +2587,62 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
     if (e != hipSuccess) return e;
   }
   if ((e = hipStreamWaitEvent(side, sy->ev[2 * steps], 0)) != hipSuccess) return e;
-  // group 0 as in run_sweep_groups: its first panel gathered by k_gather,
-  // then each block's full cross and chain
-  // (a non-fused split kernel -- k_pivot for every sub-step, 112 registers,
-  // 73 KB of LDS -- did not get these chains beside the assembly's second
-  // part either: neutral, profiles/r03_v5_heads_ab.txt)
-  {
-    const bool xg = xgather();
-    auto goutx = [&](int k) { return xg ? gout(k) : no_gather(); };
-    if ((e = panel_sweep(b, slot(0), 0, side)) != hipSuccess) return e;
-    for (int j = 1; j < zsize(0); ++j) {
-      const int k = j - 1;
-      const int64_t x0 = b.xoff[k], nx = b.xoff[k + 1] - x0;
-      upd(j, 0, -1, -1, b.xtiles + x0, nx, goutx(j), side);
-      if ((e = panel_sweep(b, slot(j), (int64_t)j * NB, side, xg)) != hipSuccess) return e;
+  // group G's lookahead: group G-1's panels on Q (side) and on the rest of
+  // the group's cross (side2), then each panel's chain, head / tail GEMMs
+  // and the next head / tail updates.  Group 0 has no previous panels: its
+  // first panel is gathered by k_gather.  (A non-fused split kernel -- k_pivot
+  // for every sub-step, 112 registers, 73 KB of LDS -- did not get group 0's
+  // chains beside the assembly's second part: neutral,
+  // profiles/r03_v5_heads_ab.txt.)
+  auto produce = [&](int G) -> hipError_t {
+    const int kb = Z * G, zb = zsize(G);
+    const Tile *tl;
+    int64_t nt;
+    if (G == 0) {
+      hipLaunchKernelGGL(k_gather<false>, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, side,
+                         b.A, b.ld, (int64_t)0, b.P[slot(0)], b.W[slot(0)], b.ld, b.S[0], nullptr,
+                         nullptr, nullptr);
+    } else {
+      list(G, 0, tl, nt);
+      qupd(zsize(G - 1), Z * (G - 1), tl, nt, gout(kb), side);  // Q
+      list(G, 1, tl, nt);
+      upd(zsize(G - 1), Z * (G - 1), -1, -1, tl, nt, gout(kb), side2);  // the rest of the cross
     }
-    if ((e = hipEventRecord(sy->ev[0], side)) != hipSuccess) return e;
-  }
+    hipError_t r;
+    const int hend = (kb + zb) * KT;  // head rows end (row tiles)
+    for (int j = 0; j < zb; ++j) {
+      const int k = kb + j;
+      chain(k, side);
+      if ((r = hipEventRecord(Esp(k), side)) != hipSuccess) return r;
+      pgemm(k, (k + 1) * KT, hend, true, side);
+      if ((r = hipEventRecord(Egh(k), side)) != hipSuccess) return r;
+      if ((r = hipStreamWaitEvent(side2, Esp(k), 0)) != hipSuccess) return r;
+      pgemm(k, (k + 1) * KT, hend, false, side2);
+      if (j + 1 < zb) {
+        list(G, 2 + j, tl, nt);
+        qupd(1, k, tl, nt, gout(k + 1), side);  // panel k on Q_{j+1}
+        if ((r = hipStreamWaitEvent(side2, Egh(k), 0)) != hipSuccess) return r;
+        list(G, zb + j + 1, tl, nt);
+        upd(j + 1, kb, -1, -1, tl, nt, gout(k + 1), side2);  // T_{j+1}
+      }
+    }
+    if ((r = hipEventRecord(sy->ev[2 * G], side)) != hipSuccess) return r;
+    return hipEventRecord(E2(G), side2);
+  };
+  if ((e = hipStreamWaitEvent(side2, sy->ev[2 * steps], 0)) != hipSuccess) return e;
+  if ((e = produce(0)) != hipSuccess) return e;
   int used = 0;
   for (int g = 0; g < ng; ++g) {
     const int kg = Z * g;
     const bool more = g + 1 < ng;
     const int kb = Z * (g + 1), zb = more ? zsize(g + 1) : 0;
     if ((e = hipStreamWaitEvent(st, sy->ev[2 * g], 0)) != hipSuccess) return e;
-    if (g > 0 && (e = hipStreamWaitEvent(st, E2(g), 0)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(st, E2(g), 0)) != hipSuccess) return e;
     if (more) {
       if ((e = hipEventRecord(sy->ev[2 * g + 1], st)) != hipSuccess) return e;  // bulk g-1 done
       if ((e = hipStreamWaitEvent(side, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
       if ((e = hipStreamWaitEvent(side2, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
-      const Tile *tl;
-      int64_t nt;
-      list(g + 1, 0, tl, nt);
-      qupd(zsize(g), kg, tl, nt, gout(kb), side);  // Q
-      list(g + 1, 1, tl, nt);
-      upd(zsize(g), kg, -1, -1, tl, nt, gout(kb), side2);  // the rest of the cross
-      const int hend = (kb + zb) * KT;  // head rows end (row tiles)
-      for (int j = 0; j < zb; ++j) {
-        const int k = kb + j;
-        chain(k, side);
-        if ((e = hipEventRecord(Esp(k), side)) != hipSuccess) return e;
-        pgemm(k, (k + 1) * KT, hend, true, side);
-        if ((e = hipEventRecord(Egh(k), side)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(side2, Esp(k), 0)) != hipSuccess) return e;
-        pgemm(k, (k + 1) * KT, hend, false, side2);
-        if (j + 1 < zb) {
-          list(g + 1, 2 + j, tl, nt);
-          qupd(1, k, tl, nt, gout(k + 1), side);  // panel k on Q_{j+1}
-          if ((e = hipStreamWaitEvent(side2, Egh(k), 0)) != hipSuccess) return e;
-          list(g + 1, zb + j + 1, tl, nt);
-          upd(j + 1, kb, -1, -1, tl, nt, gout(k + 1), side2);  // T_{j+1}
-        }
-      }
-      if ((e = hipEventRecord(sy->ev[2 * (g + 1)], side)) != hipSuccess) return e;
-      if ((e = hipEventRecord(E2(g + 1), side2)) != hipSuccess) return e;
+      if ((e = produce(g + 1)) != hipSuccess) return e;
     }
     const bool timed = tm && tm->ev && used + 2 <= tm->nev;
     if (timed) (void)hipEventRecord(tm->ev[used], st);
