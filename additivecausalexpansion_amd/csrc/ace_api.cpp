@@ -2,6 +2,7 @@
 // argument checking, layout packing, the drop-in Rcpp-export equivalents
 // and the device-resident para_update pipeline.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <chrono>
@@ -65,6 +66,22 @@ int ace_create(int device, ace_ctx **out) {
     e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, p1);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, p2);
   }
+  if (e == hipSuccess) {
+    // ACE_ASM_RESERVE=R (multiple of 8): the assembly's second part leaves
+    // R CUs free -- mask bits 0..7 are CU 0 of XCDs 0..7 (tools/probe_cumask.hip,
+    // profiles/r01_cumask_probe.txt) -- for the first group's pivot chains,
+    // which get no slot beside the assembly kernel otherwise
+    const char *v = getenv("ACE_ASM_RESERVE");
+    const int R = v ? atoi(v) : ASM_RESERVE_DEFAULT;
+    hipDeviceProp_t prop;
+    if (R > 0 && hipGetDeviceProperties(&prop, device) == hipSuccess &&
+        R < prop.multiProcessorCount) {
+      const int ncu = prop.multiProcessorCount;
+      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+      for (int i = R; i < ncu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+      e = hipExtStreamCreateWithCUMask(&c->asm2, (uint32_t)ncu, mask.data());
+    }
+  }
   if (e != hipSuccess) {
     g_create_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
     delete c;
@@ -80,6 +97,7 @@ void ace_destroy(ace_ctx *ctx) {
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->side2) (void)hipStreamDestroy(ctx->side2);
+  if (ctx->asm2) (void)hipStreamDestroy(ctx->asm2);
   delete ctx;
 }
 
@@ -432,9 +450,20 @@ void assemble_and_sweep(ace_ctx *ctx, SweepWork &w, const Shape &s, const PairSi
     ck(ctx, hipEventRecord(sy.ev[2 * steps], st), "event");
     sy.ready_recorded = true;
   }
+  // the second part on the CU-masked stream (ctx->asm2): the first group's
+  // chains run on the reserved CUs meanwhile; its tail path waits (asm_done)
+  const bool a2 = ctx->asm2 && sy.side && sy.nev >= 5 * steps + 6;
+  if (a2) {
+    ck(ctx, hipStreamWaitEvent(ctx->asm2, sy.ev[2 * steps], 0), "wait");
+    sy.asm_done = sy.ev[5 * steps + 5];
+  }
   ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
-                          nullptr, st, nullptr, 0, 1, 2),
+                          nullptr, a2 ? ctx->asm2 : st, nullptr, 0, 1, 2),
      "assembly");
+  if (a2) {
+    ck(ctx, hipEventRecord(sy.asm_done, ctx->asm2), "event");
+    ck(ctx, hipStreamWaitEvent(st, sy.asm_done, 0), "wait");
+  }
   if (ev_asm) ck(ctx, hipEventRecord(ev_asm[1], st), "event");
   ck(ctx, run_sweep(w.bufs(), st, &sy, tmg), "sweep");
 }

@@ -208,6 +208,11 @@ std::vector<Tile> own_tiles(int64_t ntile, int T, int G, int r);
 // super-block size S of that order (0: row-major grid); ACE_UPD_ORDER=S
 // overrides (diagnostic A/B switch)
 int update_order_block();
+// CUs the assembly's second part leaves to the first sweep group's chains
+// (ACE_ASM_RESERVE overrides; 0: one unmasked stream).  8 (CU 0 of every
+// XCD): 74.9 against 75.5 ms per C2 evaluation, the assembly 2.35 -> 2.62 ms
+// but the first group's four chains under it (profiles/r03_v8_reserve_ab.txt)
+constexpr int ASM_RESERVE_DEFAULT = 8;
 // Lookahead: the panel sweep of step k+1 runs on `side` while the main
 // stream updates the rest of step k.  `ev` needs 2*steps + 1 events.
 struct SweepSync {
@@ -216,6 +221,10 @@ struct SweepSync {
   hipEvent_t *ev;
   int nev;
   bool ready_recorded = false;  // caller already recorded ev[2 * steps] ("inputs ready")
+  // the assembly's second part ran on ctx->asm2: done when this event is
+  // (run_sweep_heads holds the first group's tail path until then, so the
+  // reserved CUs serve its head path); null: the assembly is on the main stream
+  hipEvent_t asm_done = nullptr;
 };
 // Optional timing of the dominant update launches (k_update<false>): event
 // pairs in ev, executed GEMM flops per timed launch in flops[].

@@ -2,7 +2,8 @@
 """Bitwise comparison of two builds of libace_hip.so on the fused model:
 two para_update evaluations (gradient, stats, mu) at a C2-shaped problem,
 each build in its own process (ACE_LIB_PATH).  Used for bit-identical A/B
-switches.  usage: python tools/cmp_libs.py libA.so libB.so [n] [kernel]"""
+switches.  usage: python tools/cmp_libs.py libA.so libB.so [n] [kernel]; CMP_ENV_B="K=V ..."
+sets environment switches for the second run only."""
 import os
 import subprocess
 import sys
@@ -37,6 +38,8 @@ def main():
         for i, lib in enumerate((a, b)):
             out = os.path.join(d, f"o{i}.npy")
             env = dict(os.environ, ACE_LIB_PATH=os.path.abspath(lib))
+            if i == 1 and os.environ.get("CMP_ENV_B"):  # "K=V ..." for the second run only
+                env.update(kv.split("=", 1) for kv in os.environ["CMP_ENV_B"].split())
             subprocess.run([sys.executable, "-c", SNIP.format(root=ROOT, n=n, kernel=kernel, out=out)],
                            env=env, check=True, timeout=120)
             res.append(np.load(out))
