@@ -239,6 +239,10 @@ struct SweepTiming {
 hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sync,
                      const SweepTiming *timing);
 double update_gemm_tiles(int64_t naug, int64_t k0, int kx, bool look);
+// every GEMM flop of one sweep, whatever the schedule: each step's update of
+// every lower tile outside its block (bulk + lookahead crosses) and its panel
+// GEMM W_i = Pn_i W_kk
+double sweep_flops(int64_t naug, int64_t npad);
 
 // ---- sharded sweep (one rank's view; ace_shard.cpp drives the steps) --------
 // Step k on rank r:  shard_pack -> [exchange: broadcast `low` from rank k%G,

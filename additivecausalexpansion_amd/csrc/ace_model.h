@@ -174,9 +174,12 @@ struct ace_model {
   std::vector<double> upd_flops;   // 2 sets x steps
   int upd_used[2] = {0, 0};
   int tset = 0, pend = -1;  // set the next timed evaluation records; set not yet read
-  double t_ms[3] = {0, 0, 0};
-  int64_t t_launch[3] = {0, 0, 0};
-  double t_work[3] = {0, 0, 0};
+  // [0] bulk update launches, [1] assembly, [2] gradient, [3] the sweep's
+  // span (first bulk launch start -> last bulk launch end, every update /
+  // cross / panel-GEMM flop of the sweep as its work)
+  double t_ms[4] = {0, 0, 0, 0};
+  int64_t t_launch[4] = {0, 0, 0, 0};
+  double t_work[4] = {0, 0, 0, 0};
   ShardModel *shard = nullptr;  // block-column-sharded model (ace_shard.cpp)
 };
 

@@ -1835,6 +1835,20 @@ double update_gemm_tiles(int64_t naug, int64_t k0, int kx, bool look) {
   return cnt;
 }
 
+double sweep_flops(int64_t naug, int64_t npad) {
+  thread_local int64_t cn = -1, cp = -1;
+  thread_local double cf = 0.0;
+  if (naug == cn && npad == cp) return cf;
+  double f = 0.0;
+  for (int64_t k0 = 0; k0 < npad; k0 += NB)
+    f += update_gemm_tiles(naug, k0, -1, false) * 2.0 * UT * UT * NB +
+         2.0 * (double)(naug - NB) * NB * NB;
+  cn = naug;
+  cp = npad;
+  cf = f;
+  return f;
+}
+
 int update_order_block() {
   static int v = -1;
   if (v < 0) {

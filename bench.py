@@ -373,6 +373,7 @@ def main():
     upd_ms, upd_n, upd_work = model.kernel_time(0)
     asm_ms, _, asm_work = model.kernel_time(1)
     grad_ms, _, grad_work = model.kernel_time(2)
+    sweep_ms, sweep_n, sweep_work = model.kernel_time(3)
     model.profile(False)
     pred = predict_leg(step.kernel_object, model, p, B) if rank == 0 else None
     r6 = None
@@ -437,6 +438,13 @@ def main():
                 "launches": upd_n,
                 "avg_launch_ms": upd_ms / upd_n if upd_n else None,
                 "algorithmic_flops_per_launch": upd_work / upd_n if upd_n else None,
+                # the sweep as a whole: every update / cross / panel-GEMM flop
+                # over the span from the first bulk launch's start to the last
+                # one's end (the side streams' work runs inside it), per evaluation
+                "sweep_span_ms": sweep_ms / sweep_n if sweep_n else None,
+                "sweep_achieved": (sweep_work / (sweep_ms * 1e-3) / 1e12) if sweep_ms > 0 else None,
+                "sweep_frac": ((sweep_work / (sweep_ms * 1e-3) / 1e12) / FP64_MFMA_PEAK_TFLOPS
+                               if sweep_ms > 0 else None),
             },
             "dense_gflops_per_eval_wall": (n ** 3) / (dt_max / a.steps) / 1e9,
             "phase_ms_per_step": {"update_kernel": upd_ms / a.steps,

@@ -285,7 +285,10 @@ int ace_model_predict_marginal(ace_model *m, const double *theta, int64_t nx, co
  * events bracket every launch of the dense update kernel (`which` = 0),
  * the assembly kernel (1) and the gradient kernel (2) on the model's
  * stream.  *ms = summed duration, *launches = count, *work = algorithmic
- * flops issued by those launches.  Enabling resets the
+ * flops issued by those launches.  `which` = 3: the
+ * sweep's span per evaluation (first bulk update launch start to the last
+ * one's end) with every update / cross / panel-GEMM flop of the sweep as
+ * its work (unsharded models).  Enabling resets the
  * counters.  An evaluation's events are read back while the next one runs
  * (no host queries between evaluations); ace_model_kernel_time reads the
  * last timed evaluation's set first, so its totals cover every timed
