@@ -79,7 +79,11 @@ int ace_create(int device, ace_ctx **out) {
       const int ncu = prop.multiProcessorCount;
       std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
       for (int i = R; i < ncu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
-      e = hipExtStreamCreateWithCUMask(&c->asm2, (uint32_t)ncu, mask.data());
+      // an optimisation only: without it the assembly runs on the main stream
+      if (hipExtStreamCreateWithCUMask(&c->asm2, (uint32_t)ncu, mask.data()) != hipSuccess) {
+        c->asm2 = nullptr;
+        (void)hipGetLastError();
+      }
     }
   }
   if (e != hipSuccess) {
