@@ -602,16 +602,18 @@ def test_merged_cross_model_is_bitwise_neutral(tmp_path, n):
     head of the bulk launch (ACE_XMERGE=1: device counter + side-stream wait
     kernel) gives the same gradient and stats bit for bit as the side-stream
     cross launches, over two evaluations (the per-sweep counter reset).
-    n = 2000: 8 steps; 2600: 11 (a last single step)."""
+    n = 2000: 8 steps; 2600: 11 (a last single step).  Also the default
+    schedule with its assembly on one unmasked stream (ACE_ASM_RESERVE=0)."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
     z2 = dict(ACE_GROUP="2", ACE_HEADS="0")  # the merged / split cross are Z = 2 schedules
-    for v in ("0", "1", "split", "group4", "heads4", "heads2"):
+    for v in ("0", "1", "split", "group4", "heads4", "heads2", "noreserve"):
         out = str(tmp_path / f"m{v}.npy")
         env = (dict(os.environ, ACE_XSPLIT="1", **z2) if v == "split" else
+               dict(os.environ, ACE_ASM_RESERVE="0") if v == "noreserve" else
                dict(os.environ, ACE_GROUP="4", ACE_HEADS="0") if v == "group4" else
                dict(os.environ, ACE_GROUP="4", ACE_HEADS="1") if v == "heads4" else
                dict(os.environ, ACE_GROUP="2", ACE_HEADS="1") if v == "heads2" else
@@ -628,3 +630,5 @@ def test_merged_cross_model_is_bitwise_neutral(tmp_path, n):
     # the head / tail lookahead split (ACE_HEADS=1) at four and two steps
     assert np.array_equal(outs["0"], outs["heads4"])
     assert np.array_equal(outs["0"], outs["heads2"])
+    # the default's assembly on the CU-masked stream against one unmasked stream
+    assert np.array_equal(outs["heads4"], outs["noreserve"])
