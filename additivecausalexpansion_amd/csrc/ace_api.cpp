@@ -494,6 +494,17 @@ void build_grad_tiles(ace_ctx *ctx, int64_t n, DBuf &tiles, int64_t *ntiles, int
   *ndiag = ntr;
 }
 
+// ACE_NORMS=0: every pair tile computes its own slice norms (A/B switch;
+// the table is bit-identical)
+static bool slice_norms_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_NORMS");
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
 namespace {
 
 // One evaluation on the stream.  theta_dev != nullptr: theta is a device
@@ -520,6 +531,15 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
     sig = std::exp(theta[0]);
   }
   const PairSide ps = m->side.view(m->n);
+  if (m->norms.p) {  // the slice norms once per point, for the assembly and the gradient
+    const int NS = s.kind == ACE_KERNEL_MATERN32 ? s.B + 1 : s.B;
+    ck(ctx, launch_slice_norms(ps.X, s.PM, m->npad, s.B, NS, tv.wk,
+                               s.kind == ACE_KERNEL_MATERN32 ? tv.wg + (s.B - 1) * s.PM : tv.wk,
+                               m->norms.d(), st),
+       "slice norms");
+    tv.norms = m->norms.d();
+    tv.ldn = m->npad;
+  }
   const int ts = m->tset;
   SweepTiming tmg;
   const size_t nset = m->ev_upd.size() / 2;
@@ -712,6 +732,8 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
     const Shape &s = m->s;
     alloc(ctx, m->y, (size_t)m->npad * sizeof(double), "alloc y");
     alloc(ctx, m->tab, (size_t)(2 * s.B * s.PM + s.B + 1) * sizeof(double), "alloc tab");
+    if (slice_norms_on())
+      alloc(ctx, m->norms, (size_t)((s.B + 1) * m->npad) * sizeof(double), "alloc norms");
     alloc(ctx, m->alpha, (size_t)m->npad * sizeof(double), "alloc alpha");
     alloc(ctx, m->scal, 16 * sizeof(double), "alloc scal");
     const int ldg = grad_part_cols(s.PM, s.B);

@@ -48,6 +48,11 @@ struct TabView {
   // device exp(theta[0]) (the device-fused training loop's theta lives in
   // HBM); null: the kernels' host `sig` argument
   const double *sig = nullptr;
+  // slice norms s_b(x_p) = sum_i w_bi x_pi^2 of every point, norms[b ldn + p]
+  // (launch_slice_norms: b < B the kernel weights, b = B the Matern
+  // gradient's last-slice weights); null: each pair tile computes its own
+  const double *norms = nullptr;
+  int64_t ldn = 0;
 };
 
 // Row-side / column-side operand of a pair kernel (row-major, padded).
@@ -321,6 +326,11 @@ hipError_t launch_final_sums(const double *y, const double *mu, const double *al
 // ---- device-fused training loop (ace_train.hip) -----------------------------
 // theta tables of make_tab (ace_common.h) from a device theta, plus
 // tab[2 B PM + B] = exp(theta[0]) (TabView::sig)
+// the TabView::norms table: NS = B (+ 1 for the Matern gradient) rows of np
+// points (ld np) from X (np x PM row-major), with mm_stage's arithmetic
+hipError_t launch_slice_norms(const double *X, int PM, int64_t np, int B, int NS,
+                              const double *wk, const double *wlast, double *norms,
+                              hipStream_t st);
 hipError_t launch_make_tab(const double *theta, int B, int p, int PM, double *tab,
                            hipStream_t st);
 struct TrainCfg {

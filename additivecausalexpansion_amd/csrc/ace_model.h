@@ -161,6 +161,7 @@ struct ace_model {
   bool has_inverse = false;  // a para_update has left a resident inverse
   SideBufs side;
   DBuf y, tab, alpha, scal, gpart, gwork, gsum, sums;
+  DBuf norms;           // per-evaluation slice norms (TabView::norms), (B + 1) x npad
   DBuf gtiles;          // gradient tile list (grad_tile_order), or none
   int64_t ngdiag = -1;  // its leading diagonal tiles
   PinnedBuf hio;  // [theta tables | gsum | sums | scal | flag] host staging

@@ -340,7 +340,9 @@ template <int PM, int KIND, bool GRAD, int NT = 256>
 __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS,
                                           const double *__restrict__ wk,
                                           const double *__restrict__ wlast, int64_t R0,
-                                          int64_t C0, int tid) {
+                                          int64_t C0, int tid,
+                                          const double *__restrict__ norms = nullptr,
+                                          int64_t ldn = 0) {
   constexpr int XP = xj_pitch(PM);
   const MmLayout o = mm_layout(PM, B, KIND, GRAD, NT / 64);
   const int NS = (GRAD && KIND == 1) ? B + 1 : B;
@@ -375,8 +377,17 @@ __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS
   if (tid < 32) L.E[tid] = kExp2Tab[tid];
   for (int e = tid; e < NS * PM; e += NT) L.W[e] = (e < B * PM) ? wk[e] : wlast[e - B * PM];
   __syncthreads();
-  // norms: task = (side, slice, point), same accumulation order as the
-  // per-slice loops they replace (i ascending, fma(x^2, w, s))
+  // norms: from the per-evaluation table (launch_slice_norms, the same
+  // arithmetic once per point instead of once per tile: bit-identical), or
+  // task = (side, slice, point), same accumulation order as the per-slice
+  // loops they replace (i ascending, fma(x^2, w, s))
+  if (norms) {
+    for (int e = tid; e < 2 * NS * 64; e += NT) {
+      const int side = e / (NS * 64), rem = e - side * NS * 64;
+      const int sl = rem >> 6, pt = rem & 63;
+      (side == 0 ? L.Nc : L.Nr)[rem] = norms[sl * ldn + (side == 0 ? C0 : R0) + pt];
+    }
+  } else
   for (int e = tid; e < 2 * NS * 64; e += NT) {
     const int side = e / (NS * 64), rem = e - side * NS * 64;
     const int sl = rem >> 6, pt = rem & 63;
@@ -452,6 +463,38 @@ __device__ __forceinline__ void gemm1_mm(const double *sXJ, const RowX<PM, FP> &
   }
 }
 
+// Slice norms of every point once per evaluation (TabView::norms): the
+// per-tile staging's loop, i ascending with fma(x^2, w, s), so every tile
+// reads the values it would have computed.
+__global__ __launch_bounds__(256) void k_slice_norms(const double *__restrict__ X, int PM,
+                                                     int64_t np, int B, int NS,
+                                                     const double *__restrict__ wk,
+                                                     const double *__restrict__ wlast,
+                                                     double *__restrict__ norms) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)NS * np) return;
+  const int b = (int)(e / np);
+  const int64_t pt = e - (int64_t)b * np;
+  const double *w = b < B ? wk + (int64_t)b * PM : wlast;
+  const double *x = X + pt * PM;
+  double s = 0.0;
+  for (int i = 0; i < PM; ++i) {
+    const double v = x[i];
+    s = fma(v * v, w[i], s);
+  }
+  norms[e] = s;
+}
+
+hipError_t launch_slice_norms(const double *X, int PM, int64_t np, int B, int NS,
+                              const double *wk, const double *wlast, double *norms,
+                              hipStream_t st) {
+  const int64_t tot = (int64_t)NS * np;
+  if (tot == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_slice_norms, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, X, PM,
+                     np, B, NS, wk, wlast, norms);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // Fused assembly (mode 0): lower 64-tiles of A (sigma on the diagonal,
 // identity on padding) and of the Kfull copy; same outputs as
@@ -512,7 +555,8 @@ __global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 32 ? 3 : 2)) v
   const int rl = 16 * wr + lr;
   const int64_t r = R0 + rl;
   constexpr int XP = xj_pitch(PM);
-  const MmLds L = mm_stage<PM, KIND, false, ASM_NT>(lds, S, B, ZS, tab.wk, tab.wk, R0, C0, tid);
+  const MmLds L = mm_stage<PM, KIND, false, ASM_NT>(lds, S, B, ZS, tab.wk, tab.wk, R0, C0, tid,
+                                                    tab.norms, tab.ldn);
   RowX<PM> xr;
   xr.load(S.X + r * PM, lk);
   double kf[CB][4];
@@ -722,7 +766,8 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
       }
   }
   const double ar = rvalid ? alpha[r] : 0.0;
-  const MmLds L = mm_stage<PM, KIND, true, NT>(lds, S, B, ZS, tab.wk, wlast, R0, C0, tid);
+  const MmLds L = mm_stage<PM, KIND, true, NT>(lds, S, B, ZS, tab.wk, wlast, R0, C0, tid,
+                                               tab.norms, tab.ldn);
   // T = w_rc (sA A[r,c] - alpha_r alpha_c), w = 2 off the diagonal (lower pairs)
   double tv[CB][4];
   double tr = 0.0;
