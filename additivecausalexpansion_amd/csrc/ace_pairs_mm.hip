@@ -817,16 +817,25 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   }
   // gpart[b][i] of this tile from slice b's partials: the waves' x parts,
   // sum_c x_ci^2 C_c, and (i == PM) the waves' sums of T K
-  auto finish = [&](int b, const double *red, int i) {
+  // summed: cc[c] already holds the four row blocks' column sums
+  // (cc[c] + cc[64 + c]) + (cc[128 + c] + cc[192 + c]) (summed once per slice)
+  auto finish = [&](int b, const double *red, int i, bool summed = false) {
     double g = 0.0;
     if (i < PM) {
 #pragma unroll
       for (int q = 0; q < NWV; ++q) g += red[q * RS + i];
       const double *cc = red + NWV * RS;
       double gc = 0.0;
-      for (int c = 0; c < 64; ++c) {
-        const double x = L.XJ[c * XP + i];
-        gc = fma(x * x, (cc[c] + cc[64 + c]) + (cc[128 + c] + cc[192 + c]), gc);
+      if (summed) {
+        for (int c = 0; c < 64; ++c) {
+          const double x = L.XJ[c * XP + i];
+          gc = fma(x * x, cc[c], gc);
+        }
+      } else {
+        for (int c = 0; c < 64; ++c) {
+          const double x = L.XJ[c * XP + i];
+          gc = fma(x * x, (cc[c] + cc[64 + c]) + (cc[128 + c] + cc[192 + c]), gc);
+        }
       }
       g += gc;
     } else {
@@ -1019,9 +1028,17 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   if (lane == 0) str[w] = tr;
   __syncthreads();
   if (per_slice) {  // all slices' partials at once
+    // each slice's four row-block column sums added once (same expression,
+    // so bit-identical), not once per feature
+    for (int e = tid; e < B * 64; e += NT) {
+      double *cc = L.Red + (e >> 6) * PER + NWV * RS;
+      const int c = e & 63;
+      cc[c] = (cc[c] + cc[64 + c]) + (cc[128 + c] + cc[192 + c]);
+    }
+    __syncthreads();
     for (int e = tid; e < B * NV; e += NT) {
       const int bb = e / NV, i = e - bb * NV;
-      finish(bb, L.Red + bb * PER, i);
+      finish(bb, L.Red + bb * PER, i, true);
     }
   }
   if (tid == 0) {
