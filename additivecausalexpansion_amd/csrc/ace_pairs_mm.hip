@@ -857,6 +857,10 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
 #define ACE_DIAG_GRAD 0
 #endif
   const int bstop = (ACE_DIAG_GRAD & 3) == 1 ? B : (ACE_DIAG_GRAD & 3) == 2 ? B - 1 : 0;
+#ifndef ACE_GRAD_UNROLL
+#define ACE_GRAD_UNROLL 1
+#endif
+#pragma unroll ACE_GRAD_UNROLL
   for (int b = B - 1; b >= bstop; --b) {
     double *red = L.Red + (per_slice ? b : (b & 1)) * PER;
     double zr = 1.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
