@@ -443,7 +443,8 @@ int ace_invkernel_dev(ace_ctx *ctx, const ace_dmat *K, double sigma, double *eig
     // the fused model's front: A = Kfull + e^sigma I assembled into the
     // sweep buffer (lower tiles) and swept, no n x n Kfull in between
     const KernSrc &k = *K->src;
-    const TabView tv = tab_view(k.tab, k.shape);
+    const TabView tv = with_norms(ctx, w.norms, tab_view(k.tab, k.shape), k.shape, k.s1->X.d(),
+                                  w.npad, ctx->stream);
     assemble_and_sweep(ctx, w, k.shape, k.s1->view(n), tv, h->sig, ydev, n, nullptr, nullptr);
     h->src = K->src;
   } else {
@@ -622,7 +623,12 @@ int ace_grad_dev(ace_ctx *ctx, int kind, int64_t n, int p, int B, const double *
   alloc(ctx, *dg, (size_t)(nt * ldg) * sizeof(double), "alloc gpart");
   alloc(ctx, *dwork, (size_t)tile_sums_work(ldg) * sizeof(double), "alloc tile sums");
   alloc(ctx, *dgs, (size_t)ldg * sizeof(double), "alloc gsum");
-  ck(ctx, launch_grad(kind, s.PM, sb->view(n), B, s.ZS, tab_view(dtab, s), Ainv, ld,
+  // swept (the resident inverse): the sweep buffers' norms table for the
+  // cached side's npad rows; else the tiles compute their own
+  const TabView tvg = swept && !cube ? with_norms(ctx, inv->sweep->norms, tab_view(dtab, s), s,
+                                                  sb->X.d(), inv->sweep->npad, ctx->stream)
+                                     : tab_view(dtab, s);
+  ck(ctx, launch_grad(kind, s.PM, sb->view(n), B, s.ZS, tvg, Ainv, ld,
                       swept ? -1.0 : 1.0, dalpha.d(), cube, dg->d(), ctx->stream, tl, tl ? nt : 0, 1,
                       ndiag),
      "grad");

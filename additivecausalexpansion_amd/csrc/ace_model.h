@@ -12,6 +12,7 @@ struct SweepWork {
   int Z = 2;  // steps per bulk launch (sweep_group()), panel slots k % 2Z
   DBuf gtiles;                          // handle path: the gradient's tile list (build_grad_tiles)
   DBuf gpart, gwork, gsum;              // handle path: gradient partial-sum scratch
+  DBuf norms;                           // handle path: slice norms (TabView::norms)
   int64_t ngtiles = 0, ngdiag = -2;     // -2: not built yet
   std::vector<int64_t> xoff, poff, moff, hoff;
   std::vector<int> mfront, mtarget;
@@ -147,6 +148,21 @@ struct SweepWork {
     return s;
   }
 };
+
+// tv with TabView::norms computed into buf for the np points of X (np x PM,
+// the padded side buffer): the assembly / gradient tiles then load their
+// slice norms (bit-identical to computing them per tile)
+inline TabView with_norms(ace_ctx *ctx, DBuf &buf, TabView tv, const Shape &s, const double *X,
+                          int64_t np, hipStream_t st) {
+  const bool m = s.kind == ACE_KERNEL_MATERN32;
+  alloc(ctx, buf, (size_t)((s.B + 1) * np) * sizeof(double), "alloc norms");
+  ck(ctx, launch_slice_norms(X, s.PM, np, s.B, m ? s.B + 1 : s.B, tv.wk,
+                             m ? tv.wg + (s.B - 1) * s.PM : tv.wk, buf.d(), st),
+     "slice norms");
+  tv.norms = buf.d();
+  tv.ldn = np;
+  return tv;
+}
 
 // =====================================================================
 // Device-resident model: one para_update per call, nothing materialised
