@@ -64,27 +64,33 @@ int ace_create(int device, ace_ctx **out) {
     };
     const int p1 = prio("ACE_SIDE_PRIO"), p2 = p1 == lo ? lo : prio("ACE_SIDE2_PRIO");
     e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, p1);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, p2);
-  }
-  if (e == hipSuccess) {
-    // ACE_ASM_RESERVE=R (multiple of 8): the assembly's second part leaves
-    // R CUs free -- mask bits 0..7 are CU 0 of XCDs 0..7 (tools/probe_cumask.hip,
-    // profiles/r01_cumask_probe.txt) -- for the first group's pivot chains,
-    // which get no slot beside the assembly kernel otherwise
+    // ACE_ASM_RESERVE=R (multiple of 8): the second side stream (the tail
+    // path) runs on every CU but R -- mask bits 0..7 are CU 0 of XCDs 0..7
+    // (tools/probe_cumask.hip, profiles/r01_cumask_probe.txt) -- and carries
+    // the assembly's second part too, so the first group's head path gets
+    // those CUs beside the assembly (its chains get no slot there otherwise).
+    // The same stream, not a fourth one: with the null stream, four streams
+    // fill the box's GPU_MAX_HW_QUEUES = 4, and a fifth made HIP share a
+    // hardware queue between two streams, under which one evaluation once
+    // stalled for 100 s (profiles/r03_v8_reserve_ab.txt).  Its priority is
+    // the default one (measured neutral for the tail path, §5)
     const char *v = getenv("ACE_ASM_RESERVE");
     const int R = v ? atoi(v) : ASM_RESERVE_DEFAULT;
     hipDeviceProp_t prop;
-    if (R > 0 && hipGetDeviceProperties(&prop, device) == hipSuccess &&
+    if (e == hipSuccess && R > 0 && hipGetDeviceProperties(&prop, device) == hipSuccess &&
         R < prop.multiProcessorCount) {
       const int ncu = prop.multiProcessorCount;
       std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
       for (int i = R; i < ncu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
-      // an optimisation only: without it the assembly runs on the main stream
-      if (hipExtStreamCreateWithCUMask(&c->asm2, (uint32_t)ncu, mask.data()) != hipSuccess) {
-        c->asm2 = nullptr;
+      if (hipExtStreamCreateWithCUMask(&c->side2, (uint32_t)ncu, mask.data()) == hipSuccess) {
+        c->asm2 = c->side2;
+      } else {  // an optimisation only: an unmasked second side stream
+        c->side2 = nullptr;
         (void)hipGetLastError();
       }
     }
+    if (e == hipSuccess && !c->side2)
+      e = hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, p2);
   }
   if (e != hipSuccess) {
     g_create_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
@@ -101,7 +107,7 @@ void ace_destroy(ace_ctx *ctx) {
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->side2) (void)hipStreamDestroy(ctx->side2);
-  if (ctx->asm2) (void)hipStreamDestroy(ctx->asm2);
+  // (asm2 is side2 when set)
   delete ctx;
 }
 

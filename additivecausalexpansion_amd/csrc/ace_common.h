@@ -22,9 +22,9 @@ struct ace_ctx {
   hipStream_t stream = nullptr;  // main stream (every ABI call syncs it)
   hipStream_t side = nullptr;    // sweep lookahead: panel factorisation
   hipStream_t side2 = nullptr;   // sweep lookahead: the second block's cross update
-  // the assembly's second part, on every CU but R reserved ones (one per XCD
-  // per 8) where the first sweep group's pivot chains then run beside it;
-  // null: ACE_ASM_RESERVE=0
+  // the assembly's second part: side2 when that stream is CU-masked to every
+  // CU but R reserved ones (one per XCD per 8), where the first sweep group's
+  // pivot chains then run beside it; null: ACE_ASM_RESERVE=0
   hipStream_t asm2 = nullptr;
   int (*poll)(void *) = nullptr; // optional interrupt poll (ace_set_interrupt_poll)
   void *poll_user = nullptr;
