@@ -124,7 +124,7 @@ class CommOps(ctypes.Structure):
 UNIQUE_ID_BYTES = 128
 
 STATUS = {0: "ACE_OK", 1: "ACE_ERR_ARG", 2: "ACE_ERR_HIP", 3: "ACE_ERR_OOM",
-          4: "ACE_ERR_UNSUPPORTED", 5: "ACE_ERR_NONFINITE", 6: "ACE_ERR_INTERRUPTED"}
+          4: "ACE_ERR_UNSUPPORTED", 5: "ACE_ERR_NONFINITE", 6: "ACE_ERR_INTERRUPTED", 7: "ACE_ERR_TIMEOUT"}
 POLL_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
 OPTIMIZER = {"GD": 0, "NAG": 0, "Adam": 1, "Nadam": 2}
 

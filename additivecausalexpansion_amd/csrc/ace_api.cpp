@@ -11,6 +11,7 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ace_hip.h"
@@ -22,6 +23,57 @@
 using namespace ace;
 
 std::string g_create_err;
+
+namespace {
+double sync_timeout_s() {
+  static double v = -1.0;
+  if (v < 0.0) {
+    const char *e = getenv("ACE_SYNC_TIMEOUT");
+    v = e ? std::max(0.0, atof(e)) : 600.0;
+  }
+  return v;
+}
+}  // namespace
+
+// Bounded drain of one stream (ace_common.h).  Polls hipStreamQuery: yields
+// for the first 100 ms (an evaluation is ~75 ms, so the common wait costs no
+// extra latency), then sleeps 100 us between polls.  On the deadline the
+// error names which of the context's streams still hold work, which is what
+// a stalled hardware queue or a hung collective looks like from the host.
+void ace_host::sync_stream(ace_ctx *ctx, hipStream_t s, const char *what) {
+  const double lim = sync_timeout_s();
+  if (lim <= 0.0) {
+    ck(ctx, hipStreamSynchronize(s), what);
+    return;
+  }
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) ck(ctx, e, what);
+    const double dt = std::chrono::duration<double>(clk::now() - t0).count();
+    if (dt > lim) {
+      std::string busy;
+      const hipStream_t all[3] = {ctx->stream, ctx->side, ctx->side2};
+      const char *names[3] = {"main", "side", "side2"};
+      for (int i = 0; i < 3; ++i) {
+        bool dup = false;
+        for (int j = 0; j < i; ++j) dup = dup || all[j] == all[i];
+        if (!all[i] || dup) continue;
+        if (hipStreamQuery(all[i]) == hipErrorNotReady) busy += std::string(" ") + names[i];
+      }
+      char buf[160];
+      snprintf(buf, sizeof buf, "%s: device work did not complete within %.0f s (streams still busy:%s)",
+               what, lim, busy.empty() ? " none" : busy.c_str());
+      ctx->err = buf;
+      fprintf(stderr, "ace: %s\n", buf);
+      throw Fail{ACE_ERR_TIMEOUT};
+    }
+    if (dt < 0.1) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+}
 
 
 extern "C" {
@@ -49,8 +101,15 @@ int ace_create(int device, ace_ctx **out) {
   }
   ace_ctx *c = new ace_ctx();
   c->device = device;
+  // ACE_STREAMS: how many streams the context creates: 3 = main +
+  // panel chain + tail path (default), 2 = the tail path on the panel
+  // stream, 1 = everything on the main stream (no lookahead overlap).  The
+  // results are bit-identical for every value.
+  const char *vs = getenv("ACE_STREAMS");
+  const int nstr = vs ? std::min(3, std::max(1, atoi(vs))) : 3;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) {
+  if (e == hipSuccess) c->nstreams = 1;
+  if (e == hipSuccess && nstr >= 2) {
     // the lookahead panel chain is latency-bound: give it the highest priority
     // so its workgroups take the first free CU slots next to the update kernel
     // (ACE_SIDE_PRIO=0: the least priority, A/B switch; ACE_SIDE2_PRIO=0: the
@@ -64,39 +123,34 @@ int ace_create(int device, ace_ctx **out) {
     };
     const int p1 = prio("ACE_SIDE_PRIO"), p2 = p1 == lo ? lo : prio("ACE_SIDE2_PRIO");
     e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, p1);
-    // ACE_ASM_RESERVE=R (multiple of 8): the second side stream (the tail
-    // path) runs on every CU but R -- mask bits 0..7 are CU 0 of XCDs 0..7
-    // (tools/probe_cumask.hip, profiles/r01_cumask_probe.txt) -- and carries
-    // the assembly's second part too, so the first group's head path gets
-    // those CUs beside the assembly (its chains get no slot there otherwise).
-    // The same stream, not a fourth one: with the null stream, four streams
-    // fill the box's GPU_MAX_HW_QUEUES = 4, and a fifth made HIP share a
-    // hardware queue between two streams, under which one evaluation once
-    // stalled for 100 s (profiles/r03_v8_reserve_ab.txt).  Its priority is
-    // the default one (measured neutral for the tail path, §5)
-    const char *v = getenv("ACE_ASM_RESERVE");
-    const int R = v ? atoi(v) : ASM_RESERVE_DEFAULT;
-    hipDeviceProp_t prop;
-    if (e == hipSuccess && R > 0 && hipGetDeviceProperties(&prop, device) == hipSuccess &&
-        R < prop.multiProcessorCount) {
-      const int ncu = prop.multiProcessorCount;
-      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-      for (int i = R; i < ncu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
-      if (hipExtStreamCreateWithCUMask(&c->side2, (uint32_t)ncu, mask.data()) == hipSuccess) {
-        c->asm2 = c->side2;
-      } else {  // an optimisation only: an unmasked second side stream
-        c->side2 = nullptr;
-        (void)hipGetLastError();
-      }
-    }
-    if (e == hipSuccess && !c->side2)
+    if (e == hipSuccess) c->nstreams = 2;
+    if (e == hipSuccess && nstr >= 3) {
       e = hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, p2);
+      if (e == hipSuccess) c->nstreams = 3;
+    }
   }
   if (e != hipSuccess) {
     g_create_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
-    delete c;
+    ace_destroy(c);
     return ACE_ERR_HIP;
   }
+  // aliases for a smaller budget: a wait on an event of the same stream is
+  // free, so the schedules run unchanged in host order
+  if (!c->side) c->side = c->stream;
+  if (!c->side2) c->side2 = c->side;
+#ifdef ACE_DIAG_MASKED_STREAM
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
+      const int ncu = prop.multiProcessorCount;
+      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+      for (int i = 8; i < ncu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+      if (hipExtStreamCreateWithCUMask(&c->diag_masked, (uint32_t)ncu, mask.data()) != hipSuccess)
+        c->diag_masked = nullptr;
+      (void)hipEventCreateWithFlags(&c->diag_ev, ACE_SYNC_EVENT_FLAGS);
+    }
+  }
+#endif
   *out = c;
   return ACE_OK;
 }
@@ -104,10 +158,13 @@ int ace_create(int device, ace_ctx **out) {
 void ace_destroy(ace_ctx *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+#ifdef ACE_DIAG_MASKED_STREAM
+  if (ctx->diag_masked) (void)hipStreamDestroy(ctx->diag_masked);
+  if (ctx->diag_ev) (void)hipEventDestroy(ctx->diag_ev);
+#endif
+  if (ctx->side2 && ctx->side2 != ctx->side) (void)hipStreamDestroy(ctx->side2);
+  if (ctx->side && ctx->side != ctx->stream) (void)hipStreamDestroy(ctx->side);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-  if (ctx->side) (void)hipStreamDestroy(ctx->side);
-  if (ctx->side2) (void)hipStreamDestroy(ctx->side2);
-  // (asm2 is side2 when set)
   delete ctx;
 }
 
@@ -460,20 +517,20 @@ void assemble_and_sweep(ace_ctx *ctx, SweepWork &w, const Shape &s, const PairSi
     ck(ctx, hipEventRecord(sy.ev[2 * steps], st), "event");
     sy.ready_recorded = true;
   }
-  // the second part on the CU-masked stream (ctx->asm2): the first group's
-  // chains run on the reserved CUs meanwhile; its tail path waits (asm_done)
-  const bool a2 = ctx->asm2 && sy.side && sy.nev >= 5 * steps + 6;
-  if (a2) {
-    ck(ctx, hipStreamWaitEvent(ctx->asm2, sy.ev[2 * steps], 0), "wait");
-    sy.asm_done = sy.ev[5 * steps + 5];
-  }
+#ifdef ACE_DIAG_MASKED_STREAM
+  if (ctx->diag_masked && sy.ready_recorded) {
+    ck(ctx, hipStreamWaitEvent(ctx->diag_masked, sy.ev[2 * steps], 0), "wait");
+    ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
+                            nullptr, ctx->diag_masked, nullptr, 0, 1, 2),
+       "assembly");
+    ck(ctx, hipEventRecord(ctx->diag_ev, ctx->diag_masked), "event");
+    ck(ctx, hipStreamWaitEvent(st, ctx->diag_ev, 0), "wait");
+    ck(ctx, hipStreamWaitEvent(ctx->side2, ctx->diag_ev, 0), "wait");
+  } else
+#endif
   ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
-                          nullptr, a2 ? ctx->asm2 : st, nullptr, 0, 1, 2),
+                          nullptr, st, nullptr, 0, 1, 2),
      "assembly");
-  if (a2) {
-    ck(ctx, hipEventRecord(sy.asm_done, ctx->asm2), "event");
-    ck(ctx, hipStreamWaitEvent(st, sy.asm_done, 0), "wait");
-  }
   if (ev_asm) ck(ctx, hipEventRecord(ev_asm[1], st), "event");
   ck(ctx, run_sweep(w.bufs(), st, &sy, tmg), "sweep");
 }
@@ -494,8 +551,7 @@ void build_grad_tiles(ace_ctx *ctx, int64_t n, DBuf &tiles, int64_t *ntiles, int
   const std::vector<Tile> o = xcd_update_order(low, S);
   lst.insert(lst.end(), o.begin(), o.end());
   alloc(ctx, tiles, lst.size() * sizeof(Tile), "alloc grad tiles");
-  ck(ctx, hipMemcpy(tiles.p, lst.data(), lst.size() * sizeof(Tile), hipMemcpyHostToDevice),
-     "upload grad tiles");
+  upload_bytes(ctx, tiles.p, lst.data(), lst.size() * sizeof(Tile), "upload grad tiles");
   *ntiles = (int64_t)lst.size();
   *ndiag = ntr;
 }
@@ -794,8 +850,7 @@ int ace_model_set_data(ace_model *m, const double *y, const double *X, const dou
   upload_side(ctx, m->side, m->s, X, Z, m->n, m->npad);
   std::vector<double> yp((size_t)m->npad, 0.0);
   std::copy(y, y + m->n, yp.begin());
-  ck(ctx, hipMemcpy(m->y.p, yp.data(), yp.size() * sizeof(double), hipMemcpyHostToDevice),
-     "upload y");
+  upload_bytes(ctx, m->y.p, yp.data(), yp.size() * sizeof(double), "upload y");
   m->std_y = std_y;
   sync(ctx);
   m->has_data = true;

@@ -17,15 +17,20 @@
 
 struct SweepWork;  // ace_model.h
 
+// Streams (DESIGN §5 "Streams and hardware queues"): all non-blocking, so
+// nothing the runtime or another library puts on the legacy null stream is
+// ordered against them, and the library itself never uses the null stream.
+// ACE_STREAMS = 3 (default) / 2 / 1 creates that many; with fewer, side2
+// aliases side and side aliases stream.  Every cross-stream wait is enqueued
+// after the record it waits for, so any serialisation of the three in host
+// order -- one stream, or two sharing a hardware queue -- is a valid
+// execution of the same graph with bit-identical results.
 struct ace_ctx {
   int device = 0;
+  int nstreams = 0;              // distinct streams created (1..3)
   hipStream_t stream = nullptr;  // main stream (every ABI call syncs it)
   hipStream_t side = nullptr;    // sweep lookahead: panel factorisation
   hipStream_t side2 = nullptr;   // sweep lookahead: the second block's cross update
-  // the assembly's second part: side2 when that stream is CU-masked to every
-  // CU but R reserved ones (one per XCD per 8), where the first sweep group's
-  // pivot chains then run beside it; null: ACE_ASM_RESERVE=0
-  hipStream_t asm2 = nullptr;
   int (*poll)(void *) = nullptr; // optional interrupt poll (ace_set_interrupt_poll)
   void *poll_user = nullptr;
   std::string err;
@@ -33,6 +38,13 @@ struct ace_ctx {
   // next invkernel_dev of the same n instead of a new 2 n^2-byte allocation
   std::vector<std::shared_ptr<SweepWork>> sweep_pool;
   std::shared_ptr<void> dmat_state;  // the handle path's cached inputs (ace_dmat.cpp)
+#ifdef ACE_DIAG_MASKED_STREAM
+  // diagnostic builds only (tools/build_variant.sh): round 3's
+  // stalled configuration, the assembly's second part on a fourth,
+  // CU-masked stream (hipExtStreamCreateWithCUMask: blocking flags)
+  hipStream_t diag_masked = nullptr;
+  hipEvent_t diag_ev = nullptr;
+#endif
 };
 
 extern std::string g_create_err;
@@ -86,20 +98,46 @@ inline void arg(ace_ctx *ctx, bool ok, const char *msg) {
   throw Fail{ACE_ERR_ARG};
 }
 
+// A failed allocation first drops the pooled sweep buffers of freed inverse
+// handles (dead contents, ace_dmat_free) and retries once.
 inline void alloc(ace_ctx *ctx, DBuf &b, size_t bytes, const char *what) {
   if (b.bytes >= bytes && b.p) return;
   b.release();
   if (bytes == 0) bytes = 16;
-  ck(ctx, hipMalloc(&b.p, bytes), what);
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if ((e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) && !ctx->sweep_pool.empty()) {
+    (void)hipGetLastError();
+    ctx->sweep_pool.clear();
+    e = hipMalloc(&b.p, bytes);
+  }
+  if (e != hipSuccess) b.p = nullptr;
+  ck(ctx, e, what);
   b.bytes = bytes;
 }
 
-// Host -> device copies are synchronous (pageable host buffers may be
-// temporaries); every call syncs its stream before returning, so no kernel
-// of a previous call can still be reading the destination.
+// Waits until everything enqueued on `s` has run, bounded: after
+// ACE_SYNC_TIMEOUT seconds (default 600; 0 = an unbounded
+// hipStreamSynchronize) the call fails with ACE_ERR_TIMEOUT and ctx->err
+// names the context's streams that still hold work, instead of blocking the
+// host forever on a stalled queue or collective (ace_api.cpp).
+void sync_stream(ace_ctx *ctx, hipStream_t s, const char *what);
+inline void sync(ace_ctx *ctx) { sync_stream(ctx, ctx->stream, "hipStreamSynchronize"); }
+
+// Host -> device copies: stream-ordered on the main stream (never the null
+// stream) and complete on return (pageable host buffers may be temporaries);
+// every call syncs its stream before returning, so no kernel of a previous
+// call can still be reading the destination.
 inline void upload(ace_ctx *ctx, DBuf &b, const double *h, size_t count, const char *what) {
   alloc(ctx, b, count * sizeof(double), what);
-  if (count) ck(ctx, hipMemcpy(b.p, h, count * sizeof(double), hipMemcpyHostToDevice), what);
+  if (!count) return;
+  ck(ctx, hipMemcpyAsync(b.p, h, count * sizeof(double), hipMemcpyHostToDevice, ctx->stream), what);
+  sync_stream(ctx, ctx->stream, what);
+}
+// the same for any trivially copyable host array (tile lists)
+inline void upload_bytes(ace_ctx *ctx, void *d, const void *h, size_t bytes, const char *what) {
+  if (!bytes) return;
+  ck(ctx, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream), what);
+  sync_stream(ctx, ctx->stream, what);
 }
 
 inline void download(ace_ctx *ctx, double *h, const double *d, size_t count, const char *what) {
@@ -131,8 +169,6 @@ struct PinnedBuf {
     return p;
   }
 };
-
-inline void sync(ace_ctx *ctx) { ck(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize"); }
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 

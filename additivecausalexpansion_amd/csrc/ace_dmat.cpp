@@ -70,6 +70,8 @@ struct ace_dmat {
   std::shared_ptr<const std::vector<double>> yaug;  // SWEPT: the y swept along in AUG row 0
   DBuf msum;                            // dense CUBE: pred_marginal's slice sum (cached)
   bool have_msum = false;
+  DBuf slice;                           // virtual CUBE: the last slice ace_dmat_read assembled
+  int64_t slice_b = -1;                 // ... and its index (-1: none)
 };
 
 namespace {
@@ -317,18 +319,25 @@ int ace_dmat_read(const ace_dmat *hc, int64_t offset, int64_t count, double *out
     const KernSrc &k = *h->src;
     const Shape &s = k.shape;
     const int64_t sl = h->rows * h->cols;
-    DBuf scratch;
-    alloc(ctx, scratch, (size_t)sl * sizeof(double), "alloc slice");
+    // the last assembled slice stays on the handle: the R shim reads an
+    // ALTREP vector element by element or 512 values at a time
+    // (rcpp/ace_hip_shim.cpp Elt / Get_region), and each later read inside
+    // that slice is then a plain download
     for (int64_t b = offset / sl; b < h->slices && b * sl < offset + count; ++b) {
       const int64_t lo = std::max(offset, b * sl), hi = std::min(offset + count, (b + 1) * sl);
-      const PairSide a = k.s1->view(h->rows), c = k.symmetric ? k.s1->view(h->rows) : k.s2->view(h->cols);
-      ck(ctx, launch_assembly(k.symmetric ? 1 : 2, s.kind, s.PM, a, c, 0, s.B, s.ZS,
-                              tab_view(k.tab, s), 0.0, scratch.d(), h->rows, nullptr, ctx->stream,
-                              nullptr, 0, 1, 0, (int)b, (int)b + 1),
-         "slice assembly");
-      download(ctx, out + (lo - offset), scratch.d() + (lo - b * sl), (size_t)(hi - lo),
+      if (h->slice_b != b) {
+        alloc(ctx, h->slice, (size_t)sl * sizeof(double), "alloc slice");
+        h->slice_b = -1;
+        const PairSide a = k.s1->view(h->rows), c = k.symmetric ? k.s1->view(h->rows) : k.s2->view(h->cols);
+        ck(ctx, launch_assembly(k.symmetric ? 1 : 2, s.kind, s.PM, a, c, 0, s.B, s.ZS,
+                                tab_view(k.tab, s), 0.0, h->slice.d(), h->rows, nullptr, ctx->stream,
+                                nullptr, 0, 1, 0, (int)b, (int)b + 1),
+           "slice assembly");
+      }
+      download(ctx, out + (lo - offset), h->slice.d() + (lo - b * sl), (size_t)(hi - lo),
                "download slice");
       sync(ctx);
+      h->slice_b = b;
     }
     h->host_read = true;
     return ACE_OK;
@@ -350,8 +359,13 @@ void ace_dmat_free(ace_dmat *h) {
   (void)hipSetDevice(h->ctx->device);
   // keep up to two sets of sweep buffers for the next invkernel_dev (the R6
   // loop frees one inverse per iteration); their contents are dead
+  // (only sets of this n: a set of another size is dropped, not kept)
   if (h->kind == ace_dmat::SWEPT && h->sweep && h->sweep.use_count() == 1) {
     auto &pool = h->ctx->sweep_pool;
+    const int64_t n = h->sweep->n;
+    pool.erase(std::remove_if(pool.begin(), pool.end(),
+                              [n](const std::shared_ptr<SweepWork> &w) { return w->n != n; }),
+               pool.end());
     if (pool.size() >= 2) pool.erase(pool.begin());
     pool.push_back(std::move(h->sweep));
   }

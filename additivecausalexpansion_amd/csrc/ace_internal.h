@@ -213,16 +213,6 @@ std::vector<Tile> own_tiles(int64_t ntile, int T, int G, int r);
 // super-block size S of that order (0: row-major grid); ACE_UPD_ORDER=S
 // overrides (diagnostic A/B switch)
 int update_order_block();
-// CUs the assembly's second part leaves to the first sweep group's chains
-// (ACE_ASM_RESERVE overrides; 0, the default: no CU mask).  On a fourth,
-// CU-masked stream it took 0.6 ms off a C2 evaluation (74.9 against 75.5 ms,
-// profiles/r03_v8_reserve_ab.txt), but with the null stream that is one
-// stream more than the box's GPU_MAX_HW_QUEUES = 4, and one evaluation then
-// stalled for 100 s in a test (HIP shares a hardware queue between two
-// streams); on the tail stream itself (no extra stream) the mask costs the
-// steady state what it saves at the start: 74.84-74.98 against 74.91-75.03 ms
-// (same box), so it is off.
-constexpr int ASM_RESERVE_DEFAULT = 0;
 // Lookahead: the panel sweep of step k+1 runs on `side` while the main
 // stream updates the rest of step k.  `ev` needs 2*steps + 1 events.
 struct SweepSync {
@@ -231,10 +221,6 @@ struct SweepSync {
   hipEvent_t *ev;
   int nev;
   bool ready_recorded = false;  // caller already recorded ev[2 * steps] ("inputs ready")
-  // the assembly's second part ran on ctx->asm2: done when this event is
-  // (run_sweep_heads holds the first group's tail path until then, so the
-  // reserved CUs serve its head path); null: the assembly is on the main stream
-  hipEvent_t asm_done = nullptr;
 };
 // Optional timing of the dominant update launches (k_update<false>): event
 // pairs in ev, executed GEMM flops per timed launch in flops[].

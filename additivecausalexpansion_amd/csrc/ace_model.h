@@ -42,8 +42,7 @@ struct SweepWork {
     if (const int S = update_order_block(); S > 0) {
       const std::vector<Tile> t = xcd_update_order(own_tiles(naug / UT, UT, 1, 0), S);
       alloc(ctx, order, t.size() * sizeof(Tile), "alloc tile order");
-      ck(ctx, hipMemcpy(order.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
-         "upload tile order");
+      upload_bytes(ctx, order.p, t.data(), t.size() * sizeof(Tile), "upload tile order");
       norder = (int64_t)t.size();
     }
     poff.clear();
@@ -56,29 +55,25 @@ struct SweepWork {
       const std::vector<Tile> t = pair_cross_tiles(naug, (int)(npad / NB), poff, Z);
       alloc(ctx, ptiles, std::max<size_t>(t.size(), 1) * sizeof(Tile), "alloc pair cross tiles");
       if (!t.empty())
-        ck(ctx, hipMemcpy(ptiles.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
-           "upload pair cross tiles");
+        upload_bytes(ctx, ptiles.p, t.data(), t.size() * sizeof(Tile), "upload pair cross tiles");
       glen = 0;
       if (tail_sort()) {
         const std::vector<Tile> o = pair_bulk_orders(naug, (int)(npad / NB), &glen, 1, 0, Z);
         alloc(ctx, gorder, o.size() * sizeof(Tile), "alloc bulk orders");
-        ck(ctx, hipMemcpy(gorder.p, o.data(), o.size() * sizeof(Tile), hipMemcpyHostToDevice),
-           "upload bulk orders");
+        upload_bytes(ctx, gorder.p, o.data(), o.size() * sizeof(Tile), "upload bulk orders");
       }
       hoff.clear();
       if (heads_on()) {
         const std::vector<Tile> h = group_head_tiles(naug, (int)(npad / NB), Z, hoff);
         alloc(ctx, htiles, std::max<size_t>(h.size(), 1) * sizeof(Tile), "alloc head tiles");
         if (!h.empty())
-          ck(ctx, hipMemcpy(htiles.p, h.data(), h.size() * sizeof(Tile), hipMemcpyHostToDevice),
-             "upload head tiles");
+          upload_bytes(ctx, htiles.p, h.data(), h.size() * sizeof(Tile), "upload head tiles");
       }
       moff.clear();
       if (glen > 0 && merge_cross() && Z == 2) {
         const std::vector<Tile> m = merged_bulk_orders(naug, (int)(npad / NB), moff, mfront, mtarget);
         alloc(ctx, morder, m.size() * sizeof(Tile), "alloc merged orders");
-        ck(ctx, hipMemcpy(morder.p, m.data(), m.size() * sizeof(Tile), hipMemcpyHostToDevice),
-           "upload merged orders");
+        upload_bytes(ctx, morder.p, m.data(), m.size() * sizeof(Tile), "upload merged orders");
         alloc(ctx, mcnt, (size_t)round_up((int64_t)mfront.size(), 4) * sizeof(int), "alloc counters");
       }
     }
@@ -87,8 +82,7 @@ struct SweepWork {
       const std::vector<Tile> t = cross_update_tiles(naug, (int)(npad / NB), xoff);
       alloc(ctx, xtiles, std::max<size_t>(t.size(), 1) * sizeof(Tile), "alloc cross tiles");
       if (!t.empty())
-        ck(ctx, hipMemcpy(xtiles.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
-           "upload cross tiles");
+        upload_bytes(ctx, xtiles.p, t.data(), t.size() * sizeof(Tile), "upload cross tiles");
     }
     const size_t need = (size_t)(5 * (npad / NB) + 8);
     while (ev.size() < need) {

@@ -98,8 +98,16 @@ void nck(ace_ctx *ctx, ncclResult_t e, const char *what) {
   throw Fail{ACE_ERR_HIP};
 }
 
-// Host-callback collectives: stage through host buffers (the stream is
-// synchronised first; the copies back are synchronous too).
+// Host-callback collectives: stage through host buffers, every copy
+// stream-ordered on `st` and drained (bounded) before the host touches it.
+void d2h(ace_ctx *ctx, void *h, const void *d, size_t bytes, hipStream_t st) {
+  ck(ctx, hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, st), "stage");
+  sync_stream(ctx, st, "stage");
+}
+void h2d(ace_ctx *ctx, void *d, const void *h, size_t bytes, hipStream_t st) {
+  ck(ctx, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st), "unstage");
+  sync_stream(ctx, st, "unstage");
+}
 void hck(ace_ctx *ctx, int rc, const char *what) {
   if (rc == 0) return;
   ctx->err = std::string(what) + ": host collective returned " + std::to_string(rc);
@@ -109,28 +117,25 @@ void hck(ace_ctx *ctx, int rc, const char *what) {
 void host_bcast(ace_ctx *ctx, const ace_comm_ops &o, double *dbuf, size_t count, int root,
                 hipStream_t st) {
   std::vector<double> h(count);
-  ck(ctx, hipStreamSynchronize(st), "sync");
-  ck(ctx, hipMemcpy(h.data(), dbuf, count * sizeof(double), hipMemcpyDeviceToHost), "stage");
+  d2h(ctx, h.data(), dbuf, count * sizeof(double), st);
   hck(ctx, o.broadcast(o.user, h.data(), (int64_t)count, root), "broadcast");
-  ck(ctx, hipMemcpy(dbuf, h.data(), count * sizeof(double), hipMemcpyHostToDevice), "unstage");
+  h2d(ctx, dbuf, h.data(), count * sizeof(double), st);
 }
 
 void host_allgather(ace_ctx *ctx, const ace_comm_ops &o, const double *dsend, double *drecv,
                     size_t count, int world, hipStream_t st) {
   std::vector<double> hs(count), hr(count * (size_t)world);
-  ck(ctx, hipStreamSynchronize(st), "sync");
-  ck(ctx, hipMemcpy(hs.data(), dsend, count * sizeof(double), hipMemcpyDeviceToHost), "stage");
+  d2h(ctx, hs.data(), dsend, count * sizeof(double), st);
   hck(ctx, o.allgather(o.user, hs.data(), hr.data(), (int64_t)count), "allgather");
-  ck(ctx, hipMemcpy(drecv, hr.data(), hr.size() * sizeof(double), hipMemcpyHostToDevice), "unstage");
+  h2d(ctx, drecv, hr.data(), hr.size() * sizeof(double), st);
 }
 
 void host_allreduce(ace_ctx *ctx, const ace_comm_ops &o, double *dbuf, size_t count, int op,
                     hipStream_t st) {
   std::vector<double> h(count);
-  ck(ctx, hipStreamSynchronize(st), "sync");
-  ck(ctx, hipMemcpy(h.data(), dbuf, count * sizeof(double), hipMemcpyDeviceToHost), "stage");
+  d2h(ctx, h.data(), dbuf, count * sizeof(double), st);
   hck(ctx, o.allreduce(o.user, h.data(), (int64_t)count, op), "allreduce");
-  ck(ctx, hipMemcpy(dbuf, h.data(), count * sizeof(double), hipMemcpyHostToDevice), "unstage");
+  h2d(ctx, dbuf, h.data(), count * sizeof(double), st);
 }
 
 // ------------------------------------------------------------------ rank
@@ -198,9 +203,7 @@ int64_t ncols_local(int64_t naug, int G, int r) {
 
 void upload_tiles(ace_ctx *ctx, DBuf &b, const std::vector<Tile> &t) {
   alloc(ctx, b, std::max<size_t>(t.size(), 1) * sizeof(Tile), "alloc tiles");
-  if (!t.empty())
-    ck(ctx, hipMemcpy(b.p, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice),
-       "upload tiles");
+  upload_bytes(ctx, b.p, t.data(), t.size() * sizeof(Tile), "upload tiles");
 }
 
 ShardSweep sweep_view(const ShardModel &m, RankState &R, int which) {
@@ -690,8 +693,7 @@ void shard_set_data(ShardModel *m, const double *y, const double *X, const doubl
   std::copy(y, y + m->n, yp.begin());
   for (auto &R : m->ranks) {
     upload_side(ctx, R->side, m->s, X, Z, m->n, m->npad);
-    ck(ctx, hipMemcpy(R->y.p, yp.data(), yp.size() * sizeof(double), hipMemcpyHostToDevice),
-       "upload y");
+    upload_bytes(ctx, R->y.p, yp.data(), yp.size() * sizeof(double), "upload y");
   }
   sync(ctx);
 }

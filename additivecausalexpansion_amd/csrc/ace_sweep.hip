@@ -2643,9 +2643,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
     if ((r = hipEventRecord(sy->ev[2 * G], side)) != hipSuccess) return r;
     return hipEventRecord(E2(G), side2);
   };
-  if ((e = hipStreamWaitEvent(side2, sy->asm_done ? sy->asm_done : sy->ev[2 * steps], 0)) !=
-      hipSuccess)
-    return e;
+  if ((e = hipStreamWaitEvent(side2, sy->ev[2 * steps], 0)) != hipSuccess) return e;
   if ((e = produce(0)) != hipSuccess) return e;
   int used = 0;
   for (int g = 0; g < ng; ++g) {

@@ -21,7 +21,8 @@ Multi-GPU (torchrun, one process per GPU):
     count (C3 n=32768 at 4, C4 n=65536 at 8, C2-shaped n = 16384 N^(1/3)
     otherwise), with the weak-scaling efficiency of SURVEY §8d,
     E(N) = [n_N^3 / t_N / N] / [16384^3 / t_1], t_1 = this run's C2 step.
-    A watchdog bounds it; the headline line is printed regardless.
+    A watchdog bounds it; the headline line is printed regardless, and a
+    failed or timed-out leg then ends the run with exit status 3.
   * `--mode sharded`: the sharded leg alone (also at N = 1, where it runs the
     RCCL code path with one rank).
 
@@ -184,6 +185,34 @@ def shard_config(world, name=None):
         return ("C2",) + tuple(CONFIGS["C2"])
     n = int(round(N1 * world ** (1.0 / 3.0) / 256.0)) * 256
     return (f"C2-shape n={n}", n, 20, 10, "Matern32")
+
+
+EXIT_SHARDED_FAILED = 3
+
+
+def run_guarded(line, fn, timeout):
+    """Runs the sharded leg fn() under a watchdog.  Returns (result, failed):
+    an exception gives ({"error": ...}, True) and the caller prints the
+    headline line, then exits EXIT_SHARDED_FAILED.  A leg still running
+    after `timeout` s (a hung collective) prints the headline line with the
+    error (rank 0) and ends the process at once with EXIT_SHARDED_FAILED:
+    the line is never lost and the hang always shows in the exit status."""
+    def watchdog():
+        if line is not None:
+            line["sharded"] = {"error": f"timed out after {timeout:.0f} s"}
+            print(json.dumps(line), flush=True)
+        sys.stderr.write(f"bench: sharded leg timed out after {timeout:.0f} s\n")
+        sys.stderr.flush()
+        os._exit(EXIT_SHARDED_FAILED)
+    timer = threading.Timer(timeout, watchdog)
+    timer.daemon = True
+    timer.start()
+    try:
+        return fn(), False
+    except Exception as e:  # the headline line is still printed by the caller
+        return {"error": f"{type(e).__name__}: {e}"[:300]}, True
+    finally:
+        timer.cancel()
 
 
 def make_step(kernel, p, B, theta, std_y, ctx, y, X, Z, model=None):
@@ -465,23 +494,13 @@ def main():
     if world > 1 and a.mode == "auto":
         model.close()
 
-        def watchdog():  # a hung collective must not cost the headline line
-            if line is not None:
-                line["sharded"] = {"error": f"timed out after {a.shard_timeout:.0f} s"}
-                print(json.dumps(line), flush=True)
-            os._exit(0)
-        timer = threading.Timer(a.shard_timeout, watchdog)
-        timer.daemon = True
-        timer.start()
-        try:
+        def leg():
             sh = run_sharded(dist, rank, world, ctx, a.shard_steps, 1)
             t1 = dt_max / a.steps
             sh["weak_scaling_efficiency"] = (sh["n"] ** 3 / (sh["ms_per_step"] * 1e-3) / world) / (
                 n ** 3 / t1) if a.config == "C2" else None
-        except Exception as e:  # reported, never fatal for the headline
-            sh = {"error": f"{type(e).__name__}: {e}"[:300]}
-            failed = True
-        timer.cancel()
+            return sh
+        sh, failed = run_guarded(line, leg, a.shard_timeout)
         if line is not None:
             line["sharded"] = sh
             # SURVEY §8d's weak-scaling efficiency of ONE sharded evaluation
@@ -490,9 +509,9 @@ def main():
             line["sharded_weak_scaling_efficiency"] = sh.get("weak_scaling_efficiency")
     if line is not None:
         print(json.dumps(line), flush=True)
-    if failed:  # peers may be stuck in a collective: no barrier
+    if failed:  # peers may be stuck in a collective: no barrier; rc shows it
         sys.stdout.flush()
-        os._exit(0)
+        os._exit(EXIT_SHARDED_FAILED)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -46,7 +46,10 @@ enum ace_status {
   ACE_ERR_OOM = 3,         /* device allocation failed                          */
   ACE_ERR_UNSUPPORTED = 4, /* shape outside the compiled range (p > 64, B > 32) */
   ACE_ERR_NONFINITE = 5,   /* non-finite gradient in ace_model_train (R's stop()) */
-  ACE_ERR_INTERRUPTED = 6  /* the interrupt poll asked to stop                  */
+  ACE_ERR_INTERRUPTED = 6, /* the interrupt poll asked to stop                  */
+  ACE_ERR_TIMEOUT = 7      /* device work did not drain within ACE_SYNC_TIMEOUT
+                              seconds (default 600): a stalled queue or a hung
+                              collective; ace_last_error names the busy streams */
 };
 
 typedef struct ace_ctx ace_ctx;
@@ -54,7 +57,9 @@ typedef struct ace_model ace_model;
 
 /* ---------------------------------------------------------------- context */
 int ace_abi_version(void);
-/* Creates a context on HIP device `device` (one process per GPU). */
+/* Creates a context on HIP device `device` (one process per GPU).  It owns
+ * up to three non-blocking HIP streams (ACE_STREAMS = 3, 2 or 1; results are
+ * bit-identical for every value) and never uses the null stream. */
 int ace_create(int device, ace_ctx **out);
 void ace_destroy(ace_ctx *ctx);
 /* Message of the last failure on this context ("" if none).  NULL ctx gives

@@ -330,10 +330,32 @@ List kernmat_Matern32_symmetric_cpp(NumericMatrix X, SEXP Z, NumericVector param
   return kernmat_sym(ACE_KERNEL_MATERN32, X, Z, parameters);
 }
 
+// `$eigenval` holds the sweep's pivots (the squared Cholesky diagonal), not
+// the eigenvalues src/kernel_SE_cpp.cpp:144-156 returns.  Every in-package
+// consumer uses only sum(log(eigenval)) (src/kernel_SE_cpp.cpp:240,
+// src/kernel_Matern_cpp.cpp:463, src/stats_cpp.cpp:29), which is log det A
+// for both, bit for bit as before.  A caller reading the values themselves
+// is told: attr(x, "ace_kind") is "pivots", and the first call in a session
+// emits a one-time R warning saying so (options(ace.quiet_pivots = TRUE)
+// silences it).
+static void mark_pivots(NumericVector &ev) {
+  ev.attr("ace_kind") = "pivots";
+  static bool told = false;
+  if (told) return;
+  told = true;
+  Function getopt("getOption");
+  const SEXP quiet = getopt("ace.quiet_pivots", false);
+  if (!Rf_asLogical(quiet))
+    Rf_warning("ace (MI355X engine): invkernel_cpp()$eigenval holds the elimination pivots of "
+               "the SPD inverse (attr \"ace_kind\" = \"pivots\"), not eigenvalues; "
+               "sum(log(.)) = log det A as in the reference.  This warning is shown once.");
+}
+
 // [[Rcpp::export]]
 List invkernel_cpp(SEXP pdmat, double sigma) {
   const int64_t n = nrows_of(pdmat);
   NumericVector ev(n);
+  mark_pivots(ev);
   if (use_handles() || is_device(pdmat)) {
     Temps t;
     ace_dmat *inv = nullptr;

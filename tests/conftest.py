@@ -42,3 +42,28 @@ def ref_c():
     L.ref_mu_solution.argtypes = [I64, D, D]
     L.ref_mu_solution.restype = ctypes.c_double
     return L
+
+
+def run_child(code, env=None, timeout=100):
+    """Runs a Python snippet in a fresh interpreter (a clean HIP runtime per
+    A/B variant).  A child that stalls dumps every thread's Python stack
+    (faulthandler) 10 s before its limit and exits, so a hang names the call
+    it was blocked in; on any failure the child's stdout / stderr tail is in
+    the assertion message.  The library's own bounded sync (ACE_SYNC_TIMEOUT)
+    is set below the limit so a stalled stream reports which streams held
+    work before faulthandler fires."""
+    import subprocess
+    env = dict(os.environ if env is None else env)
+    env.setdefault("ACE_SYNC_TIMEOUT", str(max(5, timeout - 25)))
+    pre = f"import faulthandler; faulthandler.dump_traceback_later({max(5, timeout - 10)}, exit=True)\n"
+    try:
+        r = subprocess.run([sys.executable, "-c", pre + code], env=env, timeout=timeout,
+                           capture_output=True, text=True)
+    except subprocess.TimeoutExpired as e:
+        out = (e.stdout or b"")[-3000:] if isinstance(e.stdout, bytes) else (e.stdout or "")[-3000:]
+        err = (e.stderr or b"")[-6000:] if isinstance(e.stderr, bytes) else (e.stderr or "")[-6000:]
+        raise AssertionError(f"child timed out after {timeout} s\n--- stdout\n{out}\n--- stderr\n{err}")
+    if r.returncode != 0:
+        raise AssertionError(f"child exited {r.returncode}\n--- stdout\n{r.stdout[-3000:]}\n"
+                             f"--- stderr\n{r.stderr[-6000:]}")
+    return r

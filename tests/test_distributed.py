@@ -58,3 +58,41 @@ def test_single_process_path_has_no_collective():
     dist, rank, world, local = bench._dist_init()
     assert dist is None and world == 1 and rank == 0
     assert bench._allreduce_max(None, 3.5) == 3.5
+
+
+_GUARD = """
+import sys, time, json
+sys.path.insert(0, {root!r})
+import bench
+line = {{"metric": "m", "value": 1.5}}
+def leg():
+    {body}
+sh, failed = bench.run_guarded(line, leg, {timeout})
+line["sharded"] = sh
+print(json.dumps(line), flush=True)
+if failed:
+    bench.os._exit(bench.EXIT_SHARDED_FAILED)
+"""
+
+
+@pytest.mark.parametrize("body,timeout,rc,err", [
+    ("return {'evals_per_s': 2.0}", 30, 0, None),
+    ("raise RuntimeError('rccl')", 30, 3, "RuntimeError: rccl"),
+    ("time.sleep(60)", 1.0, 3, "timed out after 1 s"),  # a hung collective
+])
+def test_sharded_leg_failure_shows_in_exit_status(body, timeout, rc, err):
+    """bench.py's sharded leg (N > 1) runs under a watchdog: a leg that
+    raises or hangs still gets the headline line printed, and the run then
+    exits non-zero (EXIT_SHARDED_FAILED = 3), so a hung collective is visible
+    in the driver's rc rather than hidden behind rc 0."""
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", _GUARD.format(root=ROOT, body=body, timeout=timeout)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == rc, r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["value"] == 1.5  # the headline survives
+    if err is None:
+        assert line["sharded"] == {"evals_per_s": 2.0}
+    else:
+        assert err in line["sharded"]["error"]

@@ -13,6 +13,8 @@ Tolerances (north_star: "within 1e-6 relative fp64"):
 import math
 
 import numpy as np
+
+from conftest import run_child
 import pytest
 from conftest import golden, golden_names
 
@@ -443,8 +445,7 @@ def test_update_tile_order_is_bitwise_neutral(A, tmp_path):
     for S in ("0", "2", "4"):
         out = str(tmp_path / f"inv{S}.npy")
         env = dict(os.environ, ACE_UPD_ORDER=S)
-        subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
-                       env=env, check=True, timeout=100)
+        run_child(_ORDER_SNIPPET.format(root=root, inp=inp, out=out), env=env, timeout=100)
         outs[S] = np.load(out)
     assert np.array_equal(outs["0"], outs["4"]) and np.array_equal(outs["2"], outs["4"])
     mine = A.invkernel_cpp(K, th[0])["inv"]  # this process: default order
@@ -469,8 +470,7 @@ def test_cross_update_on_tiles_is_bitwise_neutral(A, tmp_path):
     for v in ("0", "1"):
         out = str(tmp_path / f"inv{v}.npy")
         env = dict(os.environ, ACE_XUPD=v)
-        subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
-                       env=env, check=True, timeout=100)
+        run_child(_ORDER_SNIPPET.format(root=root, inp=inp, out=out), env=env, timeout=100)
         outs[v] = np.load(out)
     assert np.array_equal(outs["0"], outs["1"])
     assert np.array_equal(A.invkernel_cpp(K, th[0])["inv"], outs["0"])
@@ -532,8 +532,7 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)
-        subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
-                       env=env, check=True, timeout=100)
+        run_child(_ORDER_SNIPPET.format(root=root, inp=inp, out=out), env=env, timeout=100)
         outs[name] = np.load(out)
     for name in variants:
         assert np.array_equal(outs["single"], outs[name]), name
@@ -553,8 +552,7 @@ def test_gather_pivot_is_bitwise_neutral(A, tmp_path):
     np.savez(inp, K=K, s=th[0])
     out = str(tmp_path / "inv0.npy")
     env = dict(os.environ, ACE_GATHER_PIV="1")
-    subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
-                   env=env, check=True, timeout=100)
+    run_child(_ORDER_SNIPPET.format(root=root, inp=inp, out=out), env=env, timeout=100)
     assert np.array_equal(A.invkernel_cpp(K, th[0])["inv"], np.load(out))
 
 
@@ -574,8 +572,7 @@ def test_split_panel_is_bitwise_neutral(A, tmp_path):
     np.savez(inp, K=K, s=th[0])
     out = str(tmp_path / "inv0.npy")
     env = dict(os.environ, ACE_CHAIN="0")
-    subprocess.run([sys.executable, "-c", _ORDER_SNIPPET.format(root=root, inp=inp, out=out)],
-                   env=env, check=True, timeout=100)
+    run_child(_ORDER_SNIPPET.format(root=root, inp=inp, out=out), env=env, timeout=100)
     assert np.array_equal(A.invkernel_cpp(K, th[0])["inv"], np.load(out))
 
 
@@ -603,23 +600,24 @@ def test_merged_cross_model_is_bitwise_neutral(tmp_path, n):
     kernel) gives the same gradient and stats bit for bit as the side-stream
     cross launches, over two evaluations (the per-sweep counter reset).
     n = 2000: 8 steps; 2600: 11 (a last single step).  Also the default
-    schedule with its assembly on one unmasked stream (ACE_ASM_RESERVE=0)."""
+    schedule under the smaller stream budgets (ACE_STREAMS=2: the tail path
+    on the panel stream; 1: everything on the main stream), which run the
+    same launch graph serialised in host order."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
     z2 = dict(ACE_GROUP="2", ACE_HEADS="0")  # the merged / split cross are Z = 2 schedules
-    for v in ("0", "1", "split", "group4", "heads4", "heads2", "noreserve"):
+    for v in ("0", "1", "split", "group4", "heads4", "heads2", "streams2", "streams1"):
         out = str(tmp_path / f"m{v}.npy")
         env = (dict(os.environ, ACE_XSPLIT="1", **z2) if v == "split" else
-               dict(os.environ, ACE_ASM_RESERVE="0") if v == "noreserve" else
+               dict(os.environ, ACE_STREAMS=v[-1]) if v.startswith("streams") else
                dict(os.environ, ACE_GROUP="4", ACE_HEADS="0") if v == "group4" else
                dict(os.environ, ACE_GROUP="4", ACE_HEADS="1") if v == "heads4" else
                dict(os.environ, ACE_GROUP="2", ACE_HEADS="1") if v == "heads2" else
                dict(os.environ, ACE_XMERGE=v, **z2))
-        subprocess.run([sys.executable, "-c", _MODEL_SNIPPET.format(root=root, n=n, out=out)],
-                       env=env, check=True, timeout=100)
+        run_child(_MODEL_SNIPPET.format(root=root, n=n, out=out), env=env, timeout=100)
         outs[v] = np.load(out)
     assert np.all(np.isfinite(outs["1"]))
     assert np.array_equal(outs["0"], outs["1"])
@@ -630,5 +628,6 @@ def test_merged_cross_model_is_bitwise_neutral(tmp_path, n):
     # the head / tail lookahead split (ACE_HEADS=1) at four and two steps
     assert np.array_equal(outs["0"], outs["heads4"])
     assert np.array_equal(outs["0"], outs["heads2"])
-    # the default's assembly on the CU-masked stream against one unmasked stream
-    assert np.array_equal(outs["heads4"], outs["noreserve"])
+    # the default (heads4) on two streams and on one
+    assert np.array_equal(outs["heads4"], outs["streams2"])
+    assert np.array_equal(outs["heads4"], outs["streams1"])

@@ -10,6 +10,8 @@ cond x larger than the result under Q6's theta mix, so it is held to 1e-6
 of the cancelled terms std_y^2 (|K_xx,rr| + q_r).
 """
 import numpy as np
+
+from conftest import run_child
 import pytest
 from test_gpu import close
 
@@ -259,9 +261,7 @@ def test_triangular_variance_matches_full_product(tmp_path, kernel):
     for v in ("0", "1"):
         out = str(tmp_path / f"p{v}.npy")
         env = dict(os.environ, ACE_PRED_TRI=v)
-        subprocess.run([sys.executable, "-c",
-                        _TRI_SNIPPET.format(root=root, n=2300, nx=700, kernel=kernel, out=out)],
-                       env=env, check=True, timeout=100)
+        run_child(_TRI_SNIPPET.format(root=root, n=2300, nx=700, kernel=kernel, out=out), env=env, timeout=100)
         outs[v] = np.load(out)
     a, b = outs["0"], outs["1"]
     assert a.shape == b.shape and np.all(np.isfinite(a) == np.isfinite(b))

@@ -12,6 +12,8 @@ all-gather, all-reduce) on the single card.
 Tolerances as in test_gpu.py: gradients / stats 1e-6 relative (north star),
 inverse 1e-9 of its scale."""
 import numpy as np
+
+from conftest import run_child
 import pytest
 from test_gpu import close
 
@@ -179,8 +181,7 @@ def test_sharded_pair_schedule_is_bitwise_neutral(tmp_path, world, n):
     for v, extra in variants.items():
         out = str(tmp_path / f"s{v}.npz")
         env = dict(os.environ, **extra)
-        subprocess.run([sys.executable, "-c", _SCHED.format(root=root, n=n, world=world, out=out)],
-                       env=env, check=True, timeout=100)
+        run_child(_SCHED.format(root=root, n=n, world=world, out=out), env=env, timeout=100)
         outs[v] = np.load(out)
     for v in ("pair", "fused"):
         for k in ("g1", "s1", "g2", "s2", "inv"):

@@ -15,6 +15,8 @@ import subprocess
 import sys
 
 import numpy as np
+
+from conftest import run_child
 import pytest
 from conftest import golden
 from test_gpu import close
@@ -79,8 +81,7 @@ np.savez({out!r}, stats=f["train_stats"]["stats"], theta=f["Kernel"].parameters,
 def _loop(tmp_path, kernel, tol, sync):
     out = str(tmp_path / f"t{sync}_{tol}.npz")
     env = dict(os.environ, ACE_TRAIN_SYNC=str(sync))
-    subprocess.run([sys.executable, "-c", _LOOP.format(root=ROOT, kernel=kernel, tol=tol, out=out)],
-                   env=env, check=True, timeout=100)
+    run_child(_LOOP.format(root=ROOT, kernel=kernel, tol=tol, out=out), env=env, timeout=100)
     return np.load(out)
 
 
@@ -152,7 +153,7 @@ def _fit(tmp_path, kernel, mode, tol, maxiter, sync=1):
     out = str(tmp_path / f"{mode}_{sync}_{maxiter}_{tol}.npz")
     env = dict(os.environ, ACE_TRAIN_SYNC=str(sync))
     src = _FIT.format(root=ROOT, kernel=kernel, mode=mode, tol=tol, maxiter=maxiter, out=out)
-    subprocess.run([sys.executable, "-c", src], env=env, check=True, timeout=100)
+    run_child(src, env=env, timeout=100)
     return np.load(out)
 
 
