@@ -55,6 +55,16 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 #ifndef ACE_GRAD_XIREG
 #define ACE_GRAD_XIREG 0
 #endif
+// GEMM2's last column block when PM is not a multiple of 16 (p = 20: 4 live
+// features of 16): on v_mfma_f64_4x4x4_4b_f64 (ACE_GRAD_TAIL4=1, default),
+// one 4-feature group per instruction at 17 cycles instead of a 16-wide
+// block at 64 (profiles/r04_probe_mfma_f64.txt: 4 blocks of 4x4x4, A lane
+// 16k + 4m + i, B lane 16k + 4m + j, D lane 16i + 4m + j for block m).  The
+// GEMM1 result fragment is its A operand as it stands: lane (lr = 4m + i,
+// lk = k) holds U[row lr][column 4kk + k] for k-step kk.
+#ifndef ACE_GRAD_TAIL4
+#define ACE_GRAD_TAIL4 1
+#endif
 #define MM_PAIR_FENCE(cb, v) \
   if (ACE_MM_PG > 0 && ((4 * (cb) + (v) + 1) % (ACE_MM_PG > 0 ? ACE_MM_PG : 1)) == 0) \
     __builtin_amdgcn_sched_barrier(0)
@@ -147,6 +157,58 @@ __device__ __forceinline__ double exp_tb5(double x, const double *tab) {
   return __builtin_amdgcn_ldexp(q * tab[ki & 31], ki >> 5);
 }
 
+// 2^(j/128), j = 0..127, correctly rounded (Python Decimal at 60 digits)
+__device__ const double kExp2Tab128[128] = {
+    1.0, 1.0054299011128027, 1.0108892860517005, 1.016378314910953,
+    1.0218971486541166, 1.0274459491187637, 1.0330248790212284, 1.0386341019613787,
+    1.0442737824274138, 1.0499440858006872, 1.0556451783605572, 1.061377227289262,
+    1.0671404006768237, 1.0729348675259756, 1.0787607977571199, 1.0846183622133092,
+    1.0905077326652577, 1.0964290818163769, 1.102382583307841, 1.1083684117236787,
+    1.1143867425958924, 1.1204377524096067, 1.1265216186082418, 1.1326385195987192,
+    1.1387886347566916, 1.1449721444318042, 1.1511892299529827, 1.1574400736337511,
+    1.1637248587775775, 1.1700437696832502, 1.1763969916502812, 1.182784710984341,
+    1.189207115002721, 1.1956643920398273, 1.202156731452703, 1.2086843236265816,
+    1.215247359980469, 1.2218460329727576, 1.22848053610687, 1.2351510639369334,
+    1.241857812073484, 1.2486009771892048, 1.255380757024691, 1.2621973503942507,
+    1.2690509571917332, 1.275941778396392, 1.2828700160787783, 1.2898358734066657,
+    1.2968395546510096, 1.3038812651919358, 1.3109612115247644, 1.318079601266064,
+    1.3252366431597413, 1.3324325470831615, 1.339667524053303, 1.3469417862329458,
+    1.3542555469368927, 1.3616090206382248, 1.3690024229745905, 1.3764359707545302,
+    1.383909881963832, 1.3914243757719262, 1.3989796725383112, 1.4065759938190154,
+    1.4142135623730951, 1.4218926021691656, 1.42961333839197, 1.4373759974489824,
+    1.4451808069770467, 1.4530279958490526, 1.460917794180647, 1.4688504333369818,
+    1.4768261459394993, 1.4848451658727524, 1.4929077282912648, 1.5010140696264256,
+    1.5091644275934228, 1.5173590411982147, 1.5255981507445384, 1.533881997840956,
+    1.5422108254079407, 1.550584877685, 1.559004400237837, 1.567469639965553,
+    1.5759808451078865, 1.5845382652524937, 1.593142151342267, 1.6017927556826934,
+    1.6104903319492543, 1.6192351351948637, 1.6280274218573478, 1.6368674497669644,
+    1.645755478153965, 1.6546917676561943, 1.6636765803267364, 1.6727101796415966,
+    1.681792830507429, 1.6909247992693053, 1.7001063537185235, 1.709337763100463,
+    1.718619298122478, 1.7279512309618377, 1.7373338352737062, 1.746767386199169,
+    1.7562521603732995, 1.7657884359332727, 1.7753764925265212, 1.785016611318935,
+    1.7947090750031072, 1.804454167806624, 1.8142521755003989, 1.8241033854070534,
+    1.8340080864093424, 1.843966568958626, 1.8539791250833855, 1.864046048397789,
+    1.8741676341103, 1.8843441790323345, 1.8945759815869656, 1.9048633418176741,
+    1.9152065613971474, 1.925605943636125, 1.9360617934922943, 1.9465744175792332,
+    1.9571441241754002, 1.9677712232331759, 1.978456026387951, 1.9891988469672663,
+};
+// exp for the gradient's trace factors (ACE_GRAD_EXP=2): the 128-entry
+// table, |r| <= ln2/256, degree-4 Taylor (truncation < 1.3e-15 relative, the
+// degree-5 / 32-entry form's class) -- one FMA fewer per pair than exp_tb5.
+// The split of ln2/128 is exp_tb's ln2/32 split divided by 4 (exact).
+__device__ __forceinline__ double exp_tb128(double x, const double *tab) {
+  const double kf = __builtin_rint(x * 184.66496523378732);  // 128 / ln2
+  double r = fma(-kf, 0.02166084938653512 * 0.25, x);          // (ln2 / 128) hi
+  r = fma(-kf, 5.9631716539705866e-12 * 0.25, r);              // (ln2 / 128) lo
+  const int ki = (int)kf;
+  double q = 1.0 / 24.0;
+  q = fma(q, r, 1.0 / 6.0);
+  q = fma(q, r, 0.5);
+  q = fma(q, r, 1.0);
+  q = fma(q, r, 1.0);
+  return __builtin_amdgcn_ldexp(q * tab[ki & 127], ki >> 7);
+}
+
 // Table-free form for the gradient's trace factors (ACE_GRAD_EXP=1):
 // x = m ln2 + r, |r| <= ln2/2, exp(r) by a degree-10 polynomial with the
 // first three Taylor coefficients pinned and the rest fitted on Chebyshev
@@ -173,12 +235,12 @@ __device__ __forceinline__ double exp_pl(double x) {
   return __builtin_amdgcn_ldexp(q, (int)kf);
 }
 __device__ __forceinline__ double exp_grad(double x, const double *tab) {
-  return ACE_GRAD_EXP ? exp_pl(x) : exp_tb5(x, tab);
+  return ACE_GRAD_EXP == 2 ? exp_tb128(x, tab) : ACE_GRAD_EXP ? exp_pl(x) : exp_tb5(x, tab);
 }
 // degree-11 form of exp_pl (7e-18 relative over the interval) for the
 // assembly (ACE_ASM_EXP=1): K enters the inverse
 #ifndef ACE_ASM_EXP
-#define ACE_ASM_EXP 0
+#define ACE_ASM_EXP 2
 #endif
 __device__ __forceinline__ double exp_pl11(double x) {
   const double kf = __builtin_rint(x * 1.4426950408889634);
@@ -198,8 +260,43 @@ __device__ __forceinline__ double exp_pl11(double x) {
   q = fma(q, r, 1.0);
   return __builtin_amdgcn_ldexp(q, (int)kf);
 }
+// 2^(j/64), j = 0..63, correctly rounded (Python Decimal at 60 digits)
+__device__ const double kExp2Tab64[64] = {
+    1.0, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
+    1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
+    1.0905077326652577, 1.102382583307841, 1.1143867425958924, 1.1265216186082418,
+    1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
+    1.189207115002721, 1.202156731452703, 1.215247359980469, 1.22848053610687,
+    1.241857812073484, 1.255380757024691, 1.2690509571917332, 1.2828700160787783,
+    1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.339667524053303,
+    1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
+    1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
+    1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
+    1.5422108254079407, 1.559004400237837, 1.5759808451078865, 1.593142151342267,
+    1.6104903319492543, 1.6280274218573478, 1.645755478153965, 1.6636765803267364,
+    1.681792830507429, 1.7001063537185235, 1.718619298122478, 1.7373338352737062,
+    1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
+    1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
+    1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951,
+};
+// exp for the assembly (ACE_ASM_EXP=2, default): the 64-entry table, |r| <=
+// ln2/128, degree-5 Taylor (truncation < 3.6e-17 relative, below half an ulp
+// like exp_tb's degree 6) -- one FMA fewer per pair and slice than exp_tb
+__device__ __forceinline__ double exp_tb64(double x, const double *tab) {
+  const double kf = __builtin_rint(x * 92.33248261689366);  // 64 / ln2
+  double r = fma(-kf, 0.02166084938653512 * 0.5, x);          // (ln2 / 64) hi
+  r = fma(-kf, 5.9631716539705866e-12 * 0.5, r);              // (ln2 / 64) lo
+  const int ki = (int)kf;
+  double q = 1.0 / 120.0;
+  q = fma(q, r, 1.0 / 24.0);
+  q = fma(q, r, 1.0 / 6.0);
+  q = fma(q, r, 0.5);
+  q = fma(q, r, 1.0);
+  q = fma(q, r, 1.0);
+  return __builtin_amdgcn_ldexp(q * tab[ki & 63], ki >> 6);
+}
 __device__ __forceinline__ double exp_asm(double x, const double *tab) {
-  return ACE_ASM_EXP ? exp_pl11(x) : exp_tb(x, tab);
+  return ACE_ASM_EXP == 2 ? exp_tb64(x, tab) : ACE_ASM_EXP ? exp_pl11(x) : exp_tb(x, tab);
 }
 
 // sqrt(x), x >= 0 and normal or 0 (r2 values): hardware rsq (~2^-24
@@ -209,6 +306,20 @@ __device__ __forceinline__ double exp_asm(double x, const double *tab) {
 // (the estimate is taken at max(x, 1e-300)).
 __device__ __forceinline__ double sqrt_pk(double x) {
   const double y = __builtin_amdgcn_rsq(fmax(x, 1e-300));
+  double s = x * y;
+  double h = 0.5 * y;
+  const double e = fma(-h, s, 0.5);
+  s = fma(s, e, s);
+  h = fma(h, e, h);
+  const double d = fma(-s, s, x);
+  return fma(d, h, s);
+}
+
+// sqrt_pk for x >= 1e-300 (the assembly clamps Matern r2 there: t = 1e-150
+// gives the same 1 + sqrt3 t = 1 and exponential as t = 0 in double), without
+// the clamp inside
+__device__ __forceinline__ double sqrt_pk_pos(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
   double s = x * y;
   double h = 0.5 * y;
   const double e = fma(-h, s, 0.5);
@@ -239,7 +350,7 @@ __device__ __forceinline__ double kval_mm(int b, double r2, double lam, double z
     if (zlo == 0.0 || zhi == 0.0) return 0.0;
     return (sgn_mm(zlo) * sgn_mm(zhi)) * exp_asm(((lam - r2) + lzlo) + lzhi, etab);
   } else {
-    const double t = sqrt_pk(r2);
+    const double t = sqrt_pk_pos(r2);  // r2 >= 1e-300 (k_asm_mm)
     const double e = (1.0 + SQRT3 * t) * exp_asm(lam - SQRT3 * t, etab);
     if (b == 0) return e;
     return (e * zlo) * zhi;  // z = 0 gives 0 (the reference's explicit zero test)
@@ -303,7 +414,7 @@ __host__ __device__ inline MmLayout mm_layout(int PM, int B, int KIND, bool grad
   const int NS = (grad && KIND == 1) ? B + 1 : B;
   int off = 0;
   o.etab = off;
-  off += 32;
+  off += (grad && ACE_GRAD_EXP == 2) ? 128 : (!grad && ACE_ASM_EXP == 2) ? 64 : 32;
   o.xj = off;
   off += 64 * xj_pitch(PM);
   o.xi = off;
@@ -374,7 +485,13 @@ __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS
     L.Z[tid - 64] = 1.0;
     if (KIND == 0) L.LZ[tid - 64] = 0.0;
   }
-  if (tid < 32) L.E[tid] = kExp2Tab[tid];
+  if (GRAD && ACE_GRAD_EXP == 2) {
+    for (int e = tid; e < 128; e += NT) L.E[e] = kExp2Tab128[e];
+  } else if (!GRAD && ACE_ASM_EXP == 2) {
+    if (tid < 64) L.E[tid] = kExp2Tab64[tid];
+  } else if (tid < 32) {
+    L.E[tid] = kExp2Tab[tid];
+  }
   for (int e = tid; e < NS * PM; e += NT) L.W[e] = (e < B * PM) ? wk[e] : wlast[e - B * PM];
   __syncthreads();
   // norms: from the per-evaluation table (launch_slice_norms, the same
@@ -585,8 +702,10 @@ __global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 32 ? 3 : 2)) v
         for (int v = 0; v < 4; ++v) {
           const int cl = 16 * cb + lk + 4 * v;
           const int64_t c = C0 + cbase + cl;
-          double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), 0.0);
-          if (DG && c == r) r2 = 0.0;
+          // Matern: r2 >= 1e-300 (sqrt_pk_pos's domain; the same K as 0)
+          constexpr double R2MIN = KIND == 1 ? 1e-300 : 0.0;
+          double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), R2MIN);
+          if (DG && c == r) r2 = R2MIN;
           double zc = 0.0, lzc = 0.0;
           if (b > 0) {
             zc = L.Z[(b - 1) * 64 + cbase + cl];
@@ -712,8 +831,14 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   constexpr bool XIL = PM <= 32;             // row covariates staged in LDS
   constexpr int NV = PM + 1;
   constexpr int NQ = (PM + 15) / 16;         // GEMM2 16-wide column blocks
+  // the last block's PM % 16 features on 4x4x4 MFMAs (NT4 groups of 4); not
+  // in the Matern two-buffer form (large B), where it would spill at 128 VGPRs
+  constexpr bool TAIL4 = ACE_GRAD_TAIL4 && (PM % 16) != 0 && (PS || KIND == 0);
+  constexpr int NT4 = TAIL4 ? (PM % 16) / 4 : 0;
+  constexpr int NQF = TAIL4 ? NQ - 1 : NQ;   // blocks on v_mfma_f64_16x16x4f64
   // GEMM2 column blocks per pass of its k-loop (one at CB = 2: register cap)
-  constexpr int QG = CB == 2 ? (NQ < ACE_MM_QG2 ? NQ : ACE_MM_QG2) : (NQ < ACE_MM_QG ? NQ : ACE_MM_QG);
+  constexpr int QG0 = CB == 2 ? (NQF < ACE_MM_QG2 ? NQF : ACE_MM_QG2) : (NQF < ACE_MM_QG ? NQF : ACE_MM_QG);
+  constexpr int QG = QG0 > 0 ? QG0 : 1;  // (NQF = 0: the loop below does not run)
   constexpr int RS = PM + 1;                 // partial row: [x part | T K]
   constexpr int PER = NWV * RS + 4 * 64;     // per-slice partials (+ column sums)
   constexpr int NKK = 4 * CB;                // GEMM2 k-steps (the wave's columns / 4)
@@ -798,6 +923,18 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
         const int nn = 16 * q + lr;
         xiv[q][v] = nn < PM ? L.XI[(16 * wr + lk + 4 * v) * (PM + 1) + nn] : 0.0;
       }
+  }
+  // tail (TAIL4): this lane's output element of group t is row 16 wr + 4 m4
+  // + i4, feature 16 NQF + 4 t + j4; its covariate is the same every slice
+  const int i4 = lane >> 4, m4 = (lane >> 2) & 3, j4 = lane & 3;
+  double x4[NT4 > 0 ? NT4 : 1];
+  if (TAIL4) {
+    const int rr = 16 * wr + 4 * m4 + i4;
+#pragma unroll
+    for (int t4 = 0; t4 < NT4; ++t4) {
+      const int nn = 16 * NQF + 4 * t4 + j4;
+      x4[t4] = XIL ? L.XI[rr * (PM + 1) + nn] : (R0 + rr < n ? S.X[(R0 + rr) * PM + nn] : 0.0);
+    }
   }
   double fc[CB][4];  // Matern: 1 + sqrt3 t of slice b+1
   d4 acc[CB];
@@ -941,7 +1078,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
     if (ACE_GRAD_PRIO == 1) __builtin_amdgcn_s_setprio(2);
     // GEMM2: V = U X_J, QG column blocks per pass of the k-loop
 #pragma unroll
-    for (int q0 = 0; q0 < ((ACE_DIAG_GRAD & 32) ? 0 : NQ); q0 += QG) {
+    for (int q0 = 0; q0 < ((ACE_DIAG_GRAD & 32) ? 0 : NQF); q0 += QG) {
       d4 a2[QG];
 #pragma unroll
       for (int j = 0; j < QG; ++j) a2[j] = d4{0.0, 0.0, 0.0, 0.0};
@@ -951,7 +1088,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
 #pragma unroll
         for (int j = 0; j < QG; ++j) {
           const int nn = 16 * (q0 + j) + lr;
-          if (q0 + j < NQ)
+          if (q0 + j < NQF)
             a2[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[kk >> 2][kk & 3],
                                                          nn < PM ? xc[nn] : 0.0, a2[j], 0, 0, 0);
         }
@@ -960,7 +1097,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
       // a2[j][v] = V[row 16 wr + lk + 4 v][feature 16 (q0 + j) + lr]
 #pragma unroll
       for (int j = 0; j < QG; ++j) {
-        if (q0 + j >= NQ) continue;
+        if (q0 + j >= NQF) continue;
         const int nn = 16 * (q0 + j) + lr;
         double part = 0.0;
         if (nn < PM) {
@@ -975,6 +1112,33 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
         part = add_xor16(part);
         part = add_xor32(part);
         if (lk == 0 && nn < PM) red[w * RS + nn] = part;
+      }
+    }
+    if (TAIL4 && !(ACE_DIAG_GRAD & 32)) {
+      // V[row 4 m4 + i4][feature 16 NQF + 4 t + j4] = sum_c U X_J over the
+      // wave's columns: 4x4x4 MFMAs, k-step kk = columns 4 kk .. 4 kk + 3
+      double a4[NT4 > 0 ? NT4 : 1];
+#pragma unroll
+      for (int t4 = 0; t4 < NT4; ++t4) a4[t4] = 0.0;
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        const double *xc = L.XJ + (cbase + 4 * kk + i4) * XP + 16 * NQF + j4;
+#pragma unroll
+        for (int t4 = 0; t4 < NT4; ++t4)
+          a4[t4] = __builtin_amdgcn_mfma_f64_4x4x4f64(acc[kk >> 2][kk & 3], xc[4 * t4], a4[t4], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // R of row 4 m4 + i4 (rs holds row lr's sum in every lane of that lr)
+      const double R4 = ACE_GRAD_RVLDS ? L.Rv[16 * w + 4 * m4 + i4] : __shfl(rs, 4 * m4 + i4, 64);
+#pragma unroll
+      for (int t4 = 0; t4 < NT4; ++t4) {
+        const double x = x4[t4];
+        double part = fma(x * x, R4, -2.0 * x * a4[t4]);
+        part = add_xor16(part);   // over i4
+        part = add_xor32(part);
+        part += xor_row(part, 4);  // over m4
+        part += xor_row(part, 8);
+        if (lane < 4) red[w * RS + 16 * NQF + 4 * t4 + j4] = part;
       }
     }
     if (ACE_GRAD_PRIO == 1) __builtin_amdgcn_s_setprio(0);

@@ -1,10 +1,11 @@
 #!/bin/bash
 # One GPU call of several bounded steps (each under its own timeout, chained
 # with &&): $1 = tag, the rest = step names among
-#   probe   tools/probe_mfma_f64 (fp64 MFMA layouts / rates)
+#   probe   tools/probe_mfma_f64 (fp64 MFMA layouts / rates), tools/probe_valu_rates
 #   round   tools/run_round.sh (tests, smoke, bench, rocprof stats)
 #   tests   the GPU test suite alone
 #   bench   bench.py alone
+#   tcc     tools/run_pmc_tcc.sh (L2 hit / miss, HBM traffic per launch)
 #   repro   tools/repro_stall.sh on tools/libace_masked.so, then the default library
 set -o pipefail
 tag=$1; shift
@@ -12,12 +13,19 @@ mkdir -p gpurun_out/$tag
 rc=0
 for step in "$@"; do
   case $step in
-    probe) timeout -k 10 120 ./tools/probe_mfma_f64 > gpurun_out/$tag/probe_mfma.txt 2>&1; rc=$?; tail -4 gpurun_out/$tag/probe_mfma.txt ;;
+    probe) timeout -k 10 120 ./tools/probe_mfma_f64 > gpurun_out/$tag/probe_mfma.txt 2>&1 && \
+           timeout -k 10 120 ./tools/probe_valu_rates > gpurun_out/$tag/probe_valu.txt 2>&1; rc=$?
+           tail -4 gpurun_out/$tag/probe_mfma.txt; cat gpurun_out/$tag/probe_valu.txt ;;
     round) bash tools/run_round.sh $tag; rc=$? ;;
     tests) timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --durations=20 --timeout 120 --timeout-method thread > gpurun_out/$tag/tests.log 2>&1; rc=$?; tail -3 gpurun_out/$tag/tests.log ;;
     bench) timeout -k 10 400 python bench.py --steps 10 --warmup 2 > gpurun_out/$tag/bench.json 2> gpurun_out/$tag/bench.err; rc=$?; cut -c1-600 gpurun_out/$tag/bench.json ;;
     repro) timeout -k 10 420 bash tools/repro_stall.sh tools/libace_masked.so 40 masked; rc=$?
            [ $rc -eq 0 ] && { timeout -k 10 200 bash tools/repro_stall.sh additivecausalexpansion_amd/libace_hip.so 10 default; rc=$?; } ;;
+    tcc) bash tools/run_pmc_tcc.sh $tag/tcc; rc=$? ;;
+    abgrad) bash tools/ab_grad.sh $tag tools/libace_tail.so tools/libace_tailexp.so; rc=$? ;;
+    abnew) bash tools/ab_grad.sh $tag tools/libace_tail.so tools/libace_new.so; rc=$? ;;
+    sq) bash tools/run_sq.sh $tag/sq > /dev/null; rc=$?; cat gpurun_out/$tag/sq/sq.txt | head -80 ;;
+    prof) bash tools/run_prof.sh $tag/prof --steps 5 --warmup 1 > /dev/null; rc=$? ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac
   echo "[step $step rc=$rc]"
