@@ -496,6 +496,43 @@ int ace_pred_marginal(ace_ctx *ctx, int64_t nX, int64_t nx, int B, const double 
 
 }  // extern "C"
 
+// CUs per shader engine the assembly's second part leaves to the first sweep group's
+// head path (ACE_ASM_PERSIST, default 1; 0: the plain grid)
+static int asm_persist_reserve() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_ASM_PERSIST");
+    v = e ? std::max(0, std::min(2, atoi(e))) : 1;
+  }
+  return v;
+}
+
+// with the reservation: ACE_ASM_TAIL=1 (default) lets group 0's tail path run
+// on the reserved CUs beside its head path, =2 after it (0: it waits for the
+// whole assembly); ACE_ASM_FILL=1 (default) hands
+// the reserved CUs back to the assembly's queue once group 0's lookahead is
+// done (a filler launch on side2)
+static int env_flag(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+struct AsmFill {
+  int kind, PM, B, ZS, slots;
+  PairSide ps;
+  int64_t npad, naug;
+  TabView tv;
+  double sig;
+  double *A;
+  int *queue;
+};
+
+static hipError_t asm_fill(void *arg, hipStream_t st) {
+  const AsmFill *f = (const AsmFill *)arg;
+  return launch_assembly_persist(f->kind, f->PM, f->ps, f->npad, f->B, f->ZS, f->tv, f->sig, f->A,
+                                 f->naug, st, f->queue, 0, f->slots);
+}
+
 // A = Kfull + sig I (lower 64-tiles, assembly mode 0) into w.A with the AUG
 // rows [y; 1] (y null: the 1 row only), then the sweep.  The first sweep
 // group's panels' columns are assembled first: that group's pivot chains and
@@ -505,14 +542,21 @@ void assemble_and_sweep(ace_ctx *ctx, SweepWork &w, const Shape &s, const PairSi
                         const TabView &tv, double sig, const double *y, int64_t n,
                         const SweepTiming *tmg, hipEvent_t *ev_asm) {
   hipStream_t st = ctx->stream;
+  const int steps = (int)(w.npad / NB);
+  SweepSync sy = w.sync(ctx);
+  // ACE_ASM_PERSIST=R: the second part as a persistent work queue that
+  // leaves R CUs of every shader engine to the first group's head path
+  // (DESIGN §5); the queue is reset before anything can join it
+  const int R = asm_persist_reserve();
+  const bool persist = R > 0 && sy.side && sy.nev >= 5 * steps + 6 && pairs_use_mm(s.PM, false) &&
+                       mm_lds_ok(s.PM, s.B, s.kind, false);
   ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, n, y, st), "aug init");
   ck(ctx, hipMemsetAsync(w.flag.p, 0, sizeof(int), st), "memset flag");
-  SweepSync sy = w.sync(ctx);
+  if (persist) ck(ctx, hipMemsetAsync(w.aq.p, 0, (2 + 64) * sizeof(int), st), "memset queue");
   if (ev_asm) ck(ctx, hipEventRecord(ev_asm[0], st), "event");
   ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
                           nullptr, st, nullptr, 0, 1, 1),
      "assembly (first panel)");
-  const int steps = (int)(w.npad / NB);
   if (sy.side && sy.nev >= 2 * steps + 1) {  // run_sweep's "inputs ready" event
     ck(ctx, hipEventRecord(sy.ev[2 * steps], st), "event");
     sy.ready_recorded = true;
@@ -528,6 +572,24 @@ void assemble_and_sweep(ace_ctx *ctx, SweepWork &w, const Shape &s, const PairSi
     ck(ctx, hipStreamWaitEvent(ctx->side2, ctx->diag_ev, 0), "wait");
   } else
 #endif
+  AsmFill fill;
+  if (persist && sy.ready_recorded) {
+    ck(ctx, launch_assembly_persist(s.kind, s.PM, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
+                                    st, w.aq.i(), R),
+       "assembly (persistent)");
+    const int tail = env_flag("ACE_ASM_TAIL", 1);
+    if (tail == 0) {  // group 0's tail path after the whole assembly
+      sy.tail_after = sy.ev[5 * steps + 5];
+      ck(ctx, hipEventRecord(sy.tail_after, st), "event");
+    }
+    sy.tail_split = tail == 2;  // ... after group 0's head path
+    const int per = env_flag("ACE_ASM_FILL", 1) ? assembly_persist_per_cu(s.kind, s.PM, s.B) : 0;
+    if (per > 0) {  // the reserved CUs: R per engine, 4 engines per XCD, 8 XCDs
+      fill = AsmFill{s.kind, s.PM, s.B, s.ZS, 32 * R * per, ps, w.npad, w.naug, tv, sig, w.A.d(), w.aq.i()};
+      sy.fill = asm_fill;
+      sy.fill_arg = &fill;
+    }
+  } else
   ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
                           nullptr, st, nullptr, 0, 1, 2),
      "assembly");

@@ -89,6 +89,14 @@ hipError_t launch_assembly_mm(int kind, int PM, PairSide S, int64_t npad, int B,
                               TabView tab, double sig, double *out, int64_t ld,
                               double *kcopy, hipStream_t st, const Tile *tiles,
                               int64_t ntiles, int G, int part = 0);
+// the assembly's second part (part 2 of mode 0) as a persistent work queue
+// that leaves `reserve` CU ids of shader engine 0 of every XCD free (queue:
+// two device ints, reset here on the stream)
+hipError_t launch_assembly_persist(int kind, int PM, PairSide S, int64_t npad, int B, int ZS,
+                                   TabView tab, double sig, double *out, int64_t ld,
+                                   hipStream_t st, int *queue, int reserve, int fill = 0);
+// workgroup slots of one CU for the persistent assembly (0 if unknown)
+int assembly_persist_per_cu(int kind, int PM, int B);
 bool pairs_use_mm(int PM, bool grad);
 bool mm_lds_ok(int PM, int B, int kind, bool grad);
 hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
@@ -221,6 +229,15 @@ struct SweepSync {
   hipEvent_t *ev;
   int nev;
   bool ready_recorded = false;  // caller already recorded ev[2 * steps] ("inputs ready")
+  // recorded on the main stream after the whole assembly: the first group's
+  // tail path waits for it when the assembly's second part leaves CUs to the
+  // head path (ACE_ASM_PERSIST); null: it waits for ev[2 * steps]
+  hipEvent_t tail_after = nullptr;
+  // called on side2 after group 0's tail path, before its completion event
+  // (ACE_ASM_FILL: the persistent assembly's filler launch)
+  hipError_t (*fill)(void *, hipStream_t) = nullptr;
+  bool tail_split = false;  // group 0's tail path after its whole head path
+  void *fill_arg = nullptr;
 };
 // Optional timing of the dominant update launches (k_update<false>): event
 // pairs in ev, executed GEMM flops per timed launch in flops[].

@@ -11,6 +11,7 @@ struct SweepWork {
   DBuf A, Ps[8], Ws[8], SW, S0, S1, piv, flag, order, xtiles, ptiles, gorder, morder, mcnt, htiles;
   int Z = 2;  // steps per bulk launch (sweep_group()), panel slots k % 2Z
   DBuf gtiles;                          // handle path: the gradient's tile list (build_grad_tiles)
+  DBuf aq;                              // persistent assembly: tile counter, exits, CU claims
   DBuf gpart, gwork, gsum;              // handle path: gradient partial-sum scratch
   DBuf norms;                           // handle path: slice norms (TabView::norms)
   int64_t ngtiles = 0, ngdiag = -2;     // -2: not built yet
@@ -38,6 +39,7 @@ struct SweepWork {
     alloc(ctx, S1, (size_t)(SUB * NB) * sizeof(double), "alloc S");
     alloc(ctx, piv, (size_t)npad * sizeof(double), "alloc piv");
     alloc(ctx, flag, 16, "alloc flag");
+    alloc(ctx, aq, (2 + 64) * sizeof(int), "alloc assembly queue");
     norder = 0;
     if (const int S = update_order_block(); S > 0) {
       const std::vector<Tile> t = xcd_update_order(own_tiles(naug / UT, UT, 1, 0), S);

@@ -299,6 +299,7 @@ __device__ __forceinline__ double exp_asm(double x, const double *tab) {
   return ACE_ASM_EXP == 2 ? exp_tb64(x, tab) : ACE_ASM_EXP ? exp_pl11(x) : exp_tb(x, tab);
 }
 
+
 // sqrt(x), x >= 0 and normal or 0 (r2 values): hardware rsq (~2^-24
 // relative), one Goldschmidt step and one correction -- 0 ulp against the
 // correctly rounded sqrt over 4M samples (tools/probe_trans.hip; the
@@ -631,41 +632,23 @@ static int asm_first_cols(int nt) {
 #define ACE_ASM_CB 4
 #endif
 constexpr int ASM_NT = 64 * 4 * (4 / ACE_ASM_CB);
-template <int PM, int KIND>
-__global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, int B, int ZS, TabView tab,
-                                                double sig, double *__restrict__ out, int64_t ld,
-                                                double *__restrict__ kcopy,
-                                                const Tile *__restrict__ tiles, int G, int part,
-                                                int nt, int JB) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  const double sg = tab.sig ? *tab.sig : sig;  // exp(theta[0]) on the diagonal
-  int64_t I, J;
-  // part 1: the tiles of the first sweep group's panels' columns (J < JB =
-  // Z NB / AT, column by column) -- what that group's pivot chains and
-  // lookahead crosses need; part 2: the rest (the lower triangle of tiles >=
-  // JB); 0: every lower tile / the list
-  if (tiles || part == 0) {
-    tile_of(tiles, blockIdx.x, I, J);
-  } else if (part == 1) {
-    int64_t idx = blockIdx.x;
-    J = 0;
-    while (idx >= nt - J) {
-      idx -= nt - J;
-      ++J;
-    }
-    I = J + idx;
-  } else {
-    tile_of(nullptr, blockIdx.x, I, J);
-    I += JB;
-    J += JB;
-  }
+// One lower 64-tile (I, J) of the assembly (k_asm_mm, k_asm_mm_q)
+template <int PM, int KIND, bool LOWER = false>
+__device__ __forceinline__ void asm_mm_tile(double *lds, PairSide S, int B, int ZS, const TabView &tab,
+                                            double sg, double *__restrict__ out, int64_t ld,
+                                            double *__restrict__ kcopy, int64_t I, int64_t J,
+                                            int G) {
   if (G > 1) {
     const int64_t coff = lcol(J * AT, G) - J * AT;
     out += coff * ld;
     if (kcopy) kcopy += coff * ld;
   }
   constexpr int CB = ACE_ASM_CB;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int tid = threadIdx.x;
+  // LOWER (the persistent loop): the lane's indices opaque per tile, so the
+  // compiler does not hoist every lane-derived address out of the tile loop
+  if (LOWER) __asm__ volatile("" : "+v"(tid));
+  const int lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
   const int wr = w & 3, cbase = 16 * CB * (w >> 2);
   const int64_t R0 = I * AT, C0 = J * AT, n = S.n;
@@ -718,7 +701,7 @@ __global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 32 ? 3 : 2)) v
         }
     }
   };
-  if (I == J) slices(std::true_type{});
+  if (!LOWER && I == J) slices(std::true_type{});  // LOWER: strictly lower tiles only
   else slices(std::false_type{});
 #pragma unroll
   for (int cb = 0; cb < CB; ++cb)
@@ -732,6 +715,92 @@ __global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 32 ? 3 : 2)) v
         out[r + c * ld] = (r == c) ? 1.0 : 0.0;  // identity padding
       }
     }
+}
+
+template <int PM, int KIND>
+__global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 32 ? 3 : 2)) void k_asm_mm(PairSide S, int B, int ZS, TabView tab,
+                                                double sig, double *__restrict__ out, int64_t ld,
+                                                double *__restrict__ kcopy,
+                                                const Tile *__restrict__ tiles, int G, int part,
+                                                int nt, int JB) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const double sg = tab.sig ? *tab.sig : sig;  // exp(theta[0]) on the diagonal
+  int64_t I, J;
+  // part 1: the tiles of the first sweep group's panels' columns (J < JB =
+  // Z NB / AT, column by column) -- what that group's pivot chains and
+  // lookahead crosses need; part 2: the rest (the lower triangle of tiles >=
+  // JB); 0: every lower tile / the list
+  if (tiles || part == 0) {
+    tile_of(tiles, blockIdx.x, I, J);
+  } else if (part == 3) {  // the diagonal tiles of part 2 (beside k_asm_mm_q)
+    I = J = JB + (int64_t)blockIdx.x;
+  } else if (part == 1) {
+    int64_t idx = blockIdx.x;
+    J = 0;
+    while (idx >= nt - J) {
+      idx -= nt - J;
+      ++J;
+    }
+    I = J + idx;
+  } else {
+    tile_of(nullptr, blockIdx.x, I, J);
+    I += JB;
+    J += JB;
+  }
+  asm_mm_tile<PM, KIND>(lds, S, B, ZS, tab, sg, out, ld, kcopy, I, J, G);
+}
+
+// The assembly's second part as a persistent work queue (ACE_ASM_PERSIST):
+// one workgroup per launch slot takes tiles of part 2 from a device counter
+// (its strictly lower tiles; the diagonal ones run as a plain grid first)
+// until none are left, and the workgroups that land on a reserved CU -- the
+// first `reserve` CUs of every shader engine to receive one (HW_REG_HW_ID /
+// HW_REG_XCC_ID, tools/probe_hwid.hip) -- leave at once.  Those CUs then stay
+// free for the first sweep group's head path (side stream), which gets no
+// slot beside a full assembly grid: the CU reservation of
+// round 3's masked stream, without a fourth stream.  Every workgroup reaches
+// the exit (the counter runs past nblk); the tiles are those of part 2, each
+// assembled exactly as by k_asm_mm (bit-identical).
+template <int PM, int KIND>
+__global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 24 ? 4 : PM <= 32 ? 3 : 2)) void k_asm_mm_q(
+    PairSide S, int B, int ZS, TabView tab, double sig, double *__restrict__ out, int64_t ld,
+    int *__restrict__ queue, int64_t nblk, int JB, int reserve) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int next;
+  if (reserve > 0) {
+    // at most reserve / 4 of the workgroups leave (queue[1] counts them;
+    // twice the reserved slots): a misread CU id can cost speed, never tiles
+    if (threadIdx.x == 0) {
+      // the first `reserve` CUs of each shader engine that a workgroup lands
+      // on claim the engine's slots queue[2 + 2 (4 xcc + se) + r] (CU id + 1):
+      // workgroups are handed to the engines in turn and wait for a CU of
+      // their own engine, so every engine keeps one, whichever are harvested
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7;  // HW_REG_XCC_ID
+      const unsigned se = (hw >> 13) & 3;
+      const int key = (int)((hw >> 8) & 0xff) + 1;  // cu [11:8], sh [12], se [15:13]
+      int mine = 0;
+      for (int r = 0; r < reserve && !mine; ++r) {
+        const int old = atomicCAS(queue + 2 + 2 * (4 * xcc + se) + r, 0, key);
+        mine = old == 0 || old == key;
+      }
+      next = mine ? (atomicAdd(queue + 1, 1) < (int)gridDim.x * reserve / 4) : 0;
+    }
+    __syncthreads();
+    if (next) return;  // the whole workgroup (one CU)
+    __syncthreads();
+  }
+  const double sg = tab.sig ? *tab.sig : sig;
+  for (;;) {
+    if (threadIdx.x == 0) next = atomicAdd(queue, 1);
+    __syncthreads();  // also: every wave is done with the previous tile's LDS
+    const int64_t idx = next;
+    __syncthreads();
+    if (idx >= nblk) break;
+    int64_t I, J;
+    tile_of(nullptr, idx, I, J);
+    asm_mm_tile<PM, KIND, true>(lds, S, B, ZS, tab, sg, out, ld, nullptr, I + JB + 1, J + JB, 1);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1335,6 +1404,7 @@ static hipError_t asm_mm_pm(int kind, PairSide S, int64_t npad, int B, int ZS, T
   const int64_t nblk = tiles ? ntiles
                        : part == 1 ? JB * nt - JB * (JB - 1) / 2
                        : part == 2 ? (nt - JB) * (nt - JB + 1) / 2
+                       : part == 3 ? nt - JB
                                    : nt * (nt + 1) / 2;
   if (nblk == 0) return hipSuccess;
   const size_t lds = (size_t)mm_layout(PM, B, kind == 0 ? 0 : 1, false).total * sizeof(double);
@@ -1350,6 +1420,90 @@ static hipError_t asm_mm_pm(int kind, PairSide S, int64_t npad, int B, int ZS, T
     hipLaunchKernelGGL((k_asm_mm<PM, 1>), dim3((unsigned)nblk), dim3(ASM_NT), lds, st, S, B, ZS,
                        tab, sig, out, ld, kcopy, tiles, G, part, (int)nt, (int)JB);
   return hipGetLastError();
+}
+
+template <int PM>
+static hipError_t asm_mm_persist_pm(int kind, PairSide S, int64_t npad, int B, int ZS, TabView tab,
+                                    double sig, double *out, int64_t ld, hipStream_t st, int *queue,
+                                    int reserve, int slots, bool fill) {
+  const int64_t nt = npad / AT, JB = asm_first_cols((int)nt);
+  const int64_t nblk = (nt - JB) * (nt - JB - 1) / 2;  // strictly lower tiles of part 2
+  if (nt - JB <= 0) return hipSuccess;
+  const size_t lds = (size_t)mm_layout(PM, B, kind == 0 ? 0 : 1, false).total * sizeof(double);
+  if (lds > 65536) {
+    const void *f = kind == 0 ? (const void *)k_asm_mm_q<PM, 0> : (const void *)k_asm_mm_q<PM, 1>;
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  // part 2's diagonal tiles (the r == c / r < c path) as a plain grid first;
+  // a filler launch (fill: `slots` more workgroups on another stream, none
+  // reserved) only joins the queue of the running one
+  hipError_t e = fill ? hipSuccess
+                      : asm_mm_pm<PM>(kind, S, npad, B, ZS, tab, sig, out, ld, nullptr, st, nullptr, 0, 1, 3);
+  if (e != hipSuccess || nblk == 0) return e;
+  if (fill) reserve = 0;
+  if (kind == 0)
+    hipLaunchKernelGGL((k_asm_mm_q<PM, 0>), dim3((unsigned)slots), dim3(ASM_NT), lds, st, S, B, ZS,
+                       tab, sig, out, ld, queue, nblk, (int)JB, reserve);
+  else
+    hipLaunchKernelGGL((k_asm_mm_q<PM, 1>), dim3((unsigned)slots), dim3(ASM_NT), lds, st, S, B, ZS,
+                       tab, sig, out, ld, queue, nblk, (int)JB, reserve);
+  return hipGetLastError();
+}
+
+// Workgroup slots of k_asm_mm_q (occupancy x CUs), 0 if unknown
+template <int PM>
+static int asm_mm_slots(int kind, int B) {
+  int dev = 0, ncu = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const size_t lds = (size_t)mm_layout(PM, B, kind == 0 ? 0 : 1, false).total * sizeof(double);
+  const void *f = kind == 0 ? (const void *)k_asm_mm_q<PM, 0> : (const void *)k_asm_mm_q<PM, 1>;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, ASM_NT, lds) != hipSuccess) return 0;
+  // never more than the register file holds (the occupancy API can report
+  // one workgroup per CU too many, MI355X_MICROARCH.md): a workgroup that does
+  // not fit at launch would be dispatched later into a reserved CU's slot
+  hipFuncAttributes fa;
+  if (hipFuncGetAttributes(&fa, f) == hipSuccess && fa.numRegs > 0) {
+    const int alloc = (fa.numRegs + 7) / 8 * 8;
+    const int waves = std::min(8, 512 / alloc);  // per SIMD
+    per = std::min(per, waves * 4 / (ASM_NT / 64));
+  }
+  return per * ncu;
+}
+
+int assembly_persist_per_cu(int kind, int PM, int B) {
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+    return 0;
+  switch (PM) {
+#define ACE_CASE(P) \
+  case P: return asm_mm_slots<P>(kind, B) / ncu;
+    ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
+    ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
+#undef ACE_CASE
+    default: return 0;
+  }
+}
+
+hipError_t launch_assembly_persist(int kind, int PM, PairSide S, int64_t npad, int B, int ZS,
+                                   TabView tab, double sig, double *out, int64_t ld,
+                                   hipStream_t st, int *queue, int reserve, int fill) {
+  switch (PM) {
+#define ACE_CASE(P)                                                                          \
+  case P: {                                                                                  \
+    const int slots = fill > 0 ? fill : asm_mm_slots<P>(kind, B);                            \
+    if (slots <= 0) return hipErrorInvalidValue;                                             \
+    return asm_mm_persist_pm<P>(kind, S, npad, B, ZS, tab, sig, out, ld, st, queue, reserve, \
+                                slots, fill > 0);                                            \
+  }
+    ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
+    ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
+#undef ACE_CASE
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_assembly_mm(int kind, int PM, PairSide S, int64_t npad, int B, int ZS,

@@ -573,6 +573,18 @@ constexpr int BK = ACE_BK;  // panel columns staged per LDS buffer
 constexpr int LDL = 144;    // LDS row pitch (doubles): 128 + 16, bank-conflict free
 constexpr int NCH = NB / BK;
 constexpr int UTHREADS = 512;
+// Panel staging (the update / panel-GEMM kernels): each thread moves two
+// double2 of a BK x width chunk row.  ACE_STAGE_SPLIT=1 (default): the two
+// halves of the row (sm and sm + width / 2, sm = 2 (lane % (width / 4))), so
+// each ds_write_b128 lane group of 8 covers 128 contiguous bytes -- all 32
+// write banks -- instead of 8 lanes 32 bytes apart (2-way conflicts,
+// MI355X_MICROARCH.md LDS table).  The LDS layout and the MFMA reads are
+// unchanged: bit-identical.  0: 4 consecutive doubles per thread.
+#ifndef ACE_STAGE_SPLIT
+#define ACE_STAGE_SPLIT 1
+#endif
+constexpr int SM128 = ACE_STAGE_SPLIT ? 2 : 4, SH128 = ACE_STAGE_SPLIT ? 64 : 2;
+constexpr int SM64 = ACE_STAGE_SPLIT ? 2 : 4, SH64 = ACE_STAGE_SPLIT ? 32 : 2;
 constexpr int XSPLIT_HEAD = 8;  // entries of the split cross's head launch (3 tiles + padding)
 static_assert(BK == 16, "staging maps 512 threads x 4 doubles onto a 128 x 16 chunk");
 
@@ -762,14 +774,14 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
   }
   // staging: each thread moves 4 doubles of each operand per chunk (issued
   // before the C tile, so chunk 0 reaches LDS without waiting for C)
-  const int sk = tid >> 5, sm = (tid & 31) * 4;
+  const int sk = tid >> 5, sm = (tid & 31) * SM128;  // 2nd half at sm + SH128
   // scalar panel bases + 32-bit element offsets (as k_update_multi)
   const int roff = (int)((R0 + sm) + (int64_t)sk * ldp), coff = (int)((C0 + sm) + (int64_t)sk * ldp);
   double2 rw[2], rp[2];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    rw[e] = *reinterpret_cast<const double2 *>(Rop + roff + 2 * e);
-    rp[e] = *reinterpret_cast<const double2 *>(Cop + coff + 2 * e);
+    rw[e] = *reinterpret_cast<const double2 *>(Rop + roff + SH128 * e);
+    rp[e] = *reinterpret_cast<const double2 *>(Cop + coff + SH128 * e);
   }
   __builtin_amdgcn_sched_barrier(0);  // keep the C-tile loads behind them
   const int wr = wv & 1, wc = wv >> 1;  // rows 64*wr.., cols 32*wc..
@@ -785,8 +797,8 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
     }
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2 * e]) = rw[e];
-    *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2 * e]) = rp[e];
+    *reinterpret_cast<double2 *>(&sW[0][sk][sm + SH128 * e]) = rw[e];
+    *reinterpret_cast<double2 *>(&sP[0][sk][sm + SH128 * e]) = rp[e];
   }
   __syncthreads();
   for (int ch = 0; ch < NCH; ++ch) {
@@ -796,8 +808,8 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
       const double *nw = Rop + off, *np = Cop + off;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        rw[e] = *reinterpret_cast<const double2 *>(nw + roff + 2 * e);
-        rp[e] = *reinterpret_cast<const double2 *>(np + coff + 2 * e);
+        rw[e] = *reinterpret_cast<const double2 *>(nw + roff + SH128 * e);
+        rp[e] = *reinterpret_cast<const double2 *>(np + coff + SH128 * e);
       }
     }
 #pragma unroll
@@ -816,8 +828,8 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
     if (ch + 1 < NCH) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2 * e]) = rw[e];
-        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2 * e]) = rp[e];
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + SH128 * e]) = rw[e];
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + SH128 * e]) = rp[e];
       }
     }
     __syncthreads();
@@ -865,14 +877,14 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
   if (G > 1 && !owns_col(R0, G, r) && !(owns_col(k0, G, r) && R0 >= k0)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
-  const int sk = tid >> 5, sm = (tid & 31) * 4;
+  const int sk = tid >> 5, sm = (tid & 31) * SM128;  // 2nd half at sm + SH128
   const double *gW = Pn + (R0 + sm) + (int64_t)sk * ldp;
   const double *gP = W + (k0 + C0 + sm) + (int64_t)sk * ldp;  // W_kk(c, k) = W[k0 + c, k]
   double2 rw[2], rp[2];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    rw[e] = *reinterpret_cast<const double2 *>(gW + 2 * e);
-    rp[e] = *reinterpret_cast<const double2 *>(gP + 2 * e);
+    rw[e] = *reinterpret_cast<const double2 *>(gW + SH128 * e);
+    rp[e] = *reinterpret_cast<const double2 *>(gP + SH128 * e);
   }
   const int wr = wv & 1, wc = wv >> 1;
   d4 acc[2][4];
@@ -882,8 +894,8 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
     for (int ri = 0; ri < 4; ++ri) acc[ci][ri] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2 * e]) = rw[e];
-    *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2 * e]) = rp[e];
+    *reinterpret_cast<double2 *>(&sW[0][sk][sm + SH128 * e]) = rw[e];
+    *reinterpret_cast<double2 *>(&sP[0][sk][sm + SH128 * e]) = rp[e];
   }
   __syncthreads();
   for (int ch = 0; ch < NCH; ++ch) {
@@ -892,8 +904,8 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
       const int64_t off = (int64_t)(ch + 1) * BK * ldp;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        rw[e] = *reinterpret_cast<const double2 *>(gW + off + 2 * e);
-        rp[e] = *reinterpret_cast<const double2 *>(gP + off + 2 * e);
+        rw[e] = *reinterpret_cast<const double2 *>(gW + off + SH128 * e);
+        rp[e] = *reinterpret_cast<const double2 *>(gP + off + SH128 * e);
       }
     }
 #pragma unroll
@@ -912,8 +924,8 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
     if (ch + 1 < NCH) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2 * e]) = rw[e];
-        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2 * e]) = rp[e];
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + SH128 * e]) = rw[e];
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + SH128 * e]) = rp[e];
       }
     }
     __syncthreads();
@@ -1021,7 +1033,7 @@ __device__ __forceinline__ void update_pair_tile(
     }
     return;
   }
-  const int sk = tid >> 5, sm = (tid & 31) * 4;
+  const int sk = tid >> 5, sm = (tid & 31) * 4;  // (the split mapping costs this kernel 12 VGPRs)
   // 32-bit element offsets from the (scalar) panel bases: the loads take a
   // scalar base + vector offset (no 64-bit address VGPRs; -1 ms per C2
   // evaluation, profiles/r03_v4_group_ab.txt)
@@ -1268,7 +1280,10 @@ __device__ __forceinline__ void update_multi_tile(int I, int J, double (&sW)[2][
     }
     return;
   }
-  const int sk = tid >> 5, sm = (tid & 31) * 4;
+  // (the sharded form keeps the 4-consecutive mapping: the split one costs
+  // it 8 VGPRs and a wave per SIMD)
+  constexpr int SMU = SH ? 4 : SM128, SHU = SH ? 2 : SH128;
+  const int sk = tid >> 5, sm = (tid & 31) * SMU;  // 2nd half at sm + SHU
   // 32-bit element offsets from the (scalar) panel bases: the loads take a
   // scalar base + vector offset, so the segment pointers cost no VGPRs
   const int roff = (int)((R0 + sm) + (int64_t)sk * ldp), coff = (int)((C0 + sm) + (int64_t)sk * ldp);
@@ -1276,9 +1291,9 @@ __device__ __forceinline__ void update_multi_tile(int I, int J, double (&sW)[2][
   {
     const double *w = psel(ps.R, seg0) + roff, *pp = psel(ps.C, seg0) + coff;
     rw0 = *reinterpret_cast<const double2 *>(w);
-    rw1 = *reinterpret_cast<const double2 *>(w + 2);
+    rw1 = *reinterpret_cast<const double2 *>(w + SHU);
     rp0 = *reinterpret_cast<const double2 *>(pp);
-    rp1 = *reinterpret_cast<const double2 *>(pp + 2);
+    rp1 = *reinterpret_cast<const double2 *>(pp + SHU);
   }
   __builtin_amdgcn_sched_barrier(0);  // keep the C-tile loads behind them
   const int wr = wv & 1, wc = wv >> 1;
@@ -1298,9 +1313,9 @@ __device__ __forceinline__ void update_multi_tile(int I, int J, double (&sW)[2][
       }
     }
   *reinterpret_cast<double2 *>(&sW[0][sk][sm]) = rw0;
-  *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2]) = rw1;
+  *reinterpret_cast<double2 *>(&sW[0][sk][sm + SHU]) = rw1;
   *reinterpret_cast<double2 *>(&sP[0][sk][sm]) = rp0;
-  *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2]) = rp1;
+  *reinterpret_cast<double2 *>(&sP[0][sk][sm + SHU]) = rp1;
   __syncthreads();
   // chunk ch of every segment uses LDS buffer ch & 1 (NCH is even, so the
   // parity runs on across segments)
@@ -1316,9 +1331,9 @@ __device__ __forceinline__ void update_multi_tile(int I, int J, double (&sW)[2][
         const double *nw = (ch + 1 < NCH ? sw + (int64_t)(ch + 1) * BK * ldp : nxw) + roff;
         const double *np = (ch + 1 < NCH ? sp + (int64_t)(ch + 1) * BK * ldp : nxp) + coff;
         rw0 = *reinterpret_cast<const double2 *>(nw);
-        rw1 = *reinterpret_cast<const double2 *>(nw + 2);
+        rw1 = *reinterpret_cast<const double2 *>(nw + SHU);
         rp0 = *reinterpret_cast<const double2 *>(np);
-        rp1 = *reinterpret_cast<const double2 *>(np + 2);
+        rp1 = *reinterpret_cast<const double2 *>(np + SHU);
       }
 #pragma unroll
       for (int kk = 0; kk < BK / 4; ++kk) {
@@ -1335,9 +1350,9 @@ __device__ __forceinline__ void update_multi_tile(int I, int J, double (&sW)[2][
       }
       if (more) {
         *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm]) = rw0;
-        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2]) = rw1;
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + SHU]) = rw1;
         *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm]) = rp0;
-        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2]) = rp1;
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + SHU]) = rp1;
       }
       __syncthreads();
     }
@@ -1477,19 +1492,19 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
       for (int j = 0; j < 4; ++j) acc[ci][ri][j] = A[r + (c + 4 * j) * ld];
     }
   // staging: 256 threads x (4 doubles of each operand) per 64 x 16 chunk
-  const int sk = tid >> 4, sm = (tid & 15) * 4;
+  const int sk = tid >> 4, sm = (tid & 15) * SM64;  // 2nd half at sm + SH64
   const double *gW = Rop + (R0 + sm) + (int64_t)sk * ldp;
   const double *gP = Cop + (C0 + sm) + (int64_t)sk * ldp;
   double2 rw[2], rp[2];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    rw[e] = *reinterpret_cast<const double2 *>(gW + 2 * e);
-    rp[e] = *reinterpret_cast<const double2 *>(gP + 2 * e);
+    rw[e] = *reinterpret_cast<const double2 *>(gW + SH64 * e);
+    rp[e] = *reinterpret_cast<const double2 *>(gP + SH64 * e);
   }
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2 * e]) = rw[e];
-    *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2 * e]) = rp[e];
+    *reinterpret_cast<double2 *>(&sW[0][sk][sm + SH64 * e]) = rw[e];
+    *reinterpret_cast<double2 *>(&sP[0][sk][sm + SH64 * e]) = rp[e];
   }
   __syncthreads();
   for (int ch = 0; ch < NCH; ++ch) {
@@ -1498,8 +1513,8 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
       const int64_t off = (int64_t)(ch + 1) * BK * ldp;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        rw[e] = *reinterpret_cast<const double2 *>(gW + off + 2 * e);
-        rp[e] = *reinterpret_cast<const double2 *>(gP + off + 2 * e);
+        rw[e] = *reinterpret_cast<const double2 *>(gW + off + SH64 * e);
+        rp[e] = *reinterpret_cast<const double2 *>(gP + off + SH64 * e);
       }
     }
 #pragma unroll
@@ -1518,8 +1533,8 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
     if (ch + 1 < NCH) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2 * e]) = rw[e];
-        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2 * e]) = rp[e];
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + SH64 * e]) = rw[e];
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + SH64 * e]) = rp[e];
       }
     }
     __syncthreads();
@@ -1565,21 +1580,21 @@ __global__ __launch_bounds__(256) void k_update_q(double *__restrict__ A, int64_
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[ci][ri][j] = A[r + (c + 4 * j) * ld];
     }
-  const int sk = tid >> 4, sm = (tid & 15) * 4;
+  const int sk = tid >> 4, sm = (tid & 15) * SM64;  // 2nd half at sm + SH64
   // staging registers as named values (an array here was kept in scratch)
   double2 w0, w1, p0, p1;
   for (int pj = 0; pj < npan; ++pj) {
     const double *gW = psel(ps.R, pj) + (R0 + sm) + (int64_t)sk * ldp;
     const double *gP = psel(ps.C, pj) + (C0 + sm) + (int64_t)sk * ldp;
     w0 = *reinterpret_cast<const double2 *>(gW);
-    w1 = *reinterpret_cast<const double2 *>(gW + 2);
+    w1 = *reinterpret_cast<const double2 *>(gW + SH64);
     p0 = *reinterpret_cast<const double2 *>(gP);
-    p1 = *reinterpret_cast<const double2 *>(gP + 2);
+    p1 = *reinterpret_cast<const double2 *>(gP + SH64);
     __syncthreads();  // the previous panel's last chunk is consumed
     *reinterpret_cast<double2 *>(&sW[0][sk][sm]) = w0;
-    *reinterpret_cast<double2 *>(&sW[0][sk][sm + 2]) = w1;
+    *reinterpret_cast<double2 *>(&sW[0][sk][sm + SH64]) = w1;
     *reinterpret_cast<double2 *>(&sP[0][sk][sm]) = p0;
-    *reinterpret_cast<double2 *>(&sP[0][sk][sm + 2]) = p1;
+    *reinterpret_cast<double2 *>(&sP[0][sk][sm + SH64]) = p1;
     __syncthreads();
 #pragma unroll 2
     for (int ch = 0; ch < NCH; ++ch) {
@@ -1587,9 +1602,9 @@ __global__ __launch_bounds__(256) void k_update_q(double *__restrict__ A, int64_
       if (ch + 1 < NCH) {
         const int64_t off = (int64_t)(ch + 1) * BK * ldp;
         w0 = *reinterpret_cast<const double2 *>(gW + off);
-        w1 = *reinterpret_cast<const double2 *>(gW + off + 2);
+        w1 = *reinterpret_cast<const double2 *>(gW + off + SH64);
         p0 = *reinterpret_cast<const double2 *>(gP + off);
-        p1 = *reinterpret_cast<const double2 *>(gP + off + 2);
+        p1 = *reinterpret_cast<const double2 *>(gP + off + SH64);
       }
 #pragma unroll
       for (int kk = 0; kk < BK / 4; ++kk) {
@@ -1606,9 +1621,9 @@ __global__ __launch_bounds__(256) void k_update_q(double *__restrict__ A, int64_
       }
       if (ch + 1 < NCH) {
         *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm]) = w0;
-        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + 2]) = w1;
+        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + SH64]) = w1;
         *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm]) = p0;
-        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + 2]) = p1;
+        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + SH64]) = p1;
       }
       __syncthreads();
     }
@@ -2624,26 +2639,51 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
     }
     hipError_t r;
     const int hend = (kb + zb) * KT;  // head rows end (row tiles)
-    for (int j = 0; j < zb; ++j) {
+    // the head path (side) needs nothing of the tail path (side2): group 0's
+    // tail may wait for the whole head path (sy->tail_split) -- on the CUs
+    // the assembly leaves free the two would otherwise share them step by step
+    const bool split = G == 0 && sy->tail_split;
+    auto head = [&](int j) -> hipError_t {
       const int k = kb + j;
       chain(k, side);
-      if ((r = hipEventRecord(Esp(k), side)) != hipSuccess) return r;
+      hipError_t q;
+      if ((q = hipEventRecord(Esp(k), side)) != hipSuccess) return q;
       pgemm(k, (k + 1) * KT, hend, true, side);
-      if ((r = hipEventRecord(Egh(k), side)) != hipSuccess) return r;
-      if ((r = hipStreamWaitEvent(side2, Esp(k), 0)) != hipSuccess) return r;
-      pgemm(k, (k + 1) * KT, hend, false, side2);
+      if ((q = hipEventRecord(Egh(k), side)) != hipSuccess) return q;
       if (j + 1 < zb) {
         list(G, 2 + j, tl, nt);
         qupd(1, k, tl, nt, gout(k + 1), side);  // panel k on Q_{j+1}
-        if ((r = hipStreamWaitEvent(side2, Egh(k), 0)) != hipSuccess) return r;
+      }
+      return hipSuccess;
+    };
+    auto tail = [&](int j) -> hipError_t {
+      const int k = kb + j;
+      hipError_t q;
+      if ((q = hipStreamWaitEvent(side2, Esp(k), 0)) != hipSuccess) return q;
+      pgemm(k, (k + 1) * KT, hend, false, side2);
+      if (j + 1 < zb) {
+        if ((q = hipStreamWaitEvent(side2, Egh(k), 0)) != hipSuccess) return q;
         list(G, zb + j + 1, tl, nt);
         upd(j + 1, kb, -1, -1, tl, nt, gout(k + 1), side2);  // T_{j+1}
       }
+      return hipSuccess;
+    };
+    for (int j = 0; j < zb; ++j) {
+      if ((r = head(j)) != hipSuccess) return r;
+      if (!split && (r = tail(j)) != hipSuccess) return r;
     }
     if ((r = hipEventRecord(sy->ev[2 * G], side)) != hipSuccess) return r;
+    if (split) {
+      if ((r = hipStreamWaitEvent(side2, sy->ev[2 * G], 0)) != hipSuccess) return r;
+      for (int j = 0; j < zb; ++j)
+        if ((r = tail(j)) != hipSuccess) return r;
+    }
+    if (G == 0 && sy->fill && (r = sy->fill(sy->fill_arg, side2)) != hipSuccess) return r;
     return hipEventRecord(E2(G), side2);
   };
-  if ((e = hipStreamWaitEvent(side2, sy->ev[2 * steps], 0)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(side2, sy->tail_after ? sy->tail_after : sy->ev[2 * steps], 0)) !=
+      hipSuccess)
+    return e;
   if ((e = produce(0)) != hipSuccess) return e;
   int used = 0;
   for (int g = 0; g < ng; ++g) {

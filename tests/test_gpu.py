@@ -631,3 +631,33 @@ def test_merged_cross_model_is_bitwise_neutral(tmp_path, n):
     # the default (heads4) on two streams and on one
     assert np.array_equal(outs["heads4"], outs["streams2"])
     assert np.array_equal(outs["heads4"], outs["streams1"])
+
+
+_MODEL_SNIPPET_K = _MODEL_SNIPPET.replace('"Matern32"', '{kernel!r}')
+
+
+@pytest.mark.parametrize("kernel,n", [("Matern32", 2000), ("SE", 2600)])
+def test_persistent_assembly_is_bitwise_neutral(tmp_path, kernel, n):
+    """The assembly's second part as a persistent tile queue that leaves one
+    CU per shader engine to the first group's lookahead (default:
+    ACE_ASM_PERSIST=1, the tail path beside the head path and a filler launch
+    joining the queue afterwards) assembles every tile exactly as the plain
+    grid does: gradient, stats and mu bit for bit against ACE_ASM_PERSIST=0,
+    over two evaluations (the queue reset per evaluation), and under the
+    other switches and the one-stream budget."""
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    variants = {"plain": {"ACE_ASM_PERSIST": "0"}, "default": {},
+                "tail_after": {"ACE_ASM_TAIL": "0", "ACE_ASM_FILL": "0"},
+                "tail_split": {"ACE_ASM_TAIL": "2"},
+                "two_per_engine": {"ACE_ASM_PERSIST": "2"},
+                "one_stream": {"ACE_STREAMS": "1"}}
+    outs = {}
+    for name, ev in variants.items():
+        out = str(tmp_path / f"p_{name}.npy")
+        run_child(_MODEL_SNIPPET_K.format(root=root, n=n, out=out, kernel=kernel),
+                  env=dict(os.environ, **ev), timeout=100)
+        outs[name] = np.load(out)
+    assert np.all(np.isfinite(outs["plain"]))
+    for name in variants:
+        assert np.array_equal(outs["plain"], outs[name]), name

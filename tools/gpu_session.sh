@@ -24,6 +24,31 @@ for step in "$@"; do
     tcc) bash tools/run_pmc_tcc.sh $tag/tcc; rc=$? ;;
     abgrad) bash tools/ab_grad.sh $tag tools/libace_tail.so tools/libace_tailexp.so; rc=$? ;;
     abnew) bash tools/ab_grad.sh $tag tools/libace_tail.so tools/libace_new.so; rc=$? ;;
+    abstage) timeout -k 10 200 python tools/cmp_libs.py tools/libace_new.so tools/libace_stage.so 16384 Matern32 && \
+             timeout -k 10 200 python tools/cmp_libs.py tools/libace_new.so tools/libace_stage.so 4096 SE && \
+             { timeout -k 10 200 python tools/cmp_libs.py tools/libace_stage.so tools/libace_cur.so 16384 Matern32; \
+               timeout -k 10 200 python tools/cmp_libs.py tools/libace_stage.so tools/libace_cur.so 4096 SE; true; } && \
+             ROUNDS=3 bash tools/ab_libs.sh tools/libace_new.so tools/libace_stage.so tools/libace_cur.so -- --no-r6; rc=$? ;;
+    abpersist) timeout -k 10 60 ./tools/probe_hwid > gpurun_out/$tag/probe_hwid.txt 2>&1; cat gpurun_out/$tag/probe_hwid.txt | tail -3
+             timeout -k 10 200 python tools/cmp_libs.py tools/libace_new.so tools/libace_cur.so 16384 Matern32 && \
+             CMP_ENV_B="ACE_ASM_PERSIST=1" timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_cur.so 16384 Matern32 && \
+             CMP_ENV_B="ACE_ASM_PERSIST=2" timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_cur.so 4096 SE && \
+             ROUNDS=3 bash tools/ab_envs.sh "" "ACE_ASM_PERSIST=1" "ACE_ASM_PERSIST=2"; rc=$? ;;
+    trace) NSHOW=1 bash tools/trace_group.sh $tag/tg "" "ACE_ASM_PERSIST=1" > gpurun_out/$tag/timeline.txt 2>&1; rc=$?; head -c 6000 gpurun_out/$tag/timeline.txt ;;
+    persist2) CMP_ENV_B="ACE_ASM_PERSIST=1" timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_cur.so 16384 Matern32 && \
+              CMP_ENV_B="ACE_ASM_PERSIST=2" timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_cur.so 4096 SE && \
+              NSHOW=1 bash tools/trace_group.sh $tag/tg "" "ACE_ASM_PERSIST=1" "ACE_ASM_PERSIST=2" > gpurun_out/$tag/timeline.txt 2>&1 && \
+              ROUNDS=3 bash tools/ab_envs.sh "" "ACE_ASM_PERSIST=1" "ACE_ASM_PERSIST=2"; rc=$?; head -c 5000 gpurun_out/$tag/timeline.txt ;;
+    persist3) CMP_ENV_B="ACE_ASM_PERSIST=1 ACE_ASM_TAIL=1 ACE_ASM_FILL=1" timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_cur.so 16384 Matern32 && \
+              CMP_ENV_B="ACE_ASM_PERSIST=2 ACE_ASM_FILL=1" timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_cur.so 4096 SE && \
+              NSHOW=1 bash tools/trace_group.sh $tag/tg "ACE_ASM_PERSIST=1 ACE_ASM_TAIL=1" "ACE_ASM_PERSIST=1 ACE_ASM_FILL=1" "ACE_ASM_PERSIST=1 ACE_ASM_TAIL=1 ACE_ASM_FILL=1" > gpurun_out/$tag/timeline.txt 2>&1 && \
+              ROUNDS=3 bash tools/ab_envs.sh "" "ACE_ASM_PERSIST=1" "ACE_ASM_PERSIST=1 ACE_ASM_TAIL=1" "ACE_ASM_PERSIST=1 ACE_ASM_FILL=1" "ACE_ASM_PERSIST=1 ACE_ASM_TAIL=1 ACE_ASM_FILL=1" "ACE_ASM_PERSIST=2 ACE_ASM_FILL=1"; rc=$? ;;
+    persist4) CMP_ENV_B="ACE_ASM_PERSIST=1 ACE_ASM_TAIL=2 ACE_ASM_FILL=1" timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_cur.so 16384 Matern32 && \
+              NSHOW=1 bash tools/trace_group.sh $tag/tg "ACE_ASM_PERSIST=1 ACE_ASM_TAIL=2" "ACE_ASM_PERSIST=1 ACE_ASM_TAIL=2 ACE_ASM_FILL=1" > gpurun_out/$tag/timeline.txt 2>&1 && \
+              ROUNDS=3 bash tools/ab_envs.sh "" "ACE_ASM_PERSIST=1" "ACE_ASM_PERSIST=1 ACE_ASM_TAIL=1 ACE_ASM_FILL=1" "ACE_ASM_PERSIST=1 ACE_ASM_TAIL=2" "ACE_ASM_PERSIST=1 ACE_ASM_TAIL=2 ACE_ASM_FILL=1"; rc=$? ;;
+    abexp) timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_exp256.so 16384 Matern32; \
+           timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_exp256.so 4096 SE; \
+           ROUNDS=3 bash tools/ab_libs.sh tools/libace_cur.so tools/libace_exp256.so -- --no-r6; rc=$? ;;
     sq) bash tools/run_sq.sh $tag/sq > /dev/null; rc=$?; cat gpurun_out/$tag/sq/sq.txt | head -80 ;;
     prof) bash tools/run_prof.sh $tag/prof --steps 5 --warmup 1 > /dev/null; rc=$? ;;
     *) echo "unknown step $step"; rc=2 ;;
