@@ -131,17 +131,20 @@ def rocprof_bulk_avg():
 def pair_hbm_gbs(asm_ms, grad_ms):
     """HBM GB/s of the fused assembly and gradient phases (SURVEY §8d asks for
     them beside their VALU/MFMA rates): PMC bytes per eval from the newest
-    profiles/rNN_pmc_traffic.json (one assembly launch and the gradient
-    launches of each eval) over this run's phase times."""
+    profiles/rNN_pmc_traffic.json (the assembly and gradient launches of
+    each eval) over this run's phase times."""
     import glob
     files = _newest_first_last(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
     if not files:
         return None
     try:
         ks = json.load(open(files[-1]))["kernels"]
-        a, g = ks["k_asm_mm"], ks["k_grad_mm"]
+        g = ks["k_grad_mm"]
         evals = g["launches"] / 2  # diagonal + strictly-lower gradient launch per eval
-        asm_b = a["traffic"] * a["launches"] / evals  # the assembly is 2 launches per eval
+        # the assembly: its plain-grid parts (k_asm_mm) and, since round 4, the
+        # persistent queue launches (k_asm_mm_q: main + filler)
+        asm_b = sum(ks[k]["traffic"] * ks[k]["launches"] for k in ("k_asm_mm", "k_asm_mm_q")
+                    if k in ks) / evals
         grad_b = g["traffic"] * g["launches"] / evals
     except (KeyError, ValueError, OSError, ZeroDivisionError):
         return None

@@ -28,6 +28,7 @@ KERNELS = {
     "k_panel_gemm": "ace::k_panel_gemm(",
     "k_grad2": "ace::k_grad2<",
     "k_asm_mm": "ace::k_asm_mm<",
+    "k_asm_mm_q": "ace::k_asm_mm_q<",
     "k_grad_mm": "ace::k_grad_mm<",
 }
 
