@@ -49,6 +49,7 @@ for step in "$@"; do
     abexp) timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_exp256.so 16384 Matern32; \
            timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_exp256.so 4096 SE; \
            ROUNDS=3 bash tools/ab_libs.sh tools/libace_cur.so tools/libace_exp256.so -- --no-r6; rc=$? ;;
+    pmc) bash tools/run_pmc.sh $tag/pmc > /dev/null; rc=$?; head -c 3000 gpurun_out/$tag/pmc/pmc_traffic.json ;;
     sq) bash tools/run_sq.sh $tag/sq > /dev/null; rc=$?; cat gpurun_out/$tag/sq/sq.txt | head -80 ;;
     prof) bash tools/run_prof.sh $tag/prof --steps 5 --warmup 1 > /dev/null; rc=$? ;;
     *) echo "unknown step $step"; rc=2 ;;
