@@ -716,7 +716,15 @@ void model_collect_timing(ace_model *m, int ts) {
     m->t_ms[3] += ms;
     m->t_launch[3] += 1;
     m->t_work[3] += sweep_flops(m->sw.naug, m->sw.npad);
+    // the lead-in: the assembly's (main) launch end to the first bulk start
+    ck(m->ctx, hipEventElapsedTime(&ms, m->ev_asm[2 * ts + 1], ev[0]), "elapsed");
+    m->t_ms[4] += ms;
+    m->t_launch[4] += 1;
   }
+  // the evaluation's device span: assembly start to gradient end
+  ck(m->ctx, hipEventElapsedTime(&ms, m->ev_asm[2 * ts], m->ev_grad[2 * ts + 1]), "elapsed");
+  m->t_ms[5] += ms;
+  m->t_launch[5] += 1;
   const double n = (double)m->n, pairs = n * (n + 1) / 2, B = m->s.B, p = m->s.p;
   // work: the update launches' GEMM flops (counted per launch
   // from its tiles), pair kernels by their algorithmic flop formulas
@@ -1062,7 +1070,7 @@ int ace_model_profile(ace_model *m, int enable) {
   if (!m) return ACE_ERR_ARG;
   m->prof = enable != 0;
   m->pend = -1;  // counters restart: drop an unread set
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < 6; ++j) {
     m->t_ms[j] = 0;
     m->t_launch[j] = 0;
     m->t_work[j] = 0;
@@ -1071,7 +1079,7 @@ int ace_model_profile(ace_model *m, int enable) {
 }
 
 int ace_model_kernel_time(ace_model *m, int which, double *ms, int64_t *launches, double *work) {
-  if (!m || which < 0 || which > 3) return ACE_ERR_ARG;
+  if (!m || which < 0 || which > 5) return ACE_ERR_ARG;
   if (m->pend >= 0) {  // the last timed evaluation's set (its work is complete)
     try {
       model_collect_timing(m, m->pend);

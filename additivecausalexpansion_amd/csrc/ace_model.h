@@ -190,9 +190,9 @@ struct ace_model {
   // [0] bulk update launches, [1] assembly, [2] gradient, [3] the sweep's
   // span (first bulk launch start -> last bulk launch end, every update /
   // cross / panel-GEMM flop of the sweep as its work)
-  double t_ms[4] = {0, 0, 0, 0};
-  int64_t t_launch[4] = {0, 0, 0, 0};
-  double t_work[4] = {0, 0, 0, 0};
+  double t_ms[6] = {0, 0, 0, 0, 0, 0};
+  int64_t t_launch[6] = {0, 0, 0, 0, 0, 0};
+  double t_work[6] = {0, 0, 0, 0, 0, 0};
   ShardModel *shard = nullptr;  // block-column-sharded model (ace_shard.cpp)
 };
 

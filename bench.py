@@ -406,6 +406,8 @@ def main():
     asm_ms, _, asm_work = model.kernel_time(1)
     grad_ms, _, grad_work = model.kernel_time(2)
     sweep_ms, sweep_n, sweep_work = model.kernel_time(3)
+    lead_ms, lead_n, _ = model.kernel_time(4)
+    span_ms, span_n, _ = model.kernel_time(5)
     model.profile(False)
     pred = predict_leg(step.kernel_object, model, p, B) if rank == 0 else None
     r6 = None
@@ -482,6 +484,12 @@ def main():
             "phase_ms_per_step": {"update_kernel": upd_ms / a.steps,
                                   "assembly_kernel": asm_ms / a.steps,
                                   "gradient_kernel": grad_ms / a.steps},
+            # device timeline per evaluation (HIP events on the model's stream):
+            # assembly main-launch end -> first bulk launch start, and the
+            # span from the assembly's start to the gradient's end
+            "timeline_ms_per_eval": {
+                "assembly_end_to_first_bulk": lead_ms / lead_n if lead_n else None,
+                "device_span": span_ms / span_n if span_n else None},
             "pair_kernels_tflops": {
                 "assembly": asm_work / (asm_ms * 1e-3) / 1e12 if asm_ms else None,
                 "gradient": grad_work / (grad_ms * 1e-3) / 1e12 if grad_ms else None},

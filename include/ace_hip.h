@@ -293,7 +293,9 @@ int ace_model_predict_marginal(ace_model *m, const double *theta, int64_t nx, co
  * flops issued by those launches.  `which` = 3: the
  * sweep's span per evaluation (first bulk update launch start to the last
  * one's end) with every update / cross / panel-GEMM flop of the sweep as
- * its work (unsharded models).  Enabling resets the
+ * its work (unsharded models); 4: from the end of the assembly's main
+ * launch to the first bulk update launch's start (unsharded); 5: the
+ * evaluation's device span, assembly start to gradient end.  Enabling resets the
  * counters.  An evaluation's events are read back while the next one runs
  * (no host queries between evaluations); ace_model_kernel_time reads the
  * last timed evaluation's set first, so its totals cover every timed
