@@ -806,13 +806,13 @@ __global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 24 ? 4 : PM <=
 // ---------------------------------------------------------------------------
 // Fused gradient traces (same outputs as k_grad2): per slice b (descending),
 //   GEMM1  G = X_J (w_b X_I)^T          -> r2, K_b, U = T K_b [/ (1 + sqrt(3 r~2_b))]
-//   GEMM2  V = U [X_J | X_J^2]          -> for every feature i
-//          sum_rc U d_i^2 = sum_r (x_ri^2 R_r - 2 x_ri V_ri + V2_ri)
-//          with R_r the row sums of U (in registers + 2 shuffles).
+//   GEMM2  V = U X_J                    -> for every feature i
+//          sum_rc U d_i^2 = sum_r x_ri^2 R_r + sum_c x_ci^2 C_c - 2 sum_r x_ri V_ri
+//          with R_r / C_c the row / column sums of U (lane exchanges, below).
 // U never leaves the registers: the GEMM1 result fragment (row r = 16w+lr,
 // column c = 16cb+lk+4v) is exactly GEMM2's A fragment for k-step 4cb+v.
-// The four waves' per-slice partials meet in LDS; with one buffer per slice
-// the slice loop has no workgroup barrier at all.
+// The waves' per-slice partials meet in LDS; with one buffer per slice the
+// slice loop has no workgroup barrier at all.
 // Matern32: r~2_b uses the gradient-indexed weights, which equal slice b+1's
 // kernel weights (Q1), so the factor 1 + sqrt3 t of slice b+1 is cached per
 // pair; the last slice gets its own GEMM with wg[B-1].
