@@ -18,6 +18,9 @@
 // (cb, v in 0..3) -- exactly the fragment layout of the MFMA result
 // D = X_J (w_b X_I)^T, so no data moves between the GEMM and the
 // elementwise kernel math.
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <type_traits>
 
 #include "ace_internal.h"
@@ -1451,12 +1454,21 @@ static hipError_t asm_mm_persist_pm(int kind, PairSide S, int64_t npad, int B, i
   return hipGetLastError();
 }
 
-// Workgroup slots of k_asm_mm_q (occupancy x CUs), 0 if unknown
+// Workgroup slots of k_asm_mm_q (occupancy x CUs), 0 if unknown; cached per
+// (device, kind, B): the queries cost host time every evaluation otherwise
 template <int PM>
 static int asm_mm_slots(int kind, int B) {
   int dev = 0, ncu = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int>, int> cache;
+  const auto key = std::make_tuple(dev, kind, B);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    const auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
   const size_t lds = (size_t)mm_layout(PM, B, kind == 0 ? 0 : 1, false).total * sizeof(double);
   const void *f = kind == 0 ? (const void *)k_asm_mm_q<PM, 0> : (const void *)k_asm_mm_q<PM, 1>;
@@ -1470,11 +1482,13 @@ static int asm_mm_slots(int kind, int B) {
     const int waves = std::min(8, 512 / alloc);  // per SIMD
     per = std::min(per, waves * 4 / (ASM_NT / 64));
   }
+  std::lock_guard<std::mutex> g(mu);
+  cache[key] = per * ncu;
   return per * ncu;
 }
 
 int assembly_persist_per_cu(int kind, int PM, int B) {
-  int dev = 0, ncu = 0;
+  int dev = 0, ncu = 0;  // (an attribute read: cheap, unlike the occupancy query)
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
     return 0;
