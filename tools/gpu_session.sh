@@ -48,6 +48,9 @@ for step in "$@"; do
               ROUNDS=3 bash tools/ab_envs.sh "" "ACE_ASM_PERSIST=1" "ACE_ASM_PERSIST=1 ACE_ASM_TAIL=1 ACE_ASM_FILL=1" "ACE_ASM_PERSIST=1 ACE_ASM_TAIL=2" "ACE_ASM_PERSIST=1 ACE_ASM_TAIL=2 ACE_ASM_FILL=1"; rc=$? ;;
     lead) ROUNDS=2 bash tools/ab_envs.sh "" "ACE_ASM_PERSIST=0" "ACE_ASM_TAIL=0 ACE_ASM_FILL=0" "ACE_ASM_TAIL=2"; rc=$? ;;
     evt) for i in 1 2 3; do for f in "" "--no-profile"; do timeout -k 5 100 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-r6 $f | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('[$f]', round(d['ms_per_step'],3))" || exit 1; done; done; rc=$? ;;
+    cfgs) timeout -k 10 200 python bench.py --config C1 --steps 10 --warmup 2 --no-cpu-baseline --no-r6 > gpurun_out/$tag/bench_c1.json && \
+          timeout -k 10 300 python bench.py --config C3 --steps 3 --warmup 1 --no-cpu-baseline --no-r6 > gpurun_out/$tag/bench_c3.json; rc=$?
+          cut -c1-300 gpurun_out/$tag/bench_c1.json gpurun_out/$tag/bench_c3.json ;;
     abexp) timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_exp256.so 16384 Matern32; \
            timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_exp256.so 4096 SE; \
            ROUNDS=3 bash tools/ab_libs.sh tools/libace_cur.so tools/libace_exp256.so -- --no-r6; rc=$? ;;
