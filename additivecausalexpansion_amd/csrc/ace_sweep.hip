@@ -46,6 +46,50 @@ typedef double d4 __attribute__((ext_vector_type(4)));
     if (ACE_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(ACE_CHAIN_PRIO); \
   } while (0)
 
+// ACE_DIAG_WGTIME (diagnostic builds only, tools/wg_timeline.py): per
+// workgroup of the sweep kernels, the wall clock (100 MHz) at entry and per
+// wave at exit, the CU (HW_REG_HW_ID / XCC_ID) and the launch's grid, into a
+// device record array read back by ace_diag_wgtime.  The bulk launches are
+// sampled (every 32nd workgroup).  Workgroups start with one extra barrier.
+#ifdef ACE_DIAG_WGTIME
+constexpr int WGT_REC = 16, WGT_CAP = 1 << 18;
+__device__ unsigned long long d_wgt_rec[(size_t)WGT_CAP * WGT_REC];
+__device__ unsigned d_wgt_cnt;
+struct WgTime {
+  unsigned slot = ~0u;
+  __device__ WgTime(int kid, unsigned *sh, bool on) {
+    if (!on) return;
+    const unsigned long long t0 = wall_clock64();
+    if (threadIdx.x == 0) {
+      const unsigned sl = atomicAdd(&d_wgt_cnt, 1u);
+      *sh = sl;
+      if (sl < WGT_CAP) {
+        unsigned long long *r = d_wgt_rec + (size_t)sl * WGT_REC;
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 15;
+        r[0] = (unsigned long long)kid | ((unsigned long long)blockIdx.x << 8) |
+               ((unsigned long long)gridDim.x << 36);
+        r[1] = (unsigned long long)hw | ((unsigned long long)xcc << 32) |
+               ((unsigned long long)(blockDim.x >> 6) << 40);
+        r[2] = t0;
+        r[3] = (unsigned long long)blockIdx.y | ((unsigned long long)gridDim.y << 32);
+      }
+    }
+    __syncthreads();
+    slot = *sh;
+  }
+  __device__ ~WgTime() {
+    if (slot < WGT_CAP && (threadIdx.x & 63) == 0)
+      d_wgt_rec[(size_t)slot * WGT_REC + 4 + (threadIdx.x >> 6)] = wall_clock64();
+  }
+};
+#define ACE_WGT(kid, on)                 \
+  __shared__ unsigned wgt_slot_sh_;      \
+  WgTime wgt_(kid, &wgt_slot_sh_, (on))
+#else
+#define ACE_WGT(kid, on)
+#endif
+
 // ---------------------------------------------------------------- pivot
 // Sweeps the 64x64 sub-block s of the panel's pivot rows:
 //   d = D_tt; D_ij -= D_it D_tj / d; D_it /= d; D_tj /= d; D_tt = -1/d
@@ -146,6 +190,7 @@ __global__ __launch_bounds__(64 * NW) void k_pivot(const double *__restrict__ S,
                                                    double *__restrict__ SW,
                                                    double *__restrict__ piv, int64_t p0,
                                                    int *__restrict__ flag) {
+  ACE_WGT(1, true);
   CHAIN_PRIO();
   constexpr int CW = SUB / NW;
   __shared__ PivotLds<NW> L;
@@ -376,6 +421,7 @@ __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int
                                                      double *__restrict__ SWn,
                                                      double *__restrict__ piv,
                                                      int *__restrict__ flag) {
+  ACE_WGT(2, true);
   CHAIN_PRIO();
   __shared__ double sSW[SUB][PLD];  // sSW[b][a] = SW(a, b)
   __shared__ double sSt[SUB][SLD];  // sSt[c][t] = S(t, 64 cc + c)
@@ -684,6 +730,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
                                                         int64_t ldp, int64_t k0, int kx,
                                                         const Tile *__restrict__ tiles, int G,
                                                         GatherOut go) {
+  ACE_WGT(6, gridDim.x < 4096 || blockIdx.x % 32 == 0);
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
   constexpr int KT = NB / UT;
@@ -866,6 +913,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
                                                               int64_t ldp, int64_t k0, int G,
                                                               int r, int rt0 = 0,
                                                               int rs0 = 1 << 30, int rs1 = 1 << 30) {
+  ACE_WGT(3, true);
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];  // Pn rows of the tile
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];  // W_kk rows c
   // row tile rt0 + blockIdx.x, skipping row tiles [rs0, rs1) (the head/tail
@@ -1385,6 +1433,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_multi(double *__restrict
                                                               int64_t ka0, int kx0, int kx1,
                                                               const Tile *__restrict__ tiles,
                                                               GatherOut go, int G) {
+  ACE_WGT(5, gridDim.x < 4096 || blockIdx.x % 32 == 0);
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
   constexpr int KT = NB / UT;
@@ -1560,6 +1609,7 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
 __global__ __launch_bounds__(256) void k_update_q(double *__restrict__ A, int64_t ld, PanelSet ps,
                                                   int npan, int64_t ldp,
                                                   const Tile *__restrict__ tiles, GatherOut go) {
+  ACE_WGT(4, true);
   __shared__ __attribute__((aligned(16))) double sW[2][BK][XL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][XL];
   const Tile tt = tiles[blockIdx.x >> 2];
@@ -2890,3 +2940,24 @@ hipError_t shard_update_main(const ShardSweep &b, int k, int buf, int kx, hipStr
 }
 
 }  // namespace ace
+
+#ifdef ACE_DIAG_WGTIME
+// Diagnostic builds: copies up to cap records (16 x u64 each, see WgTime) to
+// dst and returns how many the device wrote since the last reset (reset != 0
+// zeroes the counter after the copy).  Device-synchronous.
+extern "C" long long ace_diag_wgtime(void *dst, long long cap, int reset) {
+  unsigned cnt = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(ace::d_wgt_cnt), sizeof(cnt)) != hipSuccess) return -1;
+  const long long n = std::min<long long>(std::min<long long>(cnt, ace::WGT_CAP), cap);
+  if (dst && n > 0 &&
+      hipMemcpyFromSymbol(dst, HIP_SYMBOL(ace::d_wgt_rec), (size_t)n * ace::WGT_REC * 8) != hipSuccess)
+    return -1;
+  if (reset) {
+    const unsigned z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(ace::d_wgt_cnt), &z, sizeof(z)) != hipSuccess) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+  }
+  return (long long)cnt;
+}
+#endif

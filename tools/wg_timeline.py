@@ -1,0 +1,142 @@
+"""Per-workgroup timeline of the sweep's kernels in one C2 evaluation, from a
+-DACE_DIAG_WGTIME build (tools/build_variant.sh wgt -DACE_DIAG_WGTIME):
+  ACE_LIB_PATH=tools/libace_wgt.so python tools/wg_timeline.py [n]
+
+For every launch of the chain kernels (k_pivot, k_panel_split) and the head
+launches (k_panel_gemm_t, k_update_q): the launch span (first workgroup
+entry to last wave exit), each workgroup's own duration (entry to its last
+wave's exit) and the spread of the workgroups' entry times.  A span much
+longer than the workgroups' own durations means the workgroups waited for a
+CU slot (dispatch); a workgroup duration much longer than the kernel's
+uncontended time means it ran slowly beside the bulk tiles (issue sharing).
+The bulk update launches are sampled (every 32nd workgroup)."""
+import ctypes
+import os
+import sys
+from collections import defaultdict
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import additivecausalexpansion_amd as ace  # noqa: E402
+from additivecausalexpansion_amd._lib import lib  # noqa: E402
+from additivecausalexpansion_amd.synthetic import make_problem  # noqa: E402
+
+KIND = {1: "pivot", 2: "panel_split", 3: "panel_gemm_t", 4: "update_q", 5: "update_multi",
+        6: "update"}
+REC = 16
+TICK_US = 0.01  # wall_clock64: 100 MHz
+
+
+def read(L, reset):
+    f = L.ace_diag_wgtime
+    f.restype = ctypes.c_longlong
+    f.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int]
+    cnt = f(None, 0, 0)
+    buf = np.zeros((max(cnt, 1), REC), dtype=np.uint64)
+    got = f(buf.ctypes.data, cnt, 1 if reset else 0)
+    assert got >= 0, "ace_diag_wgtime failed"
+    return buf[:min(cnt, buf.shape[0])]
+
+
+def launches(recs):
+    """Records -> list of launches (kid, grid, [records]) in start order: per
+    (kid, grid), a new launch starts when a block index repeats."""
+    by = defaultdict(list)
+    for r in recs:
+        kid, bx, gx = int(r[0]) & 0xFF, (int(r[0]) >> 8) & 0xFFFFFFF, int(r[0]) >> 36
+        by_, gy = int(r[3]) & 0xFFFFFFFF, int(r[3]) >> 32
+        by[(kid, gx * max(gy, 1))].append((int(r[2]), (bx, by_), r))
+    out = []
+    for (kid, grid), lst in by.items():
+        lst.sort(key=lambda t: t[0])
+        cur, seen = [], set()
+        for t0, blk, r in lst:
+            if blk in seen:
+                out.append((kid, grid, cur))
+                cur, seen = [], set()
+            seen.add(blk)
+            cur.append(r)
+        if cur:
+            out.append((kid, grid, cur))
+    out.sort(key=lambda L: min(int(r[2]) for r in L[2]))
+    return out
+
+
+def wg_end(r):
+    nw = (int(r[1]) >> 40) & 0xFF
+    ends = [int(x) for x in r[4:4 + nw] if int(x) > 0]
+    return max(ends) if ends else int(r[2])
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+    L = lib()
+    y, X, Z, th, sy = make_problem(n, 20, 10, seed=5)
+    m = ace.DeviceModel("Matern32", n, 20, 10)
+    m.set_data(y, X, Z, sy)
+    theta = th.copy()
+    for it in (1, 2):
+        m.para_update(it, theta)
+    read(L, True)
+    m.para_update(3, theta)
+    recs = read(L, True)
+    print(f"n={n}: {len(recs)} workgroup records")
+    ls = launches(recs)
+    t0 = min(int(r[2]) for r in recs)
+    bulk_grid = max(g for k, g, _ in ls if k == 5)
+    stats = defaultdict(lambda: {"span": [], "wg": [], "spread": [], "t": []})
+    for kid, grid, rs in ls:
+        st = min(int(r[2]) for r in rs)
+        en = max(wg_end(r) for r in rs)
+        durs = [wg_end(r) - int(r[2]) for r in rs]
+        name = KIND.get(kid, str(kid))
+        if kid == 5:
+            name = "bulk(sampled)" if grid == bulk_grid else "update_multi(cross/T)"
+        s = stats[name]
+        s["span"].append((en - st) * TICK_US)
+        s["wg"].append(np.median(durs) * TICK_US)
+        s["spread"].append((max(int(r[2]) for r in rs) - st) * TICK_US)
+        s["t"].append((st - t0) * TICK_US)
+    print("%-24s %6s %10s %12s %12s   (us; medians over launches, then [p10, p90])" % (
+        "kernel", "launch", "span", "wg duration", "entry spread"))
+    for name, s in sorted(stats.items()):
+        def q(v):
+            v = np.asarray(v)
+            return "%7.1f [%5.1f,%6.1f]" % (np.median(v), np.percentile(v, 10), np.percentile(v, 90))
+        print("%-24s %6d %s %s %s" % (name, len(s["span"]), q(s["span"]), q(s["wg"]), q(s["spread"])))
+    bulks = sorted((min(int(r[2]) for r in rs) - t0) * TICK_US for k, g, rs in ls
+                   if k == 5 and g == bulk_grid)
+    if len(bulks) > 9:
+        print("launch sequence during bulk 8 (%.1f - %.1f us):" % (bulks[8], bulks[9]))
+        sequence(ls, t0, bulks[8] - 50.0, bulks[9])
+    # the first group (under the assembly) against the rest
+    for name in ("panel_split", "pivot"):
+        s = stats.get(name)
+        if not s:
+            continue
+        t = np.asarray(s["t"])
+        first = t < 3000.0
+        for lab, sel in (("first 3 ms", first), ("after", ~first)):
+            if sel.any():
+                print("  %-12s %-10s span %6.1f  wg %6.1f  spread %6.1f  (%d launches)" % (
+                    name, lab, np.median(np.asarray(s["span"])[sel]), np.median(np.asarray(s["wg"])[sel]),
+                    np.median(np.asarray(s["spread"])[sel]), int(sel.sum())))
+
+
+def sequence(ls, t0, lo_us, hi_us):
+    """Every launch starting in [lo, hi) us: name, grid, first entry, last
+    exit, median workgroup duration (us from the evaluation's first record)."""
+    for kid, grid, rs in ls:
+        st = (min(int(r[2]) for r in rs) - t0) * TICK_US
+        if not lo_us <= st < hi_us:
+            continue
+        en = (max(wg_end(r) for r in rs) - t0) * TICK_US
+        d = np.median([wg_end(r) - int(r[2]) for r in rs]) * TICK_US
+        print("    %-14s grid %6d  %9.1f - %9.1f  (wg %6.1f, %d recs)" % (
+            KIND.get(kid, str(kid)), grid, st, en, d, len(rs)))
+
+
+if __name__ == "__main__":
+    main()
