@@ -78,6 +78,9 @@ struct WgTime {
     __syncthreads();
     slot = *sh;
   }
+  __device__ void mark(int i) const {  // intermediate clock of wave 0 (records 12..15)
+    if (slot < WGT_CAP && threadIdx.x == 0) d_wgt_rec[(size_t)slot * WGT_REC + 12 + i] = wall_clock64();
+  }
   __device__ ~WgTime() {
     if (slot < WGT_CAP && (threadIdx.x & 63) == 0)
       d_wgt_rec[(size_t)slot * WGT_REC + 4 + (threadIdx.x >> 6)] = wall_clock64();
@@ -86,8 +89,10 @@ struct WgTime {
 #define ACE_WGT(kid, on)                 \
   __shared__ unsigned wgt_slot_sh_;      \
   WgTime wgt_(kid, &wgt_slot_sh_, (on))
+#define ACE_WGT_MARK(i) wgt_.mark(i)
 #else
 #define ACE_WGT(kid, on)
+#define ACE_WGT_MARK(i)
 #endif
 
 // ---------------------------------------------------------------- pivot
@@ -926,7 +931,11 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
   const int sk = tid >> 5, sm = (tid & 31) * SM128;  // 2nd half at sm + SH128
+#ifdef ACE_DIAG_PGEMM_HOT  // timing diagnostic only (results wrong): every tile reads rows 0..127
+  const double *gW = Pn + sm + (int64_t)sk * ldp;
+#else
   const double *gW = Pn + (R0 + sm) + (int64_t)sk * ldp;
+#endif
   const double *gP = W + (k0 + C0 + sm) + (int64_t)sk * ldp;  // W_kk(c, k) = W[k0 + c, k]
   double2 rw[2], rp[2];
 #pragma unroll
@@ -946,6 +955,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
     *reinterpret_cast<double2 *>(&sP[0][sk][sm + SH128 * e]) = rp[e];
   }
   __syncthreads();
+  ACE_WGT_MARK(0);
   for (int ch = 0; ch < NCH; ++ch) {
     const int cur = ch & 1;
     if (ch + 1 < NCH) {
@@ -978,6 +988,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
     }
     __syncthreads();
   }
+  ACE_WGT_MARK(1);
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci)
 #pragma unroll

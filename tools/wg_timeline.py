@@ -106,6 +106,19 @@ def main():
             v = np.asarray(v)
             return "%7.1f [%5.1f,%6.1f]" % (np.median(v), np.percentile(v, 10), np.percentile(v, 90))
         print("%-24s %6d %s %s %s" % (name, len(s["span"]), q(s["span"]), q(s["wg"]), q(s["spread"])))
+    # k_panel_gemm_t phases (wave 0): entry -> staged first chunk -> K loop done -> exit
+    ph = []
+    for kid, grid, rs in ls:
+        if kid != 3:
+            continue
+        for r in rs:
+            m0, m1 = int(r[12]), int(r[13])
+            if m0 and m1:
+                ph.append(((m0 - int(r[2])) * TICK_US, (m1 - m0) * TICK_US, (wg_end(r) - m1) * TICK_US))
+    if ph:
+        a = np.asarray(ph)
+        print("panel_gemm_t phases (median us): prologue %.1f  K loop %.1f  epilogue %.1f  (%d wgs)" % (
+            np.median(a[:, 0]), np.median(a[:, 1]), np.median(a[:, 2]), len(a)))
     bulks = sorted((min(int(r[2]) for r in rs) - t0) * TICK_US for k, g, rs in ls
                    if k == 5 and g == bulk_grid)
     if len(bulks) > 9:
