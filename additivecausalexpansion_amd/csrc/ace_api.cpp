@@ -516,6 +516,14 @@ static int env_flag(const char *name, int dflt) {
   const char *e = getenv(name);
   return e ? atoi(e) : dflt;
 }
+static int asm_tail_mode() {
+  static const int v = env_flag("ACE_ASM_TAIL", 1);
+  return v;
+}
+static bool asm_fill_on() {
+  static const bool v = env_flag("ACE_ASM_FILL", 1) != 0;
+  return v;
+}
 
 struct AsmFill {
   int kind, PM, B, ZS, slots;
@@ -577,13 +585,13 @@ void assemble_and_sweep(ace_ctx *ctx, SweepWork &w, const Shape &s, const PairSi
     ck(ctx, launch_assembly_persist(s.kind, s.PM, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
                                     st, w.aq.i(), R),
        "assembly (persistent)");
-    const int tail = env_flag("ACE_ASM_TAIL", 1);
+    const int tail = asm_tail_mode();
     if (tail == 0) {  // group 0's tail path after the whole assembly
       sy.tail_after = sy.ev[5 * steps + 5];
       ck(ctx, hipEventRecord(sy.tail_after, st), "event");
     }
     sy.tail_split = tail == 2;  // ... after group 0's head path
-    const int per = env_flag("ACE_ASM_FILL", 1) ? assembly_persist_per_cu(s.kind, s.PM, s.B) : 0;
+    const int per = asm_fill_on() ? assembly_persist_per_cu(s.kind, s.PM, s.B) : 0;
     if (per > 0) {  // the reserved CUs: R per engine, 4 engines per XCD, 8 XCDs
       fill = AsmFill{s.kind, s.PM, s.B, s.ZS, 32 * R * per, ps, w.npad, w.naug, tv, sig, w.A.d(), w.aq.i()};
       sy.fill = asm_fill;
