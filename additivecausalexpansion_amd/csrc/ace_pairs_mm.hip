@@ -24,6 +24,7 @@
 #include <type_traits>
 
 #include "ace_internal.h"
+#include "ace_wgtime.h"
 
 namespace ace {
 
@@ -897,6 +898,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
     PairSide S, int B, int ZS, TabView tab, const double *__restrict__ A, int64_t ld, double sA,
     const double *__restrict__ alpha, double *__restrict__ gpart, int64_t ldg,
     const Tile *__restrict__ tiles, int G, int64_t t0) {
+  ACE_WGT(7 + (DG ? 1 : 0), true);
   constexpr int NT = 64 * 4 * (4 / CB);      // threads
   constexpr int NWV = NT / 64;               // waves
   constexpr int XP = xj_pitch(PM);
@@ -965,6 +967,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   const double ar = rvalid ? alpha[r] : 0.0;
   const MmLds L = mm_stage<PM, KIND, true, NT>(lds, S, B, ZS, tab.wk, wlast, R0, C0, tid,
                                                tab.norms, tab.ldn);
+  ACE_WGT_MARK(0);
   // T = w_rc (sA A[r,c] - alpha_r alpha_c), w = 2 off the diagonal (lower pairs)
   double tv[CB][4];
   double tr = 0.0;
@@ -1257,6 +1260,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
       if (tid <= PM) finish(b, red, tid);
     }
   }
+  ACE_WGT_MARK(1);
   // trace of T
   tr += xor_row(tr, 1);
   tr += xor_row(tr, 2);
@@ -1501,6 +1505,14 @@ int assembly_persist_per_cu(int kind, int PM, int B) {
     default: return 0;
   }
 }
+
+#ifdef ACE_DIAG_WGTIME
+}  // namespace ace
+extern "C" long long ace_diag_wgtime_pairs(void *dst, long long cap, int reset) {
+  return ace::wgt_read(dst, cap, reset);
+}
+namespace ace {
+#endif
 
 hipError_t launch_assembly_persist(int kind, int PM, PairSide S, int64_t npad, int B, int ZS,
                                    TabView tab, double sig, double *out, int64_t ld,

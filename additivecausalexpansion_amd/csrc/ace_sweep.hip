@@ -27,6 +27,8 @@
 #include <functional>
 #include <map>
 
+#include "ace_wgtime.h"
+
 namespace ace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -45,55 +47,6 @@ typedef double d4 __attribute__((ext_vector_type(4)));
   do {               \
     if (ACE_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(ACE_CHAIN_PRIO); \
   } while (0)
-
-// ACE_DIAG_WGTIME (diagnostic builds only, tools/wg_timeline.py): per
-// workgroup of the sweep kernels, the wall clock (100 MHz) at entry and per
-// wave at exit, the CU (HW_REG_HW_ID / XCC_ID) and the launch's grid, into a
-// device record array read back by ace_diag_wgtime.  The bulk launches are
-// sampled (every 32nd workgroup).  Workgroups start with one extra barrier.
-#ifdef ACE_DIAG_WGTIME
-constexpr int WGT_REC = 16, WGT_CAP = 1 << 18;
-__device__ unsigned long long d_wgt_rec[(size_t)WGT_CAP * WGT_REC];
-__device__ unsigned d_wgt_cnt;
-struct WgTime {
-  unsigned slot = ~0u;
-  __device__ WgTime(int kid, unsigned *sh, bool on) {
-    if (!on) return;
-    const unsigned long long t0 = wall_clock64();
-    if (threadIdx.x == 0) {
-      const unsigned sl = atomicAdd(&d_wgt_cnt, 1u);
-      *sh = sl;
-      if (sl < WGT_CAP) {
-        unsigned long long *r = d_wgt_rec + (size_t)sl * WGT_REC;
-        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-        const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 15;
-        r[0] = (unsigned long long)kid | ((unsigned long long)blockIdx.x << 8) |
-               ((unsigned long long)gridDim.x << 36);
-        r[1] = (unsigned long long)hw | ((unsigned long long)xcc << 32) |
-               ((unsigned long long)(blockDim.x >> 6) << 40);
-        r[2] = t0;
-        r[3] = (unsigned long long)blockIdx.y | ((unsigned long long)gridDim.y << 32);
-      }
-    }
-    __syncthreads();
-    slot = *sh;
-  }
-  __device__ void mark(int i) const {  // intermediate clock of wave 0 (records 12..15)
-    if (slot < WGT_CAP && threadIdx.x == 0) d_wgt_rec[(size_t)slot * WGT_REC + 12 + i] = wall_clock64();
-  }
-  __device__ ~WgTime() {
-    if (slot < WGT_CAP && (threadIdx.x & 63) == 0)
-      d_wgt_rec[(size_t)slot * WGT_REC + 4 + (threadIdx.x >> 6)] = wall_clock64();
-  }
-};
-#define ACE_WGT(kid, on)                 \
-  __shared__ unsigned wgt_slot_sh_;      \
-  WgTime wgt_(kid, &wgt_slot_sh_, (on))
-#define ACE_WGT_MARK(i) wgt_.mark(i)
-#else
-#define ACE_WGT(kid, on)
-#define ACE_WGT_MARK(i)
-#endif
 
 // ---------------------------------------------------------------- pivot
 // Sweeps the 64x64 sub-block s of the panel's pivot rows:
@@ -2953,22 +2906,8 @@ hipError_t shard_update_main(const ShardSweep &b, int k, int buf, int kx, hipStr
 }  // namespace ace
 
 #ifdef ACE_DIAG_WGTIME
-// Diagnostic builds: copies up to cap records (16 x u64 each, see WgTime) to
-// dst and returns how many the device wrote since the last reset (reset != 0
-// zeroes the counter after the copy).  Device-synchronous.
+// Diagnostic builds: this translation unit's workgroup records (ace_wgtime.h)
 extern "C" long long ace_diag_wgtime(void *dst, long long cap, int reset) {
-  unsigned cnt = 0;
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(ace::d_wgt_cnt), sizeof(cnt)) != hipSuccess) return -1;
-  const long long n = std::min<long long>(std::min<long long>(cnt, ace::WGT_CAP), cap);
-  if (dst && n > 0 &&
-      hipMemcpyFromSymbol(dst, HIP_SYMBOL(ace::d_wgt_rec), (size_t)n * ace::WGT_REC * 8) != hipSuccess)
-    return -1;
-  if (reset) {
-    const unsigned z = 0;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(ace::d_wgt_cnt), &z, sizeof(z)) != hipSuccess) return -1;
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-  }
-  return (long long)cnt;
+  return ace::wgt_read(dst, cap, reset);
 }
 #endif

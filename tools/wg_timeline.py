@@ -24,20 +24,24 @@ from additivecausalexpansion_amd._lib import lib  # noqa: E402
 from additivecausalexpansion_amd.synthetic import make_problem  # noqa: E402
 
 KIND = {1: "pivot", 2: "panel_split", 3: "panel_gemm_t", 4: "update_q", 5: "update_multi",
-        6: "update"}
+        6: "update", 7: "grad_mm", 8: "grad_mm(diag)"}
 REC = 16
 TICK_US = 0.01  # wall_clock64: 100 MHz
 
 
 def read(L, reset):
-    f = L.ace_diag_wgtime
-    f.restype = ctypes.c_longlong
-    f.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int]
-    cnt = f(None, 0, 0)
-    buf = np.zeros((max(cnt, 1), REC), dtype=np.uint64)
-    got = f(buf.ctypes.data, cnt, 1 if reset else 0)
-    assert got >= 0, "ace_diag_wgtime failed"
-    return buf[:min(cnt, buf.shape[0])]
+    """Both translation units' records (sweep kernels, pair kernels)."""
+    out = []
+    for name in ("ace_diag_wgtime", "ace_diag_wgtime_pairs"):
+        f = getattr(L, name)
+        f.restype = ctypes.c_longlong
+        f.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int]
+        cnt = f(None, 0, 0)
+        buf = np.zeros((max(cnt, 1), REC), dtype=np.uint64)
+        got = f(buf.ctypes.data, cnt, 1 if reset else 0)
+        assert got >= 0, name + " failed"
+        out.append(buf[:min(cnt, buf.shape[0])])
+    return np.concatenate(out)
 
 
 def launches(recs):
@@ -119,6 +123,22 @@ def main():
         a = np.asarray(ph)
         print("panel_gemm_t phases (median us): prologue %.1f  K loop %.1f  epilogue %.1f  (%d wgs)" % (
             np.median(a[:, 0]), np.median(a[:, 1]), np.median(a[:, 2]), len(a)))
+    # gradient tiles (wave 0): entry -> staged (prologue) -> slice loop done -> exit
+    gp = []
+    for kid, grid, rs in ls:
+        if kid != 7:
+            continue
+        for r in rs:
+            m0, m1 = int(r[12]), int(r[13])
+            if m0 and m1:
+                gp.append(((m0 - int(r[2])) * TICK_US, (m1 - m0) * TICK_US, (wg_end(r) - m1) * TICK_US))
+    if gp:
+        a = np.asarray(gp)
+        tot = a.sum(axis=1)
+        print("grad_mm tiles (us): prologue median %.1f mean %.1f | slice loop median %.1f | finish median %.1f"
+              " | prologue share of workgroup time %.1f %% (%d tiles)" % (
+                  np.median(a[:, 0]), a[:, 0].mean(), np.median(a[:, 1]), np.median(a[:, 2]),
+                  100.0 * a[:, 0].sum() / tot.sum(), len(a)))
     bulks = sorted((min(int(r[2]) for r in rs) - t0) * TICK_US for k, g, rs in ls
                    if k == 5 and g == bulk_grid)
     if len(bulks) > 9:
