@@ -32,6 +32,7 @@ struct WgTime {
                ((unsigned long long)(blockDim.x >> 6) << 40);
         r[2] = t0;
         r[3] = (unsigned long long)blockIdx.y | ((unsigned long long)gridDim.y << 32);
+        for (int k = 4; k < WGT_REC; ++k) r[k] = 0;  // no stale exits / marks
       }
     }
     __syncthreads();

@@ -53,6 +53,10 @@ for step in "$@"; do
           cut -c1-300 gpurun_out/$tag/bench_c1.json gpurun_out/$tag/bench_c3.json ;;
     wgt) ACE_LIB_PATH=tools/libace_wgt.so timeout -k 10 200 python tools/wg_timeline.py > gpurun_out/$tag/wgt.txt 2>&1; rc=$?; cat gpurun_out/$tag/wgt.txt | tail -30 ;;
     wgthot) ACE_LIB_PATH=tools/libace_wgthot.so timeout -k 10 200 python tools/wg_timeline.py > gpurun_out/$tag/wgthot.txt 2>&1; rc=$?; head -12 gpurun_out/$tag/wgthot.txt ;;
+    hg) timeout -k 10 700 bash tools/host_gap.sh > gpurun_out/$tag/host_gap.txt 2>&1; rc=$?; head -60 gpurun_out/$tag/host_gap.txt ;;
+    abbatch) timeout -k 10 200 python tools/cmp_libs.py additivecausalexpansion_amd/libace_hip.so tools/libace_cur.so 16384 Matern32 && \
+             timeout -k 10 200 python tools/cmp_libs.py additivecausalexpansion_amd/libace_hip.so tools/libace_cur.so 4096 SE && \
+             ROUNDS=3 bash tools/ab_libs.sh tools/libace_cur.so additivecausalexpansion_amd/libace_hip.so -- --no-r6; rc=$? ;;
     abexp) timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_exp256.so 16384 Matern32; \
            timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_exp256.so 4096 SE; \
            ROUNDS=3 bash tools/ab_libs.sh tools/libace_cur.so tools/libace_exp256.so -- --no-r6; rc=$? ;;
