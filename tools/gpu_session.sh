@@ -57,6 +57,8 @@ for step in "$@"; do
     abbatch) timeout -k 10 200 python tools/cmp_libs.py additivecausalexpansion_amd/libace_hip.so tools/libace_cur.so 16384 Matern32 && \
              timeout -k 10 200 python tools/cmp_libs.py additivecausalexpansion_amd/libace_hip.so tools/libace_cur.so 4096 SE && \
              ROUNDS=3 bash tools/ab_libs.sh tools/libace_cur.so additivecausalexpansion_amd/libace_hip.so -- --no-r6; rc=$? ;;
+    abg0) CMP_ENV_B="ACE_GATHER_PIV=1" timeout -k 10 200 python tools/cmp_libs.py additivecausalexpansion_amd/libace_hip.so additivecausalexpansion_amd/libace_hip.so 16384 Matern32 && \
+          ROUNDS=3 bash tools/ab_envs.sh "" "ACE_GATHER_PIV=1" "ACE_HEADQ=0"; rc=$? ;;
     abexp) timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_exp256.so 16384 Matern32; \
            timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_exp256.so 4096 SE; \
            ROUNDS=3 bash tools/ab_libs.sh tools/libace_cur.so tools/libace_exp256.so -- --no-r6; rc=$? ;;
