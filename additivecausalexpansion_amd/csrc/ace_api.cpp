@@ -107,7 +107,15 @@ int ace_create(int device, ace_ctx **out) {
   // results are bit-identical for every value.
   const char *vs = getenv("ACE_STREAMS");
   const int nstr = vs ? std::min(3, std::max(1, atoi(vs))) : 3;
-  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  // ACE_MAIN_PRIO=0: the main stream (bulk update, pair kernels) at the least
+  // priority instead of the default (A/B switch)
+  {
+    const char *vm = getenv("ACE_MAIN_PRIO");
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    e = (vm && atoi(vm) == 0) ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, lo)
+                              : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  }
   if (e == hipSuccess) c->nstreams = 1;
   if (e == hipSuccess && nstr >= 2) {
     // the lookahead panel chain is latency-bound: give it the highest priority

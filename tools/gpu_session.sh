@@ -59,6 +59,7 @@ for step in "$@"; do
              ROUNDS=3 bash tools/ab_libs.sh tools/libace_cur.so additivecausalexpansion_amd/libace_hip.so -- --no-r6; rc=$? ;;
     abg0) CMP_ENV_B="ACE_GATHER_PIV=1" timeout -k 10 200 python tools/cmp_libs.py additivecausalexpansion_amd/libace_hip.so additivecausalexpansion_amd/libace_hip.so 16384 Matern32 && \
           ROUNDS=3 bash tools/ab_envs.sh "" "ACE_GATHER_PIV=1" "ACE_HEADQ=0"; rc=$? ;;
+    abprio) ROUNDS=3 bash tools/ab_envs.sh "" "ACE_MAIN_PRIO=0" "ACE_MAIN_PRIO=0 ACE_SIDE2_PRIO=2" "ACE_MAIN_PRIO=0 ACE_HEADQ=0"; rc=$? ;;
     abexp) timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_exp256.so 16384 Matern32; \
            timeout -k 10 200 python tools/cmp_libs.py tools/libace_cur.so tools/libace_exp256.so 4096 SE; \
            ROUNDS=3 bash tools/ab_libs.sh tools/libace_cur.so tools/libace_exp256.so -- --no-r6; rc=$? ;;
