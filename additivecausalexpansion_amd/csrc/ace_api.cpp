@@ -67,6 +67,7 @@ void ace_host::sync_stream(ace_ctx *ctx, hipStream_t s, const char *what) {
       snprintf(buf, sizeof buf, "%s: device work did not complete within %.0f s (streams still busy:%s)",
                what, lim, busy.empty() ? " none" : busy.c_str());
       ctx->err = buf;
+      ctx->failed = true;  // later calls refuse to run (check_usable)
       fprintf(stderr, "ace: %s\n", buf);
       throw Fail{ACE_ERR_TIMEOUT};
     }
@@ -107,15 +108,7 @@ int ace_create(int device, ace_ctx **out) {
   // results are bit-identical for every value.
   const char *vs = getenv("ACE_STREAMS");
   const int nstr = vs ? std::min(3, std::max(1, atoi(vs))) : 3;
-  // ACE_MAIN_PRIO=0: the main stream (bulk update, pair kernels) at the least
-  // priority instead of the default (A/B switch)
-  {
-    const char *vm = getenv("ACE_MAIN_PRIO");
-    int lo = 0, hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-    e = (vm && atoi(vm) == 0) ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, lo)
-                              : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  }
+  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) c->nstreams = 1;
   if (e == hipSuccess && nstr >= 2) {
     // the lookahead panel chain is latency-bound: give it the highest priority
@@ -146,19 +139,6 @@ int ace_create(int device, ace_ctx **out) {
   // free, so the schedules run unchanged in host order
   if (!c->side) c->side = c->stream;
   if (!c->side2) c->side2 = c->side;
-#ifdef ACE_DIAG_MASKED_STREAM
-  {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
-      const int ncu = prop.multiProcessorCount;
-      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-      for (int i = 8; i < ncu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
-      if (hipExtStreamCreateWithCUMask(&c->diag_masked, (uint32_t)ncu, mask.data()) != hipSuccess)
-        c->diag_masked = nullptr;
-      (void)hipEventCreateWithFlags(&c->diag_ev, ACE_SYNC_EVENT_FLAGS);
-    }
-  }
-#endif
   *out = c;
   return ACE_OK;
 }
@@ -166,10 +146,6 @@ int ace_create(int device, ace_ctx **out) {
 void ace_destroy(ace_ctx *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-#ifdef ACE_DIAG_MASKED_STREAM
-  if (ctx->diag_masked) (void)hipStreamDestroy(ctx->diag_masked);
-  if (ctx->diag_ev) (void)hipEventDestroy(ctx->diag_ev);
-#endif
   if (ctx->side2 && ctx->side2 != ctx->side) (void)hipStreamDestroy(ctx->side2);
   if (ctx->side && ctx->side != ctx->stream) (void)hipStreamDestroy(ctx->side);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -577,17 +553,6 @@ void assemble_and_sweep(ace_ctx *ctx, SweepWork &w, const Shape &s, const PairSi
     ck(ctx, hipEventRecord(sy.ev[2 * steps], st), "event");
     sy.ready_recorded = true;
   }
-#ifdef ACE_DIAG_MASKED_STREAM
-  if (ctx->diag_masked && sy.ready_recorded) {
-    ck(ctx, hipStreamWaitEvent(ctx->diag_masked, sy.ev[2 * steps], 0), "wait");
-    ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
-                            nullptr, ctx->diag_masked, nullptr, 0, 1, 2),
-       "assembly");
-    ck(ctx, hipEventRecord(ctx->diag_ev, ctx->diag_masked), "event");
-    ck(ctx, hipStreamWaitEvent(st, ctx->diag_ev, 0), "wait");
-    ck(ctx, hipStreamWaitEvent(ctx->side2, ctx->diag_ev, 0), "wait");
-  } else
-#endif
   AsmFill fill;
   if (persist && sy.ready_recorded) {
     ck(ctx, launch_assembly_persist(s.kind, s.PM, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
@@ -605,10 +570,14 @@ void assemble_and_sweep(ace_ctx *ctx, SweepWork &w, const Shape &s, const PairSi
       sy.fill = asm_fill;
       sy.fill_arg = &fill;
     }
-  } else
-  ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
-                          nullptr, st, nullptr, 0, 1, 2),
-     "assembly");
+  } else {
+    ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
+                            nullptr, st, nullptr, 0, 1, 2),
+       "assembly");
+  }
+  // with the persistent queue this marks the MAIN launch's end: the tiles
+  // the filler launch (side2, after group 0's lookahead) takes are counted in
+  // the assembly's work but not in this interval (DESIGN §8 note)
   if (ev_asm) ck(ctx, hipEventRecord(ev_asm[1], st), "event");
   ck(ctx, run_sweep(w.bufs(), st, &sy, tmg), "sweep");
 }

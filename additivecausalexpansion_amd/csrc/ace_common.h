@@ -34,17 +34,14 @@ struct ace_ctx {
   int (*poll)(void *) = nullptr; // optional interrupt poll (ace_set_interrupt_poll)
   void *poll_user = nullptr;
   std::string err;
+  // set when a bounded sync timed out (ACE_ERR_TIMEOUT): copies enqueued
+  // before the deadline may still land, so every later call on this context
+  // refuses to run (ACE_ERR_TIMEOUT) instead of reusing its buffers
+  bool failed = false;
   // sweep buffers of freed inverse handles (ace_dmat.cpp), reused by the
   // next invkernel_dev of the same n instead of a new 2 n^2-byte allocation
   std::vector<std::shared_ptr<SweepWork>> sweep_pool;
   std::shared_ptr<void> dmat_state;  // the handle path's cached inputs (ace_dmat.cpp)
-#ifdef ACE_DIAG_MASKED_STREAM
-  // diagnostic builds only (tools/build_variant.sh): round 3's
-  // stalled configuration, the assembly's second part on a fourth,
-  // CU-masked stream (hipExtStreamCreateWithCUMask: blocking flags)
-  hipStream_t diag_masked = nullptr;
-  hipEvent_t diag_ev = nullptr;
-#endif
 };
 
 extern std::string g_create_err;
@@ -123,26 +120,31 @@ inline void alloc(ace_ctx *ctx, DBuf &b, size_t bytes, const char *what) {
 void sync_stream(ace_ctx *ctx, hipStream_t s, const char *what);
 inline void sync(ace_ctx *ctx) { sync_stream(ctx, ctx->stream, "hipStreamSynchronize"); }
 
-// Host -> device copies: stream-ordered on the main stream (never the null
-// stream) and complete on return (pageable host buffers may be temporaries);
-// every call syncs its stream before returning, so no kernel of a previous
-// call can still be reading the destination.
+// Host <-> device copies: stream-ordered on the main stream (never the null
+// stream).  The stream is drained (bounded) BEFORE a copy is queued: a
+// pageable copy blocks inside the runtime until earlier stream work is done,
+// which would bypass ACE_SYNC_TIMEOUT, and a timeout then leaves no copy
+// into caller memory queued.  Uploads are complete on return (pageable host
+// buffers may be temporaries); downloads complete at the caller's next sync.
 inline void upload(ace_ctx *ctx, DBuf &b, const double *h, size_t count, const char *what) {
   alloc(ctx, b, count * sizeof(double), what);
   if (!count) return;
+  sync_stream(ctx, ctx->stream, what);
   ck(ctx, hipMemcpyAsync(b.p, h, count * sizeof(double), hipMemcpyHostToDevice, ctx->stream), what);
   sync_stream(ctx, ctx->stream, what);
 }
 // the same for any trivially copyable host array (tile lists)
 inline void upload_bytes(ace_ctx *ctx, void *d, const void *h, size_t bytes, const char *what) {
   if (!bytes) return;
+  sync_stream(ctx, ctx->stream, what);
   ck(ctx, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream), what);
   sync_stream(ctx, ctx->stream, what);
 }
 
 inline void download(ace_ctx *ctx, double *h, const double *d, size_t count, const char *what) {
-  if (count) ck(ctx, hipMemcpyAsync(h, d, count * sizeof(double), hipMemcpyDeviceToHost,
-                                    ctx->stream), what);
+  if (!count) return;
+  sync_stream(ctx, ctx->stream, what);
+  ck(ctx, hipMemcpyAsync(h, d, count * sizeof(double), hipMemcpyDeviceToHost, ctx->stream), what);
 }
 
 // Pinned host staging for the per-evaluation traffic (theta tables up, the
@@ -341,7 +343,16 @@ inline void finish_marginal(int64_t nx, const double *a, const double *kd, const
 }  // namespace ace_host
 using namespace ace_host;
 
-#define ACE_TRY try {
+// Every ABI entry point: a context whose bounded sync timed out refuses work
+inline void check_usable(ace_ctx *ctx) {
+  if (!ctx->failed) return;
+  ctx->err = "context unusable: an earlier call timed out (ACE_ERR_TIMEOUT); destroy it";
+  throw Fail{ACE_ERR_TIMEOUT};
+}
+
+#define ACE_TRY \
+  try {         \
+    check_usable(ctx);
 #define ACE_CATCH \
   }               \
   catch (const Fail &f) { return f.code; }

@@ -263,10 +263,10 @@ std::shared_ptr<SweepWork> pooled_sweep(ace_ctx *ctx, int64_t n) {
   auto w = std::make_shared<SweepWork>();
   try {
     w->ensure(ctx, n);
-  } catch (const Fail &) {
+  } catch (const Fail &f) {
     // out of device memory with pooled buffers of other sizes: drop them and
-    // try once more
-    if (pool.empty()) throw;
+    // try once more (any other failure, e.g. ACE_ERR_TIMEOUT, propagates)
+    if (f.code != ACE_ERR_OOM || pool.empty()) throw;
     pool.clear();
     w = std::make_shared<SweepWork>();
     w->ensure(ctx, n);

@@ -99,6 +99,9 @@ hipError_t launch_assembly_persist(int kind, int PM, PairSide S, int64_t npad, i
 int assembly_persist_per_cu(int kind, int PM, int B);
 bool pairs_use_mm(int PM, bool grad);
 bool mm_lds_ok(int PM, int B, int kind, bool grad);
+// mode 2 without a cube on the MFMA r2 expansion (k_cross_mm): R.n x C.n, ld
+hipError_t launch_cross_mm(int kind, int PM, PairSide R, PairSide C, int B, int ZS, TabView tab,
+                           int b0, int b1, double *out, int64_t ld, hipStream_t st);
 hipError_t launch_grad_mm(int kind, int PM, PairSide S, int B, int ZS, TabView tab,
                           const double *A, int64_t ld, double sA, const double *alpha,
                           double *gpart, hipStream_t st, const Tile *tiles, int64_t ntiles, int G,

@@ -754,6 +754,127 @@ __global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 32 ? 3 : 2)) v
   asm_mm_tile<PM, KIND>(lds, S, B, ZS, tab, sg, out, ld, kcopy, I, J, G);
 }
 
+// ---------------------------------------------------------------------------
+// Cross assembly on the MFMA r2 expansion (kernmat_*_cpp without a cube,
+// src/kernel_SE_cpp.cpp:9-64, src/kernel_Matern_cpp.cpp:52-93; prediction's
+// K_xX): tile (I, J) of the R.n x C.n block, rows from R (the reference's
+// first operand X1: test points), columns from C (X2: training points),
+// slices [b0, b1).  The symmetric tile's arithmetic (asm_mm_tile) with two
+// point sets: per slice r2 = s_b(r) + s_b(c) - 2 sum_i w_bi x_ri x_ci, the
+// cross term one GEMM1 (K = PM) on v_mfma_f64_16x16x4f64, K_b per pair on
+// the VALU in the GEMM's fragment layout; both sides' slice norms computed
+// per tile (i ascending, fma(x^2, w, s), as k_slice_norms).  Out of range
+// rows / columns are staged as zeros and never written.  Replaces
+// k_assembly<PM, KIND, 2> (lane = row, p FMAs per pair and slice on the
+// VALU: 10.8 TF/s at n = 16384, nx = 4096).
+// ---------------------------------------------------------------------------
+template <int PM, int KIND>
+__global__ __launch_bounds__(256, PM <= 32 ? 3 : 2) void k_cross_mm(PairSide R, PairSide C, int B,
+                                                                   int ZS, TabView tab, int b0,
+                                                                   int b1,
+                                                                   double *__restrict__ out,
+                                                                   int64_t ld) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  constexpr int XP = xj_pitch(PM);
+  const int64_t J = blockIdx.x, I = blockIdx.y;
+  const int64_t R0 = I * AT, C0 = J * AT;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  const MmLayout o = mm_layout(PM, B, KIND, false);
+  double *const E = lds + o.etab, *const XJ = lds + o.xj, *const Zc = lds + o.z + 64,
+               *const LZc = lds + o.lz + 64, *const Nc = lds + o.nc, *const Nr = lds + o.nr,
+               *const W = lds + o.w;
+  for (int e = tid; e < 64 * PM; e += 256) {
+    const int c = e / PM, i = e - c * PM;
+    XJ[c * XP + i] = (C0 + c < C.n) ? C.X[(C0 + c) * PM + i] : 0.0;
+  }
+  for (int e = tid; e < (B - 1) * 64; e += 256) {
+    const int bb = e >> 6, c = e & 63;
+    const bool ok = C0 + c < C.n;
+    Zc[e] = ok ? C.Z[(C0 + c) * ZS + bb] : 0.0;
+    if (KIND == 0) LZc[e] = ok ? C.LZ[(C0 + c) * ZS + bb] : 0.0;
+  }
+  if (tid < 64) {  // slice 0: z = 1, log|z| = 0
+    Zc[tid - 64] = 1.0;
+    if (KIND == 0) LZc[tid - 64] = 0.0;
+    if (ACE_ASM_EXP == 2) E[tid] = kExp2Tab64[tid];
+    else if (tid < 32) E[tid] = kExp2Tab[tid];
+  }
+  for (int e = tid; e < B * PM; e += 256) W[e] = tab.wk[e];
+  __syncthreads();
+  for (int e = tid; e < 2 * B * 64; e += 256) {
+    const int side = e / (B * 64), rem = e - side * B * 64;
+    const int sl = rem >> 6, pt = rem & 63;
+    const double *wv = W + sl * PM;
+    double s = 0.0;
+    if (side == 0) {
+#pragma unroll 4
+      for (int i = 0; i < PM; ++i) {
+        const double x = XJ[pt * XP + i];
+        s = fma(x * x, wv[i], s);
+      }
+      Nc[rem] = s;
+    } else if (R0 + pt < R.n) {
+      const double *xr = R.X + (R0 + pt) * PM;
+#pragma unroll 4
+      for (int i = 0; i < PM; ++i) {
+        const double x = xr[i];
+        s = fma(x * x, wv[i], s);
+      }
+      Nr[rem] = s;
+    } else {
+      Nr[rem] = 0.0;
+    }
+  }
+  __syncthreads();
+  const int rl = 16 * w + lr;
+  const int64_t r = R0 + rl;
+  const bool rok = r < R.n;
+  RowX<PM> xr;
+  xr.load(R.X + (rok ? r : 0) * PM, lk);
+  double kf[4][4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) kf[cb][v] = 0.0;
+  for (int b = b0; b < b1; ++b) {
+    double zr = 0.0, lzr = 0.0;
+    if (b > 0 && rok) {
+      zr = R.Z[r * ZS + b - 1];
+      if (KIND == 0) lzr = R.LZ[r * ZS + b - 1];
+    }
+    d4 acc[4];
+    gemm1_mm<XP, 4>(XJ, xr, W + b * PM, lr, lk, acc, 0);
+    const double sr = Nr[b * 64 + rl];
+    const double *nc = Nc + b * 64;
+    const double lam = tab.lam[b];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int cl = 16 * cb + lk + 4 * v;
+        constexpr double R2MIN = KIND == 1 ? 1e-300 : 0.0;
+        const double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), R2MIN);
+        double zc = 0.0, lzc = 0.0;
+        if (b > 0) {
+          zc = Zc[(b - 1) * 64 + cl];
+          if (KIND == 0) lzc = LZc[(b - 1) * 64 + cl];
+        }
+        kf[cb][v] += kval_mm<KIND>(b, r2, lam, zr, zc, lzr, lzc, E);
+        MM_PAIR_FENCE(cb, v);
+      }
+  }
+  if (!rok) return;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int64_t c = C0 + 16 * cb + lk + 4 * v;
+      if (c < C.n) out[r + c * ld] = kf[cb][v];
+    }
+}
+
 // The assembly's second part as a persistent work queue (ACE_ASM_PERSIST):
 // one workgroup per launch slot takes tiles of part 2 from a device counter
 // (its strictly lower tiles; the diagonal ones run as a plain grid first)
@@ -1525,6 +1646,36 @@ hipError_t launch_assembly_persist(int kind, int PM, PairSide S, int64_t npad, i
     return asm_mm_persist_pm<P>(kind, S, npad, B, ZS, tab, sig, out, ld, st, queue, reserve, \
                                 slots, fill > 0);                                            \
   }
+    ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
+    ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
+#undef ACE_CASE
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int PM>
+static hipError_t cross_mm_pm(int kind, PairSide R, PairSide C, int B, int ZS, TabView tab, int b0,
+                              int b1, double *out, int64_t ld, hipStream_t st) {
+  if (R.n <= 0 || C.n <= 0 || b1 <= b0) return hipSuccess;
+  const size_t lds = (size_t)mm_layout(PM, B, kind == 0 ? 0 : 1, false).total * sizeof(double);
+  const void *f = kind == 0 ? (const void *)k_cross_mm<PM, 0> : (const void *)k_cross_mm<PM, 1>;
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  const dim3 grid((unsigned)((C.n + AT - 1) / AT), (unsigned)((R.n + AT - 1) / AT));
+  if (kind == 0)
+    hipLaunchKernelGGL((k_cross_mm<PM, 0>), grid, dim3(256), lds, st, R, C, B, ZS, tab, b0, b1, out, ld);
+  else
+    hipLaunchKernelGGL((k_cross_mm<PM, 1>), grid, dim3(256), lds, st, R, C, B, ZS, tab, b0, b1, out, ld);
+  return hipGetLastError();
+}
+
+hipError_t launch_cross_mm(int kind, int PM, PairSide R, PairSide C, int B, int ZS, TabView tab,
+                           int b0, int b1, double *out, int64_t ld, hipStream_t st) {
+  switch (PM) {
+#define ACE_CASE(P) \
+  case P: return cross_mm_pm<P>(kind, R, C, B, ZS, tab, b0, b1, out, ld, st);
     ACE_CASE(4) ACE_CASE(8) ACE_CASE(12) ACE_CASE(16) ACE_CASE(20) ACE_CASE(24)
     ACE_CASE(32) ACE_CASE(48) ACE_CASE(64)
 #undef ACE_CASE

@@ -98,13 +98,20 @@ void nck(ace_ctx *ctx, ncclResult_t e, const char *what) {
   throw Fail{ACE_ERR_HIP};
 }
 
-// Host-callback collectives: stage through host buffers, every copy
-// stream-ordered on `st` and drained (bounded) before the host touches it.
+// Host-callback collectives: stage through pinned host buffers owned by the
+// model (a timed-out copy can never land in freed memory), every copy
+// stream-ordered on `st` with the stream drained (bounded) before it is
+// queued and after it, before the host touches the buffer.
+struct HostStage {
+  PinnedBuf a, b;
+};
 void d2h(ace_ctx *ctx, void *h, const void *d, size_t bytes, hipStream_t st) {
+  sync_stream(ctx, st, "stage");
   ck(ctx, hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, st), "stage");
   sync_stream(ctx, st, "stage");
 }
 void h2d(ace_ctx *ctx, void *d, const void *h, size_t bytes, hipStream_t st) {
+  sync_stream(ctx, st, "unstage");
   ck(ctx, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st), "unstage");
   sync_stream(ctx, st, "unstage");
 }
@@ -114,28 +121,29 @@ void hck(ace_ctx *ctx, int rc, const char *what) {
   throw Fail{ACE_ERR_HIP};
 }
 
-void host_bcast(ace_ctx *ctx, const ace_comm_ops &o, double *dbuf, size_t count, int root,
-                hipStream_t st) {
-  std::vector<double> h(count);
-  d2h(ctx, h.data(), dbuf, count * sizeof(double), st);
-  hck(ctx, o.broadcast(o.user, h.data(), (int64_t)count, root), "broadcast");
-  h2d(ctx, dbuf, h.data(), count * sizeof(double), st);
+void host_bcast(ace_ctx *ctx, const ace_comm_ops &o, HostStage &hs, double *dbuf, size_t count,
+                int root, hipStream_t st) {
+  double *h = hs.a.ensure(ctx, count);
+  d2h(ctx, h, dbuf, count * sizeof(double), st);
+  hck(ctx, o.broadcast(o.user, h, (int64_t)count, root), "broadcast");
+  h2d(ctx, dbuf, h, count * sizeof(double), st);
 }
 
-void host_allgather(ace_ctx *ctx, const ace_comm_ops &o, const double *dsend, double *drecv,
-                    size_t count, int world, hipStream_t st) {
-  std::vector<double> hs(count), hr(count * (size_t)world);
-  d2h(ctx, hs.data(), dsend, count * sizeof(double), st);
-  hck(ctx, o.allgather(o.user, hs.data(), hr.data(), (int64_t)count), "allgather");
-  h2d(ctx, drecv, hr.data(), hr.size() * sizeof(double), st);
+void host_allgather(ace_ctx *ctx, const ace_comm_ops &o, HostStage &hs, const double *dsend,
+                    double *drecv, size_t count, int world, hipStream_t st) {
+  double *s = hs.a.ensure(ctx, count);
+  double *r = hs.b.ensure(ctx, count * (size_t)world);
+  d2h(ctx, s, dsend, count * sizeof(double), st);
+  hck(ctx, o.allgather(o.user, s, r, (int64_t)count), "allgather");
+  h2d(ctx, drecv, r, count * (size_t)world * sizeof(double), st);
 }
 
-void host_allreduce(ace_ctx *ctx, const ace_comm_ops &o, double *dbuf, size_t count, int op,
-                    hipStream_t st) {
-  std::vector<double> h(count);
-  d2h(ctx, h.data(), dbuf, count * sizeof(double), st);
-  hck(ctx, o.allreduce(o.user, h.data(), (int64_t)count, op), "allreduce");
-  h2d(ctx, dbuf, h.data(), count * sizeof(double), st);
+void host_allreduce(ace_ctx *ctx, const ace_comm_ops &o, HostStage &hs, double *dbuf,
+                    size_t count, int op, hipStream_t st) {
+  double *h = hs.a.ensure(ctx, count);
+  d2h(ctx, h, dbuf, count * sizeof(double), st);
+  hck(ctx, o.allreduce(o.user, h, (int64_t)count, op), "allreduce");
+  h2d(ctx, dbuf, h, count * sizeof(double), st);
 }
 
 // ------------------------------------------------------------------ rank
@@ -170,6 +178,7 @@ struct ShardModel {
   bool sim = true;    // every rank simulated in this process (device copies)
   bool host = false;  // host-callback collectives (ace_comm_ops)
   ace_comm_ops ops{};
+  HostStage stage;  // pinned staging of the host-callback collectives
   ncclComm_t comm = nullptr;
   std::vector<std::unique_ptr<RankState>> ranks;  // 1 (RCCL) or G (simulated)
   DBuf vote;                                       // shard_any: one double
@@ -320,8 +329,8 @@ void exchange(ShardModel &m, int k, hipStream_t st) {
   auto own = [&](RankState &R) { return R.recv.d() + (size_t)R.r * nrow; };
   if (m.host) {
     RankState &R = *m.ranks[0];
-    host_bcast(ctx, m.ops, R.low.d(), nlow, root, st);
-    if (nrow > 0) host_allgather(ctx, m.ops, own(R), R.recv.d(), nrow, m.G, st);
+    host_bcast(ctx, m.ops, m.stage, R.low.d(), nlow, root, st);
+    if (nrow > 0) host_allgather(ctx, m.ops, m.stage, own(R), R.recv.d(), nrow, m.G, st);
     return;
   }
   if (!m.sim) {
@@ -356,7 +365,7 @@ void allreduce(ShardModel &m, int which, int64_t count, hipStream_t st) {
   if (m.G == 1) return;  // one rank: the identity
   auto buf = [&](RankState &R) { return which == 0 ? R.augvec.d() : R.red.d(); };
   if (m.host) {
-    host_allreduce(ctx, m.ops, buf(*m.ranks[0]), (size_t)count, 0, st);
+    host_allreduce(ctx, m.ops, m.stage, buf(*m.ranks[0]), (size_t)count, 0, st);
     return;
   }
   if (!m.sim) {
@@ -817,7 +826,7 @@ void shard_get_inverse(ShardModel *m, double *inv) {
                              hipMemcpyDeviceToDevice, st),
          "gather local columns");
   } else if (m->host) {
-    host_allgather(ctx, m->ops, m->ranks[0]->A[0].d(), gath.d(), (size_t)slot, m->G, st);
+    host_allgather(ctx, m->ops, m->stage, m->ranks[0]->A[0].d(), gath.d(), (size_t)slot, m->G, st);
   } else {
     nck(ctx, rccl().AllGather(m->ranks[0]->A[0].p, gath.p, (size_t)slot, ncclDouble, m->comm, st),
         "ncclAllGather (inverse)");
@@ -887,7 +896,7 @@ int shard_rank_of(const ShardModel *m, int j) { return m->ranks[(size_t)j]->r; }
 void shard_allreduce_sum(ShardModel *m, double *buf, int64_t count) {
   if (m->sim || m->G == 1 || count <= 0) return;
   if (m->host) {
-    host_allreduce(m->ctx, m->ops, buf, (size_t)count, 0, m->ctx->stream);
+    host_allreduce(m->ctx, m->ops, m->stage, buf, (size_t)count, 0, m->ctx->stream);
     return;
   }
   nck(m->ctx, rccl().AllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, m->comm,

@@ -126,6 +126,195 @@ __device__ __forceinline__ void pivot_sweep(double (&v)[SUB / NW], PivotLds<NW> 
   __syncthreads();
 }
 
+// ---------------------------------------------------------------- blocked pivot
+// The same 64x64 sweep as pivot_sweep<4> (same register layout in and out,
+// pivots into pv[]), blocked by 16 (ACE_PIVOT_BLK=1, default): the sweep
+// operator composes, so sweeping pivots 0..63 one by one equals four block
+// sweeps of the 16x16 diagonal blocks, each
+//   M_ss <- S = -D^-1 (D = M_ss),  M_sc <- D^-1 M_sc = -S M_sc,
+//   M_rc <- M_rc - M_rs D^-1 M_sc = M_rc + M_rs (S M_sc)   (r, c != s).
+// The 16 scalar pivots of M_ss run in ONE wave with no barrier and no LDS:
+// lane (r, g) = (lane & 15, lane >> 4) holds M(r, 4g .. 4g+3); pivot t's
+// row comes by a 64-bit DPP row_newbcast:t (lane t of every 16-lane row
+// holds row t's part of that row's columns) and its column by a
+// permlane16/32 swap pair that replicates row t/4 (the lanes holding
+// column t) into all four rows.  Every wave sweeps M_ss redundantly, so S
+// is in every wave's registers as the MFMA A operand (the k index of a
+// 16x16x4 step permuted to 4g + e, which needs no data movement); wave w !=
+// s then forms Un = S M_sw (4 MFMAs), writes M_sw = -Un (and its mirror
+// M_ws), and for c >= w, c != s updates M_cw += M_cs Un (4 MFMAs each, k
+// permuted to g + 4e so that Un's accumulator layout is the B operand as it
+// stands) and mirrors it: every off-diagonal block is formed once and
+// mirrored, every diagonal block from its lower triangle, so M stays exactly
+// symmetric as the scalar sweep keeps it.  Per 16 pivots ~35 VALU + 4
+// permlane + 5 DPP instructions per wave instead of 16 barriers and 64
+// columns of updates per row: the latency of the pivot chain's 64x64 sweep
+// (k_pivot 35 us alone, 93 us under the bulk update) is what this cuts.
+// M: the 64x64 matrix in LDS (pitch P, even, 16-B aligned rows).
+#ifndef ACE_PIVOT_BLK
+#define ACE_PIVOT_BLK 1
+#endif
+
+// broadcast lane T of every 16-lane row to the row (64-bit DPP)
+template <int T>
+__device__ __forceinline__ double row_bcast(double x) {
+  long v = __builtin_bit_cast(long, x);
+  long b = __builtin_amdgcn_update_dpp((long)0, v, 0x150 + T, 0xf, 0xf, false);  // v_mov_b64_dpp
+  return __builtin_bit_cast(double, b);
+}
+
+// replicate 16-lane row G of x into all four rows (v_permlane16/32_swap with
+// both operands x: swap16 -> {rows 0,0,2,2 ; rows 1,1,3,3}, swap32 ->
+// {rows lo,lo ; rows hi,hi})
+template <int G>
+__device__ __forceinline__ unsigned rep_row32(unsigned x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  const unsigned y = (G & 1) ? a[1] : a[0];
+  const auto b = __builtin_amdgcn_permlane32_swap(y, y, false, false);
+  return (G & 2) ? b[1] : b[0];
+}
+template <int G>
+__device__ __forceinline__ double rep_row(double x) {
+  const unsigned long v = __builtin_bit_cast(unsigned long, x);
+  const unsigned lo = rep_row32<G>((unsigned)v), hi = rep_row32<G>((unsigned)(v >> 32));
+  return __builtin_bit_cast(double, ((unsigned long)hi << 32) | lo);
+}
+
+// one scalar pivot t of the 16x16 block in the one-wave layout (see above)
+template <int T>
+__device__ __forceinline__ void blk_pivot(double (&x)[4], int r, int g, double &dout) {
+  constexpr int TG = T >> 2, TE = T & 3;
+  const double c = rep_row<TG>(x[TE]);  // M(r, t)
+  double rw[4];                          // M(t, 4g + e)
+#pragma unroll
+  for (int e = 0; e < 4; ++e) rw[e] = row_bcast<T>(x[e]);
+  const double d = row_bcast<T>(c);      // M(t, t)
+#if ACE_PIVOT_RCP
+  double rd = __builtin_amdgcn_rcp(d);
+  double re = fma(-d, rd, 1.0);
+  rd = fma(rd, re, rd);
+  re = fma(-d, rd, 1.0);
+  rd = fma(rd, re, rd);
+#else
+  const double rd = 1.0 / d;
+#endif
+  // branch-free (selects): row t gets M(t, j) / d, column t M(i, t) / d,
+  // the pivot -1/d, the rest M(i, j) - M(i, t) M(t, j) / d
+  const bool isrow = r == T;
+  const double cd = c * rd;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const bool jt = (4 * g + e) == T;  // lane-uniform per row: g is the row index
+    const double vn = fma(-(c * rw[e]), rd, x[e]);
+    const double vr = rw[e] * rd;
+    x[e] = jt ? (isrow ? -rd : cd) : (isrow ? vr : vn);
+  }
+  dout = d;
+}
+
+template <int P>
+__device__ __forceinline__ double2 lds_ld2(const double *p) {
+  if constexpr (P % 2 == 0) return *reinterpret_cast<const double2 *>(p);
+  else return double2{p[0], p[1]};
+}
+template <int P>
+__device__ __forceinline__ void lds_st2(double *p, double a, double b) {
+  if constexpr (P % 2 == 0) *reinterpret_cast<double2 *>(p) = double2{a, b};
+  else { p[0] = a; p[1] = b; }
+}
+
+template <int P>
+__device__ __forceinline__ void pivot_sweep_blk(double (&v)[SUB / 4], double (*M)[P], double *pv,
+                                                int tid) {
+  const int lane = tid & 63, w = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < SUB / 4; q += 2)
+    lds_st2<P>(&M[lane][16 * w + q], v[q], v[q + 1]);
+  __syncthreads();
+#pragma unroll 1
+  for (int s = 0; s < 4; ++s) {
+    const int s0 = 16 * s;
+    double x[4];
+    {
+      const double2 a = lds_ld2<P>(&M[s0 + r][s0 + 4 * g]);
+      const double2 b = lds_ld2<P>(&M[s0 + r][s0 + 4 * g + 2]);
+      x[0] = a.x; x[1] = a.y; x[2] = b.x; x[3] = b.y;
+    }
+    double dv[16];
+    blk_pivot<0>(x, r, g, dv[0]);   blk_pivot<1>(x, r, g, dv[1]);
+    blk_pivot<2>(x, r, g, dv[2]);   blk_pivot<3>(x, r, g, dv[3]);
+    blk_pivot<4>(x, r, g, dv[4]);   blk_pivot<5>(x, r, g, dv[5]);
+    blk_pivot<6>(x, r, g, dv[6]);   blk_pivot<7>(x, r, g, dv[7]);
+    blk_pivot<8>(x, r, g, dv[8]);   blk_pivot<9>(x, r, g, dv[9]);
+    blk_pivot<10>(x, r, g, dv[10]); blk_pivot<11>(x, r, g, dv[11]);
+    blk_pivot<12>(x, r, g, dv[12]); blk_pivot<13>(x, r, g, dv[13]);
+    blk_pivot<14>(x, r, g, dv[14]); blk_pivot<15>(x, r, g, dv[15]);
+    // operands of this sub-step's block update, read before anything is written
+    double bsw[4] = {0.0, 0.0, 0.0, 0.0};  // M_sw(4g + e, r) = M_ws(r, 4g + e)
+    double acs[4][4];                        // M_cs(r, g + 4e)
+    d4 ccw[4];                               // M_cw(g + 4jj, r)
+    const bool upd = w != s;
+    if (upd) {
+      const double2 a = lds_ld2<P>(&M[16 * w + r][s0 + 4 * g]);
+      const double2 b = lds_ld2<P>(&M[16 * w + r][s0 + 4 * g + 2]);
+      bsw[0] = a.x; bsw[1] = a.y; bsw[2] = b.x; bsw[3] = b.y;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c < w || c == s) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acs[c][e] = M[16 * c + r][s0 + g + 4 * e];
+          ccw[c][e] = M[16 * c + g + 4 * e][16 * w + r];
+        }
+      }
+    }
+    __syncthreads();
+    if (w == 0 && g == 0) {
+#pragma unroll
+      for (int t = 0; t < 16; ++t)
+        if (r == t) pv[s0 + t] = dv[t];
+    }
+    if (!upd) {  // the sweeping block itself: S
+      lds_st2<P>(&M[s0 + r][s0 + 4 * g], x[0], x[1]);
+      lds_st2<P>(&M[s0 + r][s0 + 4 * g + 2], x[2], x[3]);
+    } else {
+      d4 un = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) un = __builtin_amdgcn_mfma_f64_16x16x4f64(x[e], bsw[e], un, 0, 0, 0);
+      // un[jj] = Un(g + 4jj, r): M_sw = -Un and its mirror M_ws
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        M[s0 + g + 4 * jj][16 * w + r] = -un[jj];
+        M[16 * w + r][s0 + g + 4 * jj] = -un[jj];
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c < w || c == s) continue;
+        d4 acc = ccw[c];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(acs[c][e], un[e], acc, 0, 0, 0);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int a = g + 4 * jj;  // acc[jj] = M_cw(a, r)
+          if (c != w || a >= r) {
+            M[16 * c + a][16 * w + r] = acc[jj];
+            M[16 * w + r][16 * c + a] = acc[jj];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < SUB / 4; q += 2) {
+    const double2 a = lds_ld2<P>(&M[lane][16 * w + q]);
+    v[q] = a.x;
+    v[q + 1] = a.y;
+  }
+}
+
 // pivots (and the non-PD flag) and SW = -D^-1 out
 template <int NW>
 __device__ __forceinline__ void pivot_store(const double (&v)[SUB / NW], const PivotLds<NW> &L,
@@ -156,7 +345,12 @@ __global__ __launch_bounds__(64 * NW) void k_pivot(const double *__restrict__ S,
   double v[CW];
 #pragma unroll
   for (int q = 0; q < CW; ++q) v[q] = S[lane + (s * SUB + CW * w + q) * SUB];
-  pivot_sweep<NW>(v, L, tid);
+  if constexpr (ACE_PIVOT_BLK && NW == 4) {
+    __shared__ double M[SUB][SUB + 2];
+    pivot_sweep_blk<SUB + 2>(v, M, L.pv, tid);
+  } else {
+    pivot_sweep<NW>(v, L, tid);
+  }
   pivot_store<NW>(v, L, tid, SW, piv, p0, flag);
 }
 
@@ -248,7 +442,12 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
     double v[SUB / 4];
 #pragma unroll
     for (int q = 0; q < SUB / 4; ++q) v[q] = tile[lane][16 * w + q];
+#if ACE_PIVOT_BLK
+    __syncthreads();  // tile becomes the sweep's matrix
+    pivot_sweep_blk<65>(v, tile, L.pv, tid);
+#else
     pivot_sweep<4>(v, L, tid);
+#endif
     pivot_store<4>(v, L, tid, SW0, pivs, k0, flag);
   }
 }
@@ -480,7 +679,11 @@ __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int
   double v[SUB / 4];
 #pragma unroll
   for (int q = 0; q < SUB / 4; ++q) v[q] = sSW[16 * w + q][lane];
+#if ACE_PIVOT_BLK
+  pivot_sweep_blk<SLD>(v, sSt, PL.pv, tid);  // sSt is free (the update phase is done)
+#else
   pivot_sweep<4>(v, PL, tid);
+#endif
   pivot_store<4>(v, PL, tid, SWn, piv, k0 + (int64_t)(s + 1) * SUB, flag);
 }
 

@@ -26,8 +26,14 @@ Multi-GPU (torchrun, one process per GPU):
   * `--mode sharded`: the sharded leg alone (also at N = 1, where it runs the
     RCCL code path with one rank).
 
+`--gpus N` is the world size.  Without a launcher (WORLD_SIZE unset) and
+N > 1, bench.py starts `torch.distributed.run --nproc-per-node N` on itself as
+a child process and exits with its status; under a launcher, WORLD_SIZE must
+equal N (else exit 2).  `--launch-check` only rendezvouses and max-reduces.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
                        [--mode auto|replicas|sharded] [--shard-config C4]
+                       [--launch-check]
 """
 from __future__ import annotations
 
@@ -360,6 +366,44 @@ def run_sharded(dist, rank, world, ctx, steps, warmup, name=None):
     return out
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(a, argv):
+    """`--gpus N > 1` without a launcher: start N ranks with
+    torch.distributed.run as a CHILD process (never exec: nothing here has
+    touched HIP yet, but the child must own the GPUs, not this process).
+    The ranks inherit stdout, so rank 0's JSON line is the one line printed;
+    the child's exit status is returned."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL across processes)
+    proc = subprocess.Popen(cmd, env=env)
+    try:
+        return proc.wait()
+    except KeyboardInterrupt:
+        proc.terminate()
+        return proc.wait()
+
+
+def launch_check(dist, rank, world):
+    """--launch-check: the rendezvous and the max-over-ranks reduction only
+    (no GPU work): rank 0 prints one line with the world size it saw."""
+    got = _allreduce_max(dist, float(rank))
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "max_rank": int(got),
+                          "backend": dist.get_backend() if dist is not None else None}), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -374,9 +418,24 @@ def main():
     ap.add_argument("--no-r6", action="store_true", help="skip the unchanged-R6 drop-in leg")
     ap.add_argument("--no-profile", action="store_true",
                     help="diagnostic: no per-launch HIP events (no roofline / phase times)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="only rendezvous and max-reduce over the ranks (launcher test)")
     a = ap.parse_args()
 
+    # --gpus N is the world size: a bare `bench.py --gpus N` launches N ranks
+    # itself; under a launcher the two must agree
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(self_launch(a, sys.argv[1:]))
+    if env_world is not None and int(env_world) != a.gpus:
+        sys.stderr.write(f"bench: --gpus {a.gpus} but WORLD_SIZE={env_world} "
+                         "(the launcher's rank count must equal --gpus)\n")
+        sys.exit(2)
+
     dist, rank, world, local = _dist_init()
+    if a.launch_check:
+        launch_check(dist, rank, world)
+        return
     import additivecausalexpansion_amd as ace
     from additivecausalexpansion_amd.synthetic import CONFIGS, make_problem
     ctx = ace.Context(local)

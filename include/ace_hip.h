@@ -49,7 +49,12 @@ enum ace_status {
   ACE_ERR_INTERRUPTED = 6, /* the interrupt poll asked to stop                  */
   ACE_ERR_TIMEOUT = 7      /* device work did not drain within ACE_SYNC_TIMEOUT
                               seconds (default 600): a stalled queue or a hung
-                              collective; ace_last_error names the busy streams */
+                              collective; ace_last_error names the busy streams.
+                              The context is then failed: later calls on it
+                              return ACE_ERR_TIMEOUT at once (destroy it), and
+                              host buffers passed to the timed-out call must
+                              not be freed or reused (a copy queued before the
+                              deadline may still land in them)            */
 };
 
 typedef struct ace_ctx ace_ctx;

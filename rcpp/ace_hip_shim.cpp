@@ -335,21 +335,10 @@ List kernmat_Matern32_symmetric_cpp(NumericMatrix X, SEXP Z, NumericVector param
 // consumer uses only sum(log(eigenval)) (src/kernel_SE_cpp.cpp:240,
 // src/kernel_Matern_cpp.cpp:463, src/stats_cpp.cpp:29), which is log det A
 // for both, bit for bit as before.  A caller reading the values themselves
-// is told: attr(x, "ace_kind") is "pivots", and the first call in a session
-// emits a one-time R warning saying so (options(ace.quiet_pivots = TRUE)
-// silences it).
-static void mark_pivots(NumericVector &ev) {
-  ev.attr("ace_kind") = "pivots";
-  static bool told = false;
-  if (told) return;
-  told = true;
-  Function getopt("getOption");
-  const SEXP quiet = getopt("ace.quiet_pivots", false);
-  if (!Rf_asLogical(quiet))
-    Rf_warning("ace (MI355X engine): invkernel_cpp()$eigenval holds the elimination pivots of "
-               "the SPD inverse (attr \"ace_kind\" = \"pivots\"), not eigenvalues; "
-               "sum(log(.)) = log det A as in the reference.  This warning is shown once.");
-}
+// is told by attr(x, "ace_kind") = "pivots" only -- no warning: the
+// package's own R code is the caller, and a warning under options(warn = 2)
+// would longjmp out of the export past C++ destructors.
+static void mark_pivots(NumericVector &ev) { ev.attr("ace_kind") = "pivots"; }
 
 // [[Rcpp::export]]
 List invkernel_cpp(SEXP pdmat, double sigma) {
