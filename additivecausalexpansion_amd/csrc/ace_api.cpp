@@ -111,22 +111,15 @@ int ace_create(int device, ace_ctx **out) {
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) c->nstreams = 1;
   if (e == hipSuccess && nstr >= 2) {
-    // the lookahead panel chain is latency-bound: give it the highest priority
-    // so its workgroups take the first free CU slots next to the update kernel
-    // (ACE_SIDE_PRIO=0: the least priority, A/B switch; ACE_SIDE2_PRIO=0: the
-    // second side stream only; =2: the main stream's (default) priority.
-    // The range on the box: least 1, greatest -1, default 0)
+    // the lookahead streams are latency-bound: the highest priority, so their
+    // workgroups take the first free CU slots next to the update kernel
+    // (the range on the box: least 1, greatest -1, default 0)
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-    auto prio = [&](const char *var) {
-      const char *v = getenv(var);
-      return (v && atoi(v) == 0) ? lo : (v && atoi(v) == 2) ? 0 : hi;
-    };
-    const int p1 = prio("ACE_SIDE_PRIO"), p2 = p1 == lo ? lo : prio("ACE_SIDE2_PRIO");
-    e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, p1);
+    e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi);
     if (e == hipSuccess) c->nstreams = 2;
     if (e == hipSuccess && nstr >= 3) {
-      e = hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, p2);
+      e = hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, hi);
       if (e == hipSuccess) c->nstreams = 3;
     }
   }

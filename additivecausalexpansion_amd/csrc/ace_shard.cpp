@@ -176,6 +176,12 @@ struct ShardModel {
   int64_t n = 0, npad = 0, naug = 0, ntr = 0;
   int G = 1, rank = 0;
   bool sim = true;    // every rank simulated in this process (device copies)
+  // timing-only proxy (-DACE_DIAG_SHARD_PROXY builds, unique_id NULL): rank
+  // `rank` of `world` alone, scheduled as an RCCL rank (lookahead on the
+  // side streams), every collective replaced by device copies of the bytes
+  // that rank would receive; results wrong, per-rank time right
+  bool proxy = false;
+  DBuf proxy_buf;  // the broadcast's landing buffer
   bool host = false;  // host-callback collectives (ace_comm_ops)
   ace_comm_ops ops{};
   HostStage stage;  // pinned staging of the host-callback collectives
@@ -333,6 +339,21 @@ void exchange(ShardModel &m, int k, hipStream_t st) {
     if (nrow > 0) host_allgather(ctx, m.ops, m.stage, own(R), R.recv.d(), nrow, m.G, st);
     return;
   }
+  if (m.proxy) {  // the bytes this rank receives, as device copies
+    RankState &R = *m.ranks[0];
+    if (R.r != root) {
+      alloc(ctx, m.proxy_buf, nlow * sizeof(double), "alloc proxy");
+      ck(ctx, hipMemcpyAsync(m.proxy_buf.p, R.low.p, nlow * sizeof(double), hipMemcpyDeviceToDevice, st),
+         "proxy broadcast");
+    }
+    if (nrow > 0)
+      for (int q = 0; q < m.G; ++q)
+        if (q != R.r)
+          ck(ctx, hipMemcpyAsync(R.recv.d() + (size_t)q * nrow, own(R), nrow * sizeof(double),
+                                 hipMemcpyDeviceToDevice, st),
+             "proxy all-gather");
+    return;
+  }
   if (!m.sim) {
     RankState &R = *m.ranks[0];
     nck(ctx, rccl().GroupStart(), "ncclGroupStart");
@@ -366,6 +387,13 @@ void allreduce(ShardModel &m, int which, int64_t count, hipStream_t st) {
   auto buf = [&](RankState &R) { return which == 0 ? R.augvec.d() : R.red.d(); };
   if (m.host) {
     host_allreduce(ctx, m.ops, m.stage, buf(*m.ranks[0]), (size_t)count, 0, st);
+    return;
+  }
+  if (m.proxy) {  // a same-size device copy in place of the ring all-reduce
+    double *b = buf(*m.ranks[0]);
+    alloc(ctx, m.proxy_buf, std::max(m.proxy_buf.bytes, (size_t)count * sizeof(double)), "alloc proxy");
+    ck(ctx, hipMemcpyAsync(m.proxy_buf.p, b, (size_t)count * sizeof(double), hipMemcpyDeviceToDevice, st),
+       "proxy all-reduce");
     return;
   }
   if (!m.sim) {
@@ -601,8 +629,12 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
   m->host = ops != nullptr;
   if (ops) m->ops = *ops;
   m->sim = id == nullptr && !m->host;
+#ifdef ACE_DIAG_SHARD_PROXY
+  m->proxy = m->sim && world > 1;
+  if (m->proxy) m->sim = false;
+#endif
   const int64_t naug = m->naug, npad = m->npad;
-  if (!m->sim && !m->host) {
+  if (!m->sim && !m->host && !m->proxy) {
     if (!rccl().ok) {
       ctx->err = rccl().err;
       throw Fail{ACE_ERR_HIP};
@@ -637,6 +669,10 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
     alloc(ctx, R->low, (size_t)(naug * NB) * sizeof(double), "alloc exchange");
     alloc(ctx, R->recv, (size_t)world * std::max(1, maxslots) * NB * NB * sizeof(double),
           "alloc exchange");
+    if (m->proxy) {  // what the proxy never receives is zeros, not stale memory
+      ck(ctx, hipMemsetAsync(R->low.p, 0, R->low.bytes, ctx->stream), "memset exchange");
+      ck(ctx, hipMemsetAsync(R->recv.p, 0, R->recv.bytes, ctx->stream), "memset exchange");
+    }
     R->hupd = own_tiles(naug / UT, UT, world, R->r);
     if (const int S = update_order_block(); S > 0) R->hupd = xcd_update_order(R->hupd, S);
     R->nupd = (int64_t)R->hupd.size();
@@ -820,7 +856,7 @@ void shard_get_inverse(ShardModel *m, double *inv) {
   const int64_t slot = naug * ncols_local(naug, m->G, 0);  // doubles per rank
   DBuf gath, out;
   alloc(ctx, gath, (size_t)(slot * m->G) * sizeof(double), "alloc gathered inverse");
-  if (m->sim) {
+  if (m->sim || m->proxy) {
     for (auto &R : m->ranks)
       ck(ctx, hipMemcpyAsync(gath.d() + (size_t)R->r * slot, R->A[0].p, (size_t)slot * sizeof(double),
                              hipMemcpyDeviceToDevice, st),
@@ -866,7 +902,7 @@ void shard_collect_timing(ShardModel *m, double *t_ms, int64_t *t_launch, double
 // leave the others blocked in the next sweep's collectives.  Simulated
 // groups share the process's poll, so the local value is already common.
 int shard_any(ShardModel *m, int local) {
-  if (m->sim || m->G == 1) return local;
+  if (m->sim || m->proxy || m->G == 1) return local;
   ace_ctx *ctx = m->ctx;
   hipStream_t st = ctx->stream;
   if (m->host) {
@@ -894,7 +930,7 @@ int shard_rank_of(const ShardModel *m, int j) { return m->ranks[(size_t)j]->r; }
 // Sum over ranks of `count` doubles (in place, device).  Simulated groups
 // sum their local partials themselves, so only RCCL has work to do.
 void shard_allreduce_sum(ShardModel *m, double *buf, int64_t count) {
-  if (m->sim || m->G == 1 || count <= 0) return;
+  if (m->sim || m->proxy || m->G == 1 || count <= 0) return;
   if (m->host) {
     host_allreduce(m->ctx, m->ops, m->stage, buf, (size_t)count, 0, m->ctx->stream);
     return;

@@ -180,9 +180,10 @@ __device__ __forceinline__ double rep_row(double x) {
   return __builtin_bit_cast(double, ((unsigned long)hi << 32) | lo);
 }
 
-// one scalar pivot t of the 16x16 block in the one-wave layout (see above)
+// one scalar pivot t of the 16x16 block in the one-wave layout (see above);
+// the pivot d goes to pv[T] from one lane (rec: wave 0)
 template <int T>
-__device__ __forceinline__ void blk_pivot(double (&x)[4], int r, int g, double &dout) {
+__device__ __forceinline__ void blk_pivot(double (&x)[4], int r, int g, double *pv, bool rec) {
   constexpr int TG = T >> 2, TE = T & 3;
   const double c = rep_row<TG>(x[TE]);  // M(r, t)
   double rw[4];                          // M(t, 4g + e)
@@ -209,7 +210,7 @@ __device__ __forceinline__ void blk_pivot(double (&x)[4], int r, int g, double &
     const double vr = rw[e] * rd;
     x[e] = jt ? (isrow ? -rd : cd) : (isrow ? vr : vn);
   }
-  dout = d;
+  if (rec && r == T && g == 0) pv[T] = d;
 }
 
 template <int P>
@@ -241,48 +242,52 @@ __device__ __forceinline__ void pivot_sweep_blk(double (&v)[SUB / 4], double (*M
       const double2 b = lds_ld2<P>(&M[s0 + r][s0 + 4 * g + 2]);
       x[0] = a.x; x[1] = a.y; x[2] = b.x; x[3] = b.y;
     }
-    double dv[16];
-    blk_pivot<0>(x, r, g, dv[0]);   blk_pivot<1>(x, r, g, dv[1]);
-    blk_pivot<2>(x, r, g, dv[2]);   blk_pivot<3>(x, r, g, dv[3]);
-    blk_pivot<4>(x, r, g, dv[4]);   blk_pivot<5>(x, r, g, dv[5]);
-    blk_pivot<6>(x, r, g, dv[6]);   blk_pivot<7>(x, r, g, dv[7]);
-    blk_pivot<8>(x, r, g, dv[8]);   blk_pivot<9>(x, r, g, dv[9]);
-    blk_pivot<10>(x, r, g, dv[10]); blk_pivot<11>(x, r, g, dv[11]);
-    blk_pivot<12>(x, r, g, dv[12]); blk_pivot<13>(x, r, g, dv[13]);
-    blk_pivot<14>(x, r, g, dv[14]); blk_pivot<15>(x, r, g, dv[15]);
-    // operands of this sub-step's block update, read before anything is written
-    double bsw[4] = {0.0, 0.0, 0.0, 0.0};  // M_sw(4g + e, r) = M_ws(r, 4g + e)
-    double acs[4][4];                        // M_cs(r, g + 4e)
-    d4 ccw[4];                               // M_cw(g + 4jj, r)
+    {
+      double *const p = pv + s0;
+      const bool rec = w == 0;
+      blk_pivot<0>(x, r, g, p, rec);   blk_pivot<1>(x, r, g, p, rec);
+      blk_pivot<2>(x, r, g, p, rec);   blk_pivot<3>(x, r, g, p, rec);
+      blk_pivot<4>(x, r, g, p, rec);   blk_pivot<5>(x, r, g, p, rec);
+      blk_pivot<6>(x, r, g, p, rec);   blk_pivot<7>(x, r, g, p, rec);
+      blk_pivot<8>(x, r, g, p, rec);   blk_pivot<9>(x, r, g, p, rec);
+      blk_pivot<10>(x, r, g, p, rec);  blk_pivot<11>(x, r, g, p, rec);
+      blk_pivot<12>(x, r, g, p, rec);  blk_pivot<13>(x, r, g, p, rec);
+      blk_pivot<14>(x, r, g, p, rec);  blk_pivot<15>(x, r, g, p, rec);
+    }
+    // this sub-step's block update, computed from the old values before the
+    // barrier (reads), stored after it (writes of blocks other waves read)
     const bool upd = w != s;
+    d4 un = d4{0.0, 0.0, 0.0, 0.0};  // Un(g + 4jj, r) = (S M_sw)(g + 4jj, r)
+    d4 res[4];                        // M_cw(g + 4jj, r) + (M_cs Un)(g + 4jj, r)
     if (upd) {
-      const double2 a = lds_ld2<P>(&M[16 * w + r][s0 + 4 * g]);
-      const double2 b = lds_ld2<P>(&M[16 * w + r][s0 + 4 * g + 2]);
-      bsw[0] = a.x; bsw[1] = a.y; bsw[2] = b.x; bsw[3] = b.y;
+      {
+        // B operand: M_sw(4g + e, r) = M_ws(r, 4g + e)
+        const double2 a = lds_ld2<P>(&M[16 * w + r][s0 + 4 * g]);
+        const double2 b = lds_ld2<P>(&M[16 * w + r][s0 + 4 * g + 2]);
+        un = __builtin_amdgcn_mfma_f64_16x16x4f64(x[0], a.x, un, 0, 0, 0);
+        un = __builtin_amdgcn_mfma_f64_16x16x4f64(x[1], a.y, un, 0, 0, 0);
+        un = __builtin_amdgcn_mfma_f64_16x16x4f64(x[2], b.x, un, 0, 0, 0);
+        un = __builtin_amdgcn_mfma_f64_16x16x4f64(x[3], b.y, un, 0, 0, 0);
+      }
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         if (c < w || c == s) continue;
+        d4 acc;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acs[c][e] = M[16 * c + r][s0 + g + 4 * e];
-          ccw[c][e] = M[16 * c + g + 4 * e][16 * w + r];
-        }
+        for (int e = 0; e < 4; ++e) acc[e] = M[16 * c + g + 4 * e][16 * w + r];  // C: M_cw
+#pragma unroll
+        for (int e = 0; e < 4; ++e)  // A: M_cs(r, g + 4e); B: Un's layout as it stands
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(M[16 * c + r][s0 + g + 4 * e], un[e], acc, 0,
+                                                     0, 0);
+        res[c] = acc;
       }
     }
     __syncthreads();
-    if (w == 0 && g == 0) {
-#pragma unroll
-      for (int t = 0; t < 16; ++t)
-        if (r == t) pv[s0 + t] = dv[t];
-    }
     if (!upd) {  // the sweeping block itself: S
       lds_st2<P>(&M[s0 + r][s0 + 4 * g], x[0], x[1]);
       lds_st2<P>(&M[s0 + r][s0 + 4 * g + 2], x[2], x[3]);
     } else {
-      d4 un = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) un = __builtin_amdgcn_mfma_f64_16x16x4f64(x[e], bsw[e], un, 0, 0, 0);
-      // un[jj] = Un(g + 4jj, r): M_sw = -Un and its mirror M_ws
+      // M_sw = -Un and its mirror M_ws
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         M[s0 + g + 4 * jj][16 * w + r] = -un[jj];
@@ -291,16 +296,12 @@ __device__ __forceinline__ void pivot_sweep_blk(double (&v)[SUB / 4], double (*M
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         if (c < w || c == s) continue;
-        d4 acc = ccw[c];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(acs[c][e], un[e], acc, 0, 0, 0);
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          const int a = g + 4 * jj;  // acc[jj] = M_cw(a, r)
+          const int a = g + 4 * jj;  // res[c][jj] = M_cw(a, r)
           if (c != w || a >= r) {
-            M[16 * c + a][16 * w + r] = acc[jj];
-            M[16 * w + r][16 * c + a] = acc[jj];
+            M[16 * c + a][16 * w + r] = res[c][jj];
+            M[16 * w + r][16 * c + a] = res[c][jj];
           }
         }
       }
@@ -317,14 +318,14 @@ __device__ __forceinline__ void pivot_sweep_blk(double (&v)[SUB / 4], double (*M
 
 // pivots (and the non-PD flag) and SW = -D^-1 out
 template <int NW>
-__device__ __forceinline__ void pivot_store(const double (&v)[SUB / NW], const PivotLds<NW> &L,
+__device__ __forceinline__ void pivot_store(const double (&v)[SUB / NW], const double *pv,
                                             int tid, double *__restrict__ SW,
                                             double *__restrict__ piv, int64_t p0,
                                             int *__restrict__ flag) {
   constexpr int CW = SUB / NW;
   const int lane = tid & 63, w = tid >> 6;
   if (tid < SUB) {
-    const double d = L.pv[tid];
+    const double d = pv[tid];
     piv[p0 + tid] = d;
     if (!(d > 0.0) || !isfinite(d)) *flag = 1;
   }
@@ -351,32 +352,12 @@ __global__ __launch_bounds__(64 * NW) void k_pivot(const double *__restrict__ S,
   } else {
     pivot_sweep<NW>(v, L, tid);
   }
-  pivot_store<NW>(v, L, tid, SW, piv, p0, flag);
-}
-
-// waves of the pivot workgroup: 4, 8 or 16 (ACE_PIVOT_WAVES, A/B switch)
-static int pivot_waves() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("ACE_PIVOT_WAVES");
-    v = e ? atoi(e) : 4;
-    if (v != 4 && v != 8 && v != 16) v = 4;
-  }
-  return v;
+  pivot_store<NW>(v, L.pv, tid, SW, piv, p0, flag);
 }
 
 static void launch_pivot(const double *S, int s, double *SW, double *piv, int64_t p0, int *flag,
                          hipStream_t st) {
-  switch (pivot_waves()) {
-    case 16:
-      hipLaunchKernelGGL(k_pivot<16>, dim3(1), dim3(1024), 0, st, S, s, SW, piv, p0, flag);
-      break;
-    case 8:
-      hipLaunchKernelGGL(k_pivot<8>, dim3(1), dim3(512), 0, st, S, s, SW, piv, p0, flag);
-      break;
-    default:
-      hipLaunchKernelGGL(k_pivot<4>, dim3(1), dim3(256), 0, st, S, s, SW, piv, p0, flag);
-  }
+  hipLaunchKernelGGL(k_pivot<4>, dim3(1), dim3(256), 0, st, S, s, SW, piv, p0, flag);
 }
 
 // ---------------------------------------------------------------- gather
@@ -448,7 +429,7 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
 #else
     pivot_sweep<4>(v, L, tid);
 #endif
-    pivot_store<4>(v, L, tid, SW0, pivs, k0, flag);
+    pivot_store<4>(v, L.pv, tid, SW0, pivs, k0, flag);
   }
 }
 
@@ -684,7 +665,7 @@ __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int
 #else
   pivot_sweep<4>(v, PL, tid);
 #endif
-  pivot_store<4>(v, PL, tid, SWn, piv, k0 + (int64_t)(s + 1) * SUB, flag);
+  pivot_store<4>(v, PL.pv, tid, SWn, piv, k0 + (int64_t)(s + 1) * SUB, flag);
 }
 
 // ---------------------------------------------------------------- panel GEMM
@@ -1773,12 +1754,18 @@ __global__ __launch_bounds__(256) void k_update_x(double *__restrict__ A, int64_
 // k_update_x's 4-wave MFMA chain per panel and the accumulators kept across
 // panels: per element the same chain as k_update / k_update_multi, a quarter
 // of a 128-tile's work per workgroup.  go: the gather fused into the launch.
-__global__ __launch_bounds__(256) void k_update_q(double *__restrict__ A, int64_t ld, PanelSet ps,
+__global__ __launch_bounds__(256, 4) void k_update_q(double *__restrict__ A, int64_t ld, PanelSet ps,
                                                   int npan, int64_t ldp,
-                                                  const Tile *__restrict__ tiles, GatherOut go) {
+                                                  const Tile *__restrict__ tiles, GatherOut go,
+                                                  double *__restrict__ pivSW,
+                                                  double *__restrict__ piv,
+                                                  int *__restrict__ flag) {
   ACE_WGT(4, true);
-  __shared__ __attribute__((aligned(16))) double sW[2][BK][XL];
-  __shared__ __attribute__((aligned(16))) double sP[2][BK][XL];
+  // sW and sP in one buffer: the fused pivot below reuses it as its matrix
+  __shared__ __attribute__((aligned(16))) double sbuf[2][2][BK][XL];
+  static_assert(sizeof(sbuf) >= SUB * (SUB + 2) * sizeof(double), "pivot matrix fits the staging");
+  double (*sW)[BK][XL] = sbuf[0];
+  double (*sP)[BK][XL] = sbuf[1];
   const Tile tt = tiles[blockIdx.x >> 2];
   if (tt.I < 0) return;  // padding of the XCD order
   const int q = blockIdx.x & 3;
@@ -1858,6 +1845,36 @@ __global__ __launch_bounds__(256) void k_update_q(double *__restrict__ A, int64_
         if (go.k0 >= 0) gput(go, r, c + 4 * j, v);
       }
     }
+  // pivSW: this launch gathers a panel, and the quarter holding that panel's
+  // first 64 x 64 diagonal block D_0 also runs its sub-sweep (k_pivot's,
+  // into pivSW / piv / flag) -- the input is the lower values just stored,
+  // mirrored, i.e. exactly the S0 snapshot k_pivot would read: bit-identical,
+  // one head-path launch less per panel
+  if (pivSW && go.k0 >= 0 && R0 == go.k0 && C0 == go.k0) {
+    __shared__ double pv[SUB];
+    double(*M)[SUB + 2] = reinterpret_cast<double(*)[SUB + 2]>(&sbuf[0][0][0][0]);
+    // (the chunk loop ended with a barrier: the staging buffers are free)
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int ri = 0; ri < 2; ++ri) {
+        const int a = 32 * wr + 16 * ri + lr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = 32 * wc + 16 * ci + lk + 4 * j;
+          if (a >= c) {
+            M[a][c] = acc[ci][ri][j];
+            M[c][a] = acc[ci][ri][j];
+          }
+        }
+      }
+    __syncthreads();
+    double v[SUB / 4];
+#pragma unroll
+    for (int q = 0; q < SUB / 4; ++q) v[q] = M[lane][16 * wv + q];
+    pivot_sweep_blk<SUB + 2>(v, M, pv, tid);
+    pivot_store<4>(v, pv, tid, pivSW, piv, go.k0, flag);
+  }
 }
 
 // ---------------------------------------------------------------- sharded panel
@@ -2800,6 +2817,9 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
     const char *e = getenv("ACE_HEADQ");
     return !(e && atoi(e) == 0);
   }();
+  // panels k >= 1 are gathered by k_update_q launches, which sweep their D_0
+  // (the blocked pivot only: the same code as k_pivot's, bit-identical)
+  const bool fused_pivot = hq && ACE_PIVOT_BLK;
   auto qupd = [&](int npan, int kb, const Tile *tl, int64_t nt, GatherOut go, hipStream_t s_) {
     if (nt <= 0) return;
     if (!hq) {
@@ -2811,8 +2831,12 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
       ps.R[j] = j < npan ? b.W[slot(kb + j)] : nullptr;
       ps.C[j] = j < npan ? b.P[slot(kb + j)] : nullptr;
     }
+    // a launch that gathers a panel also sweeps its D_0 (k_update_q's fused
+    // pivot): that panel's chain then starts at sub-step 0's panel update
+    const bool fp = fused_pivot && go.k0 >= 0;
     hipLaunchKernelGGL(k_update_q, dim3((unsigned)(4 * nt)), dim3(256), 0, s_, b.A, b.ld, ps, npan,
-                       b.ld, tl, go);
+                       b.ld, tl, go, fp ? b.SW : nullptr, fp ? b.piv : nullptr,
+                       fp ? b.flag : nullptr);
   };
   // panel k's GEMM W_i = Pn_i W_kk over row tiles [r0, r1) (head) or all the
   // others (tail); the kernel itself skips the pivot block's rows
@@ -2823,9 +2847,9 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
                        b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, 1, 0, head ? r0 : 0,
                        head ? 1 << 30 : r0, head ? 1 << 30 : r1);
   };
-  auto chain = [&](int k, hipStream_t s_) {  // pivot + sub-steps of panel k (gathered)
+  auto chain = [&](int k, hipStream_t s_) {  // [pivot +] sub-steps of panel k (gathered)
     panel_chain(b.P[slot(k)], b.W[slot(k)], b.ld, (int64_t)k * NB, b.SW, b.S, b.piv, b.flag, 1, 0,
-                s_, false, nullptr, true);
+                s_, fused_pivot && k > 0, nullptr, true);
   };
   hipError_t e;
   if (!sy->ready_recorded) {

@@ -97,12 +97,27 @@ def _newest_first_last(files):
     return sorted(files, key=lambda f: [int(x) for x in re.findall(r"\d+", os.path.basename(f))])
 
 
-def pmc_traffic(kernel="k_update"):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/rNN_pmc_traffic.json, written by tools/pmc_traffic.py from two
-    separate rocprofv3 --pmc passes of this bench).  None if absent."""
+def _pmc_files(config):
+    """Committed PMC summaries (profiles/rNN_*pmc_traffic.json, oldest first)
+    recorded at `config` (records without the key are the C2 runs of earlier
+    rounds)."""
     import glob
-    files = _newest_first_last(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    out = []
+    for f in _newest_first_last(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json"))):
+        try:
+            if json.load(open(f)).get("config", "C2") == config:
+                out.append(f)
+        except (ValueError, OSError):
+            pass
+    return out
+
+
+def pmc_traffic(kernel="k_update", config="C2"):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    of THIS configuration (profiles/rNN_pmc_traffic.json, written by
+    tools/pmc_traffic.py from two separate rocprofv3 --pmc passes of this
+    bench).  None when no record of the configuration exists."""
+    files = _pmc_files(config)
     if not files:
         return None, None
     try:
@@ -114,7 +129,7 @@ def pmc_traffic(kernel="k_update"):
         return None, None
 
 
-def rocprof_bulk_avg():
+def rocprof_bulk_avg(config="C2"):
     """Average duration (ms) of the bulk update launch (k_update_multi; older
     summaries: k_update_pair) in the newest
     committed rocprofv3 kernel-trace summary (profiles/rNN_vMM_kernel_stats_split.csv,
@@ -122,6 +137,8 @@ def rocprof_bulk_avg():
     cross-check against this run's HIP-event average."""
     import csv
     import glob
+    if config != "C2":  # the committed summaries are of the C2 bench
+        return None, None
     files = _newest_first_last(glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats_split.csv")))
     if not files:
         return None, None
@@ -134,13 +151,12 @@ def rocprof_bulk_avg():
     return None, None
 
 
-def pair_hbm_gbs(asm_ms, grad_ms):
+def pair_hbm_gbs(asm_ms, grad_ms, config="C2"):
     """HBM GB/s of the fused assembly and gradient phases (SURVEY §8d asks for
     them beside their VALU/MFMA rates): PMC bytes per eval from the newest
     profiles/rNN_pmc_traffic.json (the assembly and gradient launches of
     each eval) over this run's phase times."""
-    import glob
-    files = _newest_first_last(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    files = _pmc_files(config)
     if not files:
         return None
     try:
@@ -331,12 +347,15 @@ def r6_leg(kernel, p, B, theta, std_y, ctx, y, X, Z, iters=5, warmup=2):
     return out
 
 
-def run_sharded(dist, rank, world, ctx, steps, warmup, name=None):
-    """One evaluation over all ranks (block-column-sharded model, RCCL)."""
+def run_sharded(dist, rank, world, ctx, steps, warmup, name=None, proxy=False):
+    """One evaluation over all ranks (block-column-sharded model, RCCL).
+    proxy: rank `rank` of `world` alone in this process with the
+    -DACE_DIAG_SHARD_PROXY library (tools/build_variant.sh): collectives are
+    same-size device copies, results wrong, the rank's per-step time right."""
     import additivecausalexpansion_amd as ace
     from additivecausalexpansion_amd.synthetic import make_problem
     label, n, p, B, kernel = shard_config(world, name)
-    uid = ace.comm_unique_id() if rank == 0 else None
+    uid = ace.comm_unique_id() if rank == 0 and not proxy else None
     if dist is not None:
         box = [uid]
         dist.broadcast_object_list(box, src=0)
@@ -418,6 +437,9 @@ def main():
     ap.add_argument("--no-r6", action="store_true", help="skip the unchanged-R6 drop-in leg")
     ap.add_argument("--no-profile", action="store_true",
                     help="diagnostic: no per-launch HIP events (no roofline / phase times)")
+    ap.add_argument("--proxy", type=str, default=None, metavar="R/G",
+                    help="diagnostic (--mode sharded, -DACE_DIAG_SHARD_PROXY library): time rank R "
+                         "of a G-rank sharded evaluation alone on this GPU")
     ap.add_argument("--launch-check", action="store_true",
                     help="only rendezvous and max-reduce over the ranks (launcher test)")
     a = ap.parse_args()
@@ -441,7 +463,14 @@ def main():
     ctx = ace.Context(local)
 
     if a.mode == "sharded":
-        sh = run_sharded(dist, rank, world, ctx, a.steps, a.warmup, a.shard_config)
+        if a.proxy:
+            os.environ["ACE_BENCH_DIAG"] = "1"  # the proxy's gradients are not finite
+            pr, pg = (int(x) for x in a.proxy.split("/"))
+            sh = run_sharded(None, pr, pg, ctx, a.steps, a.warmup, a.shard_config, proxy=True)
+            sh["proxy"] = {"rank": pr, "world": pg,
+                           "note": "one rank alone, collectives replaced by same-size device copies"}
+        else:
+            sh = run_sharded(dist, rank, world, ctx, a.steps, a.warmup, a.shard_config)
         if rank == 0:
             line = {"metric": METRIC, "value": sh["evals_per_s"], "unit": "evals/s",
                     "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -479,10 +508,10 @@ def main():
 
     line = None
     if rank == 0:
-        traffic, traffic_src = pmc_traffic("k_update_multi_bulk")
+        traffic, traffic_src = pmc_traffic("k_update_multi_bulk", a.config)
         if traffic is None:  # a summary from before the multi-panel kernel
-            traffic, traffic_src = pmc_traffic("k_update_pair_bulk")
-        rp_ms, rp_src = rocprof_bulk_avg()
+            traffic, traffic_src = pmc_traffic("k_update_pair_bulk", a.config)
+        rp_ms, rp_src = rocprof_bulk_avg(a.config)
         naug = -(-n // 256) * 256 + 128
         nt = naug // 128
         # sweep steps per bulk launch, from the launch count (steps / groups)
@@ -552,7 +581,7 @@ def main():
             "pair_kernels_tflops": {
                 "assembly": asm_work / (asm_ms * 1e-3) / 1e12 if asm_ms else None,
                 "gradient": grad_work / (grad_ms * 1e-3) / 1e12 if grad_ms else None},
-            "pair_kernels_hbm_gbs": pair_hbm_gbs(asm_ms / a.steps, grad_ms / a.steps),
+            "pair_kernels_hbm_gbs": pair_hbm_gbs(asm_ms / a.steps, grad_ms / a.steps, a.config),
             "last_stats": [float(stats[0]), float(stats[1])],
             "predict": pred,
             "r6_drop_in": r6,

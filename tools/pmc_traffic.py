@@ -63,9 +63,12 @@ def read(d, counter):
 
 def main():
     fdir, wdir = sys.argv[1], sys.argv[2]
+    # the bench configuration both passes ran (bench.py takes roofline.traffic
+    # only from a record of its own configuration)
+    config = sys.argv[3] if len(sys.argv) > 3 else "C2"
     fetch = read(fdir, "FETCH_SIZE")
     write = read(wdir, "WRITE_SIZE")
-    out = {"unit": "bytes per launch", "fetch_correction": 2.0, "kernels": {}}
+    out = {"unit": "bytes per launch", "fetch_correction": 2.0, "config": config, "kernels": {}}
     for k in list(KERNELS) + ["k_update_pair_bulk", "k_update_multi_bulk"]:
         if not fetch.get(k) or not write.get(k):
             continue
