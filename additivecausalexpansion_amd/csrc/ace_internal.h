@@ -269,7 +269,7 @@ struct ShardSweep {
   int64_t ld;         // naug
   int64_t npad;
   int G, r;
-  double *P[4], *W[4];  // naug x NB: Pn = -panel (all rows), W (own rows); slot k & 3
+  double *P[8], *W[8];  // naug x NB: Pn = -panel (all rows), W (own rows); slot k % (2 Z)
   double *SW;
   double *S[2];
   double *piv;        // npad pivots (every rank records all of them)
@@ -289,18 +289,13 @@ hipError_t shard_unpack_chain(const ShardSweep &b, int k, int buf, hipStream_t s
 hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t st);
 // every own tile except the cross of block kx (kx < 0: none)
 hipError_t shard_update_main(const ShardSweep &b, int k, int buf, int kx, hipStream_t st);
-// step k with panel slot `slot` on a tile list (skip rule kx as k_update);
-// kpack >= 0: the launch also writes the exchange buffers of step kpack
-// (what shard_pack(kpack) would copy; G > 1) and the rank's own rows of panel
-// kpack (slot kpack & 3) from the values it stores -- the list must then hold
-// every own tile with I or J in block kpack
-hipError_t shard_update_tiles(const ShardSweep &b, int k, int slot, int kx, const Tile *tiles,
-                              int64_t nt, hipStream_t st, int kpack = -1);
-// steps ka, ka + 1 in one launch (k_update_pair, panels in slots ka & 3 and
-// (ka + 1) & 3, operands swapped: R = Pn, C = W) on a tile list, skipping the
-// tiles with I or J in blocks [kx0, kx1); kpack as shard_update_tiles
-hipError_t shard_update_pair(const ShardSweep &b, int ka, int kx0, int kx1, const Tile *tiles,
-                             int64_t nt, hipStream_t st, int kpack = -1);
+// npan steps from block kb in one launch (k_update_multi<true>; one panel:
+// k_update), panels in slots (kb + j) % nslot, skipping blocks [kx0, kx1),
+// on a tile list; kpack >= 0: the launch also writes the exchange buffers of
+// step kpack (what shard_pack(kpack) would copy; G > 1) and the rank's own
+// rows of panel kpack (slot kpack % nslot)
+hipError_t shard_update_group(const ShardSweep &b, int kb, int npan, int nslot, int kx0, int kx1,
+                              const Tile *tiles, int64_t nt, hipStream_t st, int kpack = -1);
 
 // ---- small helpers -----------------------------------------------------------
 // AUG rows of columns j < n: row 0 = y (zeros if y is null), row 1 = 1

@@ -150,7 +150,7 @@ void host_allreduce(ace_ctx *ctx, const ace_comm_ops &o, HostStage &hs, double *
 struct RankState {
   int r = 0;
   DBuf A[2];  // A[1]: train_stats scratch (keeps A[0]'s inverse, Q6)
-  DBuf P[4], W[4], SW, S[2], piv, flag, low, recv;  // panel slots k & 3
+  DBuf P[8], W[8], SW, S[2], piv, flag, low, recv;  // panel slots k % (2 Z)
   DBuf tupd, tasm, tgrad;  // device tile lists
   int64_t nupd = 0, nasm = 0, nasm1 = 0, ngrad = 0, ndiag = 0;  // nasm1: first-part tiles
   std::vector<Tile> hupd;  // host copy (flop accounting)
@@ -160,10 +160,6 @@ struct RankState {
   // group g's pair cross, block 2 g first, then block 2 g + 1 minus block 2 g
   DBuf tx, tp;
   std::vector<int64_t> xoff, poff;
-  // per group g: the bulk order (pair_bulk_orders: own tiles XCD-dealt with
-  // each XCD's cheap / skipped tiles last), glen entries each (0: use tupd)
-  DBuf tgo;
-  int64_t glen = 0;
   DBuf y, tab, alpha, scal, gpart, gwork, red, sums, augvec;
   SideBufs side;
 };
@@ -175,6 +171,7 @@ struct ShardModel {
   Shape s{};
   int64_t n = 0, npad = 0, naug = 0, ntr = 0;
   int G = 1, rank = 0;
+  int Z = 2;          // sweep steps per bulk launch of the group schedule (sweep_group())
   bool sim = true;    // every rank simulated in this process (device copies)
   // timing-only proxy (-DACE_DIAG_SHARD_PROXY builds, unique_id NULL): rank
   // `rank` of `world` alone, scheduled as an RCCL rank (lookahead on the
@@ -228,7 +225,7 @@ ShardSweep sweep_view(const ShardModel &m, RankState &R, int which) {
   b.npad = m.npad;
   b.G = m.G;
   b.r = R.r;
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < 8; ++j) {
     b.P[j] = R.P[j].p ? R.P[j].d() : nullptr;
     b.W[j] = R.W[j].p ? R.W[j].d() : nullptr;
   }
@@ -259,28 +256,35 @@ double update_flops(const std::vector<Tile> &tl, int64_t naug, int64_t k0, int k
   return cnt * 2.0 * UT * UT * NB;
 }
 
-// GEMM flops of one k_update_pair launch (steps ka, ka + 1) on a tile list,
-// skipping the cross of blocks [kx0, kx1): a tile outside blocks a and b gets
-// two panels, a tile of block a one (it starts from W_a), block b none.
-double update_flops_pair(const std::vector<Tile> &tl, int64_t naug, int64_t ka0, int kx0, int kx1) {
+// GEMM flops of one k_update_multi launch (npan steps from block ka) on a tile
+// list, skipping the cross of blocks [kx0, kx1): a tile in group block jm
+// starts from W_jm and takes the later panels, any other tile every panel
+// (the kernel's rule; update_gemm_tiles_group over the whole triangle)
+double update_flops_group(const std::vector<Tile> &tl, int64_t naug, int64_t ka0, int npan, int kx0,
+                          int kx1) {
   constexpr int KT = NB / UT;
-  const int ta0 = (int)(ka0 / UT), tb0 = ta0 + KT;
+  const int ta0 = (int)(ka0 / UT);
   const int taug = (int)(naug / UT) - 1;
   double cnt = 0.0;
   for (const Tile &t : tl) {
     if (t.I < 0) continue;
     if (kx0 >= 0 && ((t.I >= kx0 * KT && t.I < kx1 * KT) || (t.J >= kx0 * KT && t.J < kx1 * KT)))
       continue;
-    const bool Ia = t.I >= ta0 && t.I < tb0, Ja = t.J >= ta0 && t.J < tb0;
-    const bool Ib = t.I >= tb0 && t.I < tb0 + KT, Jb = t.J >= tb0 && t.J < tb0 + KT;
-    if (Ib || Jb) continue;
-    cnt += ((t.I == taug) ? 16.0 / UT : 1.0) * ((Ia || Ja) ? 1.0 : 2.0);
+    const int di = t.I - ta0, dj = t.J - ta0;
+    const int bi = (di >= 0 && di < npan * KT) ? di / KT : -1;
+    const int bj = (dj >= 0 && dj < npan * KT) ? dj / KT : -1;
+    const int jm = std::max(bi, bj);
+    if (jm == npan - 1) continue;
+    cnt += ((t.I == taug) ? 16.0 / UT : 1.0) * (jm >= 0 ? npan - 1 - jm : npan);
   }
   return cnt * 2.0 * UT * UT * NB;
 }
 
-// The rank's own lookahead cross lists of the pair schedule (RankState).
-void build_cross_lists(ace_ctx *ctx, RankState &R, int64_t naug, int steps, int G) {
+// The rank's own lookahead cross lists of the group schedule (RankState):
+// per step k the tiles with I or J in block k + 1 (xoff), per group g >= 1
+// (blocks kb = Z g .. kb + z - 1) the cross of block kb (poff[2 g]) and the
+// rest of the group's cross (poff[2 g + 1]).
+void build_cross_lists(ace_ctx *ctx, RankState &R, int64_t naug, int steps, int G, int Z) {
   constexpr int KT = NB / UT;
   const std::vector<Tile> own = own_tiles(naug / UT, UT, G, R.r);
   auto in_blk = [&](int t, int blk) { return t >= blk * KT && t < (blk + 1) * KT; };
@@ -296,14 +300,21 @@ void build_cross_lists(ace_ctx *ctx, RankState &R, int64_t naug, int steps, int 
     x.insert(x.end(), o.begin(), o.end());
     R.xoff.push_back((int64_t)x.size());
   }
-  const int ng = (steps + 1) / 2;
+  const int ng = (steps + Z - 1) / Z;
   R.poff.assign(2 * ng + 1, 0);
   for (int g = 1; g < ng; ++g) {
-    const int b0 = 2 * g, b1 = 2 * g + 1;
+    const int b0 = Z * g, b1 = std::min(steps, Z * (g + 1));  // blocks [b0, b1)
     std::vector<Tile> ta, tb;
     for (const Tile &q : own) {
-      if (in_blk(q.I, b0) || in_blk(q.J, b0)) ta.push_back(q);
-      else if (b1 < steps && (in_blk(q.I, b1) || in_blk(q.J, b1))) tb.push_back(q);
+      if (in_blk(q.I, b0) || in_blk(q.J, b0)) {
+        ta.push_back(q);
+        continue;
+      }
+      for (int bb = b0 + 1; bb < b1; ++bb)
+        if (in_blk(q.I, bb) || in_blk(q.J, bb)) {
+          tb.push_back(q);
+          break;
+        }
     }
     R.poff[2 * g] = (int64_t)pr.size();
     const std::vector<Tile> oa = deal(ta), ob = deal(tb);
@@ -314,11 +325,6 @@ void build_cross_lists(ace_ctx *ctx, RankState &R, int64_t naug, int steps, int 
   }
   upload_tiles(ctx, R.tx, x);
   upload_tiles(ctx, R.tp, pr);
-  R.glen = 0;
-  if (tail_sort()) {
-    const std::vector<Tile> o = pair_bulk_orders(naug, steps, &R.glen, G, R.r);
-    upload_tiles(ctx, R.tgo, o);
-  }
 }
 
 // ---- collectives over the local ranks -------------------------------------
@@ -475,34 +481,40 @@ void run_sweep_sharded_steps(ShardModel &m, int which, bool timed) {
   }
 }
 
-// Two sweep steps per bulk launch, the single-GPU schedule (ace_sweep.hip
-// run_sweep_pairs) on each rank's own tiles.  Group g = steps 2g, 2g + 1:
-//   main:  wait(ready g) -> k_update_pair over the own tiles outside group
-//          g+1's cross (panels 2g, 2g+1) -> bulkdone(g)
-//   side:  wait(bulkdone g-1) -> pair cross of block 2g+2 with panels 2g,
-//          2g+1 -> prepare(2g+2) [pack, exchange, unpack + pivot chain]
-//          -> cross of block 2g+3 with panel 2g+2 -> prepare(2g+3) -> ready(g+1)
-//   side2: the pair cross of block 2g+3 (minus block 2g+2) meanwhile; the
-//          single cross of block 2g+3 waits for it
-// Panels live in slots k & 3.  Every mode runs the lookahead: RCCL exchanges
-// on the side stream; the simulated group's device copies on the side stream
-// (all simulated ranks share the three streams, so their bulk launches
-// overlap the side path exactly as one rank's do); the host-callback group
-// synchronises the side stream and exchanges on the host while the already
-// enqueued bulk launch runs.  The bulk launch of group g is enqueued before
-// the side path of group g+1 so that a blocking (host) exchange overlaps it.
-// Every tile sees the single-step schedule's MFMA chains in the same order:
-// bit-identical to run_sweep_sharded_steps (tests/test_shard_gpu.py).
+// Z sweep steps per bulk launch (Z = sweep_group(), 4 by default), the
+// single-GPU group schedule (ace_sweep.hip run_sweep_groups) on each rank's own
+// tiles.  Group g = steps Z g .. Z g + z - 1, panels in slots k % (2 Z):
+//   main:  wait(ready g) -> k_update_multi over the own tiles outside group
+//          g+1's cross (group g's z panels, K = z NB per tile) -> bulkdone(g)
+//   side:  wait(bulkdone g-1) -> group g's panels on block kb's cross (the
+//          launch that finalises block kb also packs step kb's exchange
+//          buffers) -> prepare(kb) [exchange, unpack + pivot chain + W] ->
+//          [wait side2] for j = 1 .. z-1: panels kb .. kb+j-1 on block
+//          kb+j's cross (packing kb+j) -> prepare(kb+j) -> ready(g+1)
+//   side2: group g's panels on the rest of group g+1's cross, concurrently
+//          with block kb's chain
+// Every mode runs the lookahead: RCCL exchanges on the side stream; the
+// simulated group's device copies on the side stream (all simulated ranks
+// share the three streams, so their bulk launches overlap the side path as
+// one rank's do); the host-callback group synchronises the side stream and
+// exchanges on the host while the already enqueued bulk launch runs.  The
+// bulk launch of group g is enqueued before the side path of group g+1 so
+// that a blocking (host) exchange overlaps it.  Every tile sees the
+// single-step schedule's MFMA chains in the same order (k_update_multi's
+// per-tile rule): bit-identical to run_sweep_sharded_steps
+// (tests/test_shard_gpu.py).
 void run_sweep_sharded(ShardModel &m, int which, bool timed) {
   ace_ctx *ctx = m.ctx;
   const int steps = (int)(m.npad / NB);
-  if (!pair_steps() || steps < 2 || !m.ranks[0]->P[2].p) {
+  const int Z = m.Z;
+  if (!pair_steps() || steps < 2 || Z < 2 || !m.ranks[0]->P[2 * Z - 1].p) {
     run_sweep_sharded_steps(m, which, timed);
     return;
   }
+  const int NS = 2 * Z;  // panel slots
   hipStream_t st = ctx->stream, side = ctx->side, side2 = ctx->side2;
-  const int ng = (steps + 1) / 2;
-  auto zsize = [&](int g) { return std::min(2, steps - 2 * g); };
+  const int ng = (steps + Z - 1) / Z;
+  auto zsize = [&](int g) { return std::min(Z, steps - Z * g); };
   std::vector<ShardSweep> v;
   for (auto &R : m.ranks) v.push_back(sweep_view(m, *R, which));
   // events: [0] inputs, ready(g) 1.., bulkdone(g) 1+ng.., side2 start / done,
@@ -519,86 +531,82 @@ void run_sweep_sharded(ShardModel &m, int which, bool timed) {
   // the cross launch that finalises block k's tiles also writes the exchange
   // buffers of step k (ACE_FUSE_PACK=0: separate k_pack_* launches)
   const bool fuse = fuse_pack();
-  auto prepare = [&](int k, bool packed) {  // panel k into slot k & 3, on `side`
+  auto prepare = [&](int k, bool packed) {  // panel k into slot k % NS, on `side`
     if (!packed)
       for (auto &b : v) ck(ctx, shard_pack(b, k, side), "shard pack");
     exchange(m, k, side);
-    for (auto &b : v) ck(ctx, shard_unpack_chain(b, k, k & 3, side, packed), "shard panel");
+    for (auto &b : v) ck(ctx, shard_unpack_chain(b, k, k % NS, side, packed), "shard panel");
   };
-  auto single_cross = [&](int k) {  // cross of block k + 1 with panel k, on `side`
-    for (size_t j = 0; j < v.size(); ++j) {
-      RankState &R = *m.ranks[j];
-      const int64_t x0 = R.xoff[(size_t)k], nx = R.xoff[(size_t)k + 1] - x0;
-      ck(ctx, shard_update_tiles(v[j], k, k & 3, -1, (const Tile *)R.tx.p + x0, nx, side,
-                                 fuse ? k + 1 : -1),
-         "shard cross update");
+  // blocks kb + 1 .. kb + z - 1 of a group from its own panels, each followed
+  // by its exchange and chain (on `side`)
+  auto inner = [&](int kb, int z) {
+    for (int j = 1; j < z; ++j) {
+      const int k = kb + j - 1;  // xoff list k: the own tiles with I or J in block k + 1
+      for (size_t q = 0; q < v.size(); ++q) {
+        RankState &R = *m.ranks[q];
+        const int64_t x0 = R.xoff[(size_t)k], nx = R.xoff[(size_t)k + 1] - x0;
+        ck(ctx, shard_update_group(v[q], kb, j, NS, -1, -1, (const Tile *)R.tx.p + x0, nx, side,
+                                   fuse ? kb + j : -1),
+           "shard cross update");
+      }
+      prepare(kb + j, fuse);
     }
   };
-  // E_IN: recorded by shard_eval after the first two panels' columns, the
-  // AUG rows and the flag (the rest of the assembly runs on under prepare(0))
+  // E_IN: recorded by shard_eval after the first group's panels' columns,
+  // the AUG rows and the flag (the rest of the assembly runs on under it)
   wait(side, E_IN);
   prepare(0, false);
-  single_cross(0);
-  prepare(1, fuse);
+  inner(0, zsize(0));
   rec(E_READY(0), side);
   m.upd_used = 0;
   rec(E_ASM, st);  // group 1's cross tiles include assembly part-2 tiles
   for (int g = 0; g < ng; ++g) {
-    const int ka = 2 * g;
+    const int kg = Z * g;
     const bool more = g + 1 < ng;
+    const int kb = Z * (g + 1), zb = more ? zsize(g + 1) : 0;
     wait(st, E_READY(g));
     const bool tm = timed && m.upd_used + 2 <= (int)m.ev_upd.size();
-    const int kx0 = more ? 2 * (g + 1) : -1, kx1 = more ? 2 * (g + 1) + zsize(g + 1) : -1;
+    const int kx0 = more ? kb : -1, kx1 = more ? kb + zb : -1;
     for (size_t j = 0; j < v.size(); ++j) {
       RankState &R = *m.ranks[j];
       if (tm && j == 0) ck(ctx, hipEventRecord(m.ev_upd[(size_t)m.upd_used], st), "event");
-      if (zsize(g) == 2 && R.glen > 0)
-        ck(ctx, shard_update_pair(v[j], ka, kx0, kx1, (const Tile *)R.tgo.p + (int64_t)g * R.glen,
-                                  R.glen, st),
-           "shard pair update");
-      else if (zsize(g) == 2)
-        ck(ctx, shard_update_pair(v[j], ka, kx0, kx1, (const Tile *)R.tupd.p, R.nupd, st),
-           "shard pair update");
-      else
-        ck(ctx, shard_update_main(v[j], ka, ka & 3, -1, st), "shard update");
+      ck(ctx, shard_update_group(v[j], kg, zsize(g), NS, kx0, kx1, (const Tile *)R.tupd.p, R.nupd,
+                                 st),
+         "shard group update");
       if (tm && j == 0) {
         ck(ctx, hipEventRecord(m.ev_upd[(size_t)m.upd_used + 1], st), "event");
         m.upd_flops[(size_t)m.upd_used / 2] =
-            zsize(g) == 2 ? update_flops_pair(R.hupd, m.naug, (int64_t)ka * NB, kx0, kx1)
-                          : update_flops(R.hupd, m.naug, (int64_t)ka * NB, -1);
+            update_flops_group(R.hupd, m.naug, (int64_t)kg * NB, zsize(g), kx0, kx1);
         m.upd_used += 2;
       }
     }
     rec(E_BULK(g), st);
     if (!more) break;
     // side path of group g + 1 (its cross tiles were last touched by bulk g-1)
-    const int kb = ka + 2;  // first block of group g + 1
     wait(side, g > 0 ? E_BULK(g - 1) : E_ASM);
-    const bool two = zsize(g + 1) == 2;
-    if (two) {  // block kb + 1's share of the pair cross on side2, concurrently
+    const bool rest = zb > 1;
+    if (rest) {  // the rest of group g+1's cross on side2, concurrently
       rec(E_S2A(g + 1), side);
       wait(side2, E_S2A(g + 1));
       for (size_t j = 0; j < v.size(); ++j) {
         RankState &R = *m.ranks[j];
         const int64_t p0 = R.poff[(size_t)(2 * (g + 1) + 1)], np = R.poff[(size_t)(2 * (g + 1) + 2)] - p0;
-        ck(ctx, shard_update_pair(v[j], ka, -1, -1, (const Tile *)R.tp.p + p0, np, side2),
-           "shard pair cross");
+        ck(ctx, shard_update_group(v[j], kg, zsize(g), NS, -1, -1, (const Tile *)R.tp.p + p0, np,
+                                   side2),
+           "shard group cross");
       }
       rec(E_S2B(g + 1), side2);
     }
     for (size_t j = 0; j < v.size(); ++j) {
       RankState &R = *m.ranks[j];
       const int64_t p0 = R.poff[(size_t)(2 * (g + 1))], np = R.poff[(size_t)(2 * (g + 1) + 1)] - p0;
-      ck(ctx, shard_update_pair(v[j], ka, -1, -1, (const Tile *)R.tp.p + p0, np, side,
-                                fuse ? kb : -1),
-         "shard pair cross");
+      ck(ctx, shard_update_group(v[j], kg, zsize(g), NS, -1, -1, (const Tile *)R.tp.p + p0, np, side,
+                                 fuse ? kb : -1),
+         "shard group cross");
     }
     prepare(kb, fuse);
-    if (two) {
-      wait(side, E_S2B(g + 1));
-      single_cross(kb);
-      prepare(kb + 1, fuse);
-    }
+    if (rest) wait(side, E_S2B(g + 1));
+    inner(kb, zb);
     rec(E_READY(g + 1), side);
   }
 }
@@ -626,6 +634,7 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
   m->ntr = (n + AT - 1) / AT;
   m->G = world;
   m->rank = rank;
+  m->Z = sweep_group();
   m->host = ops != nullptr;
   if (ops) m->ops = *ops;
   m->sim = id == nullptr && !m->host;
@@ -656,13 +665,14 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
     const int64_t nloc = ncols_local(naug, world, 0);
     alloc(ctx, R->A[0], (size_t)(naug * nloc) * sizeof(double), "alloc local A");
     ck(ctx, hipMemsetAsync(R->A[0].p, 0, R->A[0].bytes, ctx->stream), "memset A");
-    const int nslot = pair_steps() && steps >= 2 ? 4 : 2;  // pair schedule: slots k & 3
+    // group schedule: 2 Z panel slots (k % 2Z); the one-step schedule: 2
+    const int nslot = pair_steps() && steps >= 2 ? 2 * m->Z : 2;
     for (int b = 0; b < nslot; ++b) {
       alloc(ctx, R->P[b], (size_t)(naug * NB) * sizeof(double), "alloc panel");
       alloc(ctx, R->W[b], (size_t)(naug * NB) * sizeof(double), "alloc panel");
     }
     for (int b = 0; b < 2; ++b) alloc(ctx, R->S[b], (size_t)(SUB * NB) * sizeof(double), "alloc S");
-    if (nslot == 4) build_cross_lists(ctx, *R, naug, steps, world);
+    if (nslot > 2) build_cross_lists(ctx, *R, naug, steps, world, m->Z);
     alloc(ctx, R->SW, (size_t)SW_DOUBLES * sizeof(double), "alloc SW");
     alloc(ctx, R->piv, (size_t)npad * sizeof(double), "alloc piv");
     alloc(ctx, R->flag, 16, "alloc flag");
@@ -678,9 +688,9 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
     R->nupd = (int64_t)R->hupd.size();
     upload_tiles(ctx, R->tupd, R->hupd);
     std::vector<Tile> ta = own_tiles(npad / AT, AT, world, R->r);
-    // the first two panels' columns first (the pair schedule's first side
-    // path runs under the rest of the assembly, as model_pipeline's)
-    const int jb = 2 * NB / AT;
+    // the first group's panels' columns first (the group schedule's first
+    // side path runs under the rest of the assembly, as model_pipeline's)
+    const int jb = m->Z * NB / AT;
     R->nasm1 = std::stable_partition(ta.begin(), ta.end(), [&](const Tile &t) { return t.J < jb; }) -
                ta.begin();
     R->nasm = (int64_t)ta.size();
@@ -767,7 +777,7 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
     ck(ctx, hipMemcpyAsync(R->tab.p, h, tab.size() * sizeof(double), hipMemcpyHostToDevice, st),
        "upload tables");
   }
-  // assembly (own tiles) + AUG rows: the first two panels' columns, the
+  // assembly (own tiles) + AUG rows: the first group's panels' columns, the
   // AUG rows and the flag, then (the sweep's first side path may start) the rest
   if (timed) ck(ctx, hipEventRecord(m->ev_asm[0], st), "event");
   for (int part = 0; part < 2; ++part) {

@@ -1050,6 +1050,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
 // update's pipelined 8-wave tile: under the bulk update k_panel_gemm's 64-row
 // strips held 258 update-sized CU slots for ~185 us per panel (skipping it
 // took 6 ms off a C2 evaluation, profiles/r02_chain_ab.txt).
+template <int DEPTH>
 __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict__ W,
                                                               const double *__restrict__ Pn,
                                                               int64_t ldp, int64_t k0, int G,
@@ -1074,35 +1075,39 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
   const double *gW = Pn + (R0 + sm) + (int64_t)sk * ldp;
 #endif
   const double *gP = W + (k0 + C0 + sm) + (int64_t)sk * ldp;  // W_kk(c, k) = W[k0 + c, k]
-  double2 rw[2], rp[2];
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    rw[e] = *reinterpret_cast<const double2 *>(gW + SH128 * e);
-    rp[e] = *reinterpret_cast<const double2 *>(gP + SH128 * e);
-  }
+  // DEPTH = 2 (round 5; the head path's launches): two chunks of loads in
+  // flight -- a chunk is loaded into one of two register sets two iterations
+  // before it is staged, so its latency overlaps two chunks' MFMAs instead
+  // of one.  The head launches have few workgroups, each walking all 16
+  // chunks, and were bound by that latency (C1 trace: 35-45 us for 8.4
+  // MFLOP per workgroup).  DEPTH = 1: one chunk ahead in 108 VGPRs (two
+  // workgroups per CU for the many-workgroup tail launches; the second set
+  // takes 132).  Same MFMA chain in the same k order: bit-identical.
   const int wr = wv & 1, wc = wv >> 1;
   d4 acc[2][4];
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
     for (int ri = 0; ri < 4; ++ri) acc[ci][ri] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    *reinterpret_cast<double2 *>(&sW[0][sk][sm + SH128 * e]) = rw[e];
-    *reinterpret_cast<double2 *>(&sP[0][sk][sm + SH128 * e]) = rp[e];
-  }
-  __syncthreads();
-  ACE_WGT_MARK(0);
-  for (int ch = 0; ch < NCH; ++ch) {
-    const int cur = ch & 1;
-    if (ch + 1 < NCH) {
-      const int64_t off = (int64_t)(ch + 1) * BK * ldp;
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        rw[e] = *reinterpret_cast<const double2 *>(gW + off + SH128 * e);
-        rp[e] = *reinterpret_cast<const double2 *>(gP + off + SH128 * e);
-      }
-    }
+  // the two register sets as named values (arrays passed to helpers ended
+  // up in scratch)
+  double2 w00, w01, p00, p01, w10, w11, p10, p11;
+#define PG_LOAD(W0, W1, P0, P1, CH)                                               \
+  do {                                                                            \
+    const int64_t off_ = (int64_t)(CH) * BK * ldp;                                \
+    W0 = *reinterpret_cast<const double2 *>(gW + off_);                           \
+    W1 = *reinterpret_cast<const double2 *>(gW + off_ + SH128);                   \
+    P0 = *reinterpret_cast<const double2 *>(gP + off_);                           \
+    P1 = *reinterpret_cast<const double2 *>(gP + off_ + SH128);                   \
+  } while (0)
+#define PG_STAGE(W0, W1, P0, P1, BUF)                                             \
+  do {                                                                            \
+    *reinterpret_cast<double2 *>(&sW[BUF][sk][sm]) = W0;                          \
+    *reinterpret_cast<double2 *>(&sW[BUF][sk][sm + SH128]) = W1;                  \
+    *reinterpret_cast<double2 *>(&sP[BUF][sk][sm]) = P0;                          \
+    *reinterpret_cast<double2 *>(&sP[BUF][sk][sm + SH128]) = P1;                  \
+  } while (0)
+  auto mma = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < BK / 4; ++kk) {
       double a[2], b[4];
@@ -1116,15 +1121,46 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
         for (int ri = 0; ri < 4; ++ri)
           acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
     }
-    if (ch + 1 < NCH) {
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + SH128 * e]) = rw[e];
-        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + SH128 * e]) = rp[e];
-      }
+  };
+  static_assert(NCH % 2 == 0 && NCH >= 4, "two chunks per pipeline turn");
+  if constexpr (DEPTH == 1) {
+    PG_LOAD(w00, w01, p00, p01, 0);
+    PG_STAGE(w00, w01, p00, p01, 0);
+    __syncthreads();
+    ACE_WGT_MARK(0);
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int cur = ch & 1;
+      if (ch + 1 < NCH) PG_LOAD(w00, w01, p00, p01, ch + 1);
+      mma(cur);
+      if (ch + 1 < NCH) PG_STAGE(w00, w01, p00, p01, cur ^ 1);
+      __syncthreads();
+    }
+  } else {
+  PG_LOAD(w00, w01, p00, p01, 0);
+  PG_STAGE(w00, w01, p00, p01, 0);
+  PG_LOAD(w10, w11, p10, p11, 1);
+  PG_LOAD(w00, w01, p00, p01, 2);
+  __syncthreads();
+  ACE_WGT_MARK(0);
+  // turn: chunk ch (even) from LDS 0 while chunk ch+1 (set 1) is staged into
+  // LDS 1 and chunk ch+3 loaded into set 1; then chunk ch+1 from LDS 1 while
+  // chunk ch+2 (set 0) goes to LDS 0 and chunk ch+4 into set 0
+#pragma unroll 1
+  for (int ch = 0; ch < NCH; ch += 2) {
+    mma(0);
+    PG_STAGE(w10, w11, p10, p11, 1);
+    if (ch + 3 < NCH) PG_LOAD(w10, w11, p10, p11, ch + 3);
+    __syncthreads();
+    mma(1);
+    if (ch + 2 < NCH) {
+      PG_STAGE(w00, w01, p00, p01, 0);
+      if (ch + 4 < NCH) PG_LOAD(w00, w01, p00, p01, ch + 4);
     }
     __syncthreads();
   }
+  }
+#undef PG_LOAD
+#undef PG_STAGE
   ACE_WGT_MARK(1);
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci)
@@ -1785,53 +1821,68 @@ __global__ __launch_bounds__(256, 4) void k_update_q(double *__restrict__ A, int
       for (int j = 0; j < 4; ++j) acc[ci][ri][j] = A[r + (c + 4 * j) * ld];
     }
   const int sk = tid >> 4, sm = (tid & 15) * SM64;  // 2nd half at sm + SH64
-  // staging registers as named values (an array here was kept in scratch)
-  double2 w0, w1, p0, p1;
-  for (int pj = 0; pj < npan; ++pj) {
-    const double *gW = psel(ps.R, pj) + (R0 + sm) + (int64_t)sk * ldp;
-    const double *gP = psel(ps.C, pj) + (C0 + sm) + (int64_t)sk * ldp;
-    w0 = *reinterpret_cast<const double2 *>(gW);
-    w1 = *reinterpret_cast<const double2 *>(gW + SH64);
-    p0 = *reinterpret_cast<const double2 *>(gP);
-    p1 = *reinterpret_cast<const double2 *>(gP + SH64);
-    __syncthreads();  // the previous panel's last chunk is consumed
-    *reinterpret_cast<double2 *>(&sW[0][sk][sm]) = w0;
-    *reinterpret_cast<double2 *>(&sW[0][sk][sm + SH64]) = w1;
-    *reinterpret_cast<double2 *>(&sP[0][sk][sm]) = p0;
-    *reinterpret_cast<double2 *>(&sP[0][sk][sm + SH64]) = p1;
-    __syncthreads();
-#pragma unroll 2
-    for (int ch = 0; ch < NCH; ++ch) {
-      const int cur = ch & 1;
-      if (ch + 1 < NCH) {
-        const int64_t off = (int64_t)(ch + 1) * BK * ldp;
-        w0 = *reinterpret_cast<const double2 *>(gW + off);
-        w1 = *reinterpret_cast<const double2 *>(gW + off + SH64);
-        p0 = *reinterpret_cast<const double2 *>(gP + off);
-        p1 = *reinterpret_cast<const double2 *>(gP + off + SH64);
-      }
+  // The npan panels' NCH chunks as one sequence with two chunks of loads in
+  // flight (round 5): chunk t is loaded into one of two register sets two
+  // chunks before it is staged, so its latency overlaps two chunks' MFMAs.
+  // A head-path launch is latency-bound (C1 trace: 33 us per one-panel
+  // launch); the MFMA chain and its k order are unchanged: bit-identical.
+  // Staging registers as named values (an array here was kept in scratch).
+  double2 w00, w01, p00, p01, w10, w11, p10, p11;
+  const int T = npan * NCH;
+#define UQ_LOAD(W0, W1, P0, P1, TT)                                               \
+  do {                                                                            \
+    const int pj_ = (TT) / NCH, ch_ = (TT) - pj_ * NCH;                           \
+    const int64_t off_ = (int64_t)ch_ * BK * ldp;                                 \
+    const double *gW_ = psel(ps.R, pj_) + (R0 + sm) + (int64_t)sk * ldp + off_;   \
+    const double *gP_ = psel(ps.C, pj_) + (C0 + sm) + (int64_t)sk * ldp + off_;   \
+    W0 = *reinterpret_cast<const double2 *>(gW_);                                 \
+    W1 = *reinterpret_cast<const double2 *>(gW_ + SH64);                          \
+    P0 = *reinterpret_cast<const double2 *>(gP_);                                 \
+    P1 = *reinterpret_cast<const double2 *>(gP_ + SH64);                          \
+  } while (0)
+#define UQ_STAGE(W0, W1, P0, P1, BUF)                                             \
+  do {                                                                            \
+    *reinterpret_cast<double2 *>(&sW[BUF][sk][sm]) = W0;                          \
+    *reinterpret_cast<double2 *>(&sW[BUF][sk][sm + SH64]) = W1;                   \
+    *reinterpret_cast<double2 *>(&sP[BUF][sk][sm]) = P0;                          \
+    *reinterpret_cast<double2 *>(&sP[BUF][sk][sm + SH64]) = P1;                   \
+  } while (0)
+  auto mma = [&](int cur) {
 #pragma unroll
-      for (int kk = 0; kk < BK / 4; ++kk) {
-        double a[2], b[2];
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double a[2], b[2];
 #pragma unroll
-        for (int ci = 0; ci < 2; ++ci) a[ci] = sP[cur][4 * kk + lk][32 * wc + 16 * ci + lr];
+      for (int ci = 0; ci < 2; ++ci) a[ci] = sP[cur][4 * kk + lk][32 * wc + 16 * ci + lr];
 #pragma unroll
-        for (int ri = 0; ri < 2; ++ri) b[ri] = sW[cur][4 * kk + lk][32 * wr + 16 * ri + lr];
+      for (int ri = 0; ri < 2; ++ri) b[ri] = sW[cur][4 * kk + lk][32 * wr + 16 * ri + lr];
 #pragma unroll
-        for (int ci = 0; ci < 2; ++ci)
+      for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
-          for (int ri = 0; ri < 2; ++ri)
-            acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
-      }
-      if (ch + 1 < NCH) {
-        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm]) = w0;
-        *reinterpret_cast<double2 *>(&sW[cur ^ 1][sk][sm + SH64]) = w1;
-        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm]) = p0;
-        *reinterpret_cast<double2 *>(&sP[cur ^ 1][sk][sm + SH64]) = p1;
-      }
-      __syncthreads();
+        for (int ri = 0; ri < 2; ++ri)
+          acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
     }
+  };
+  static_assert(NCH % 2 == 0 && NCH >= 4, "two chunks per pipeline turn");
+  UQ_LOAD(w00, w01, p00, p01, 0);
+  UQ_STAGE(w00, w01, p00, p01, 0);
+  UQ_LOAD(w10, w11, p10, p11, 1);
+  UQ_LOAD(w00, w01, p00, p01, 2);
+  __syncthreads();
+#pragma unroll 1
+  for (int t = 0; t < T; t += 2) {
+    mma(0);
+    UQ_STAGE(w10, w11, p10, p11, 1);
+    if (t + 3 < T) UQ_LOAD(w10, w11, p10, p11, t + 3);
+    __syncthreads();
+    mma(1);
+    if (t + 2 < T) {
+      UQ_STAGE(w00, w01, p00, p01, 0);
+      if (t + 4 < T) UQ_LOAD(w00, w01, p00, p01, t + 4);
+    }
+    __syncthreads();
   }
+#undef UQ_LOAD
+#undef UQ_STAGE
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
@@ -2016,7 +2067,7 @@ static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, dou
   // on the second side stream)
   if (before_gemm) (void)hipStreamWaitEvent(st, before_gemm, 0);
   if (pgemm_tiles())
-    hipLaunchKernelGGL(k_panel_gemm_t, dim3((unsigned)(ld / UT), NB / UT), dim3(UTHREADS), 0, st,
+    hipLaunchKernelGGL(k_panel_gemm_t<1>, dim3((unsigned)(ld / UT), NB / UT), dim3(UTHREADS), 0, st,
                        W, Pn, ld, k0, G, r, 0, 1 << 30, 1 << 30);
   else
     hipLaunchKernelGGL(k_panel_gemm, dim3((unsigned)(ld / SUB)), dim3(512), 0, st, W, Pn, ld, k0,
@@ -2843,7 +2894,13 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   auto pgemm = [&](int k, int r0, int r1, bool head, hipStream_t s_) {
     const int n = head ? r1 - r0 : (int)nT - (r1 - r0);
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_panel_gemm_t, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, s_,
+    // the head rows (few workgroups, latency-bound): two chunks in flight
+    if (head)
+      hipLaunchKernelGGL(k_panel_gemm_t<2>, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, s_,
+                         b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, 1, 0, r0, 1 << 30,
+                         1 << 30);
+    else
+    hipLaunchKernelGGL(k_panel_gemm_t<1>, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, s_,
                        b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, 1, 0, head ? r0 : 0,
                        head ? 1 << 30 : r0, head ? 1 << 30 : r1);
   };
@@ -3090,35 +3147,26 @@ hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t s
   return hipGetLastError();
 }
 
-hipError_t shard_update_tiles(const ShardSweep &b, int k, int slot, int kx, const Tile *tiles,
-                              int64_t nt, hipStream_t st, int kpack) {
-  const int sp = kpack & 3;
-  const GatherOut go = kpack >= 0 ? pack_out(b.low, send_of(b, kpack), b.P[sp], b.W[sp], b.S[0],
-                                             (int64_t)kpack * NB, b.ld, b.G)
-                                  : no_gather();
-  if (nt > 0)
-    hipLaunchKernelGGL(k_update, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld, b.P[slot],
-                       b.W[slot], b.W[slot], b.ld, (int64_t)k * NB, kx, tiles, b.G, go);
-  return hipGetLastError();
-}
-
-hipError_t shard_update_pair(const ShardSweep &b, int ka, int kx0, int kx1, const Tile *tiles,
-                             int64_t nt, hipStream_t st, int kpack) {
-  const int sa = ka & 3, sb = (ka + 1) & 3;
-  const int sp = kpack & 3;
+hipError_t shard_update_group(const ShardSweep &b, int kb, int npan, int nslot, int kx0, int kx1,
+                              const Tile *tiles, int64_t nt, hipStream_t st, int kpack) {
+  const int sp = kpack >= 0 ? kpack % nslot : 0;
   const GatherOut go = kpack >= 0 ? pack_out(b.low, send_of(b, kpack), b.P[sp], b.W[sp], b.S[0],
                                              (int64_t)kpack * NB, b.ld, b.G)
                                   : no_gather();
   if (nt <= 0) return hipGetLastError();
-  if (multi2_on()) {
-    PanelSet ps{{b.P[sa], b.P[sb], nullptr, nullptr}, {b.W[sa], b.W[sb], nullptr, nullptr}};
-    hipLaunchKernelGGL(k_update_multi<true>, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld,
-                       ps, 2, b.ld, (int64_t)ka * NB, kx0, kx1, tiles, go, b.G);
-  } else {
-    hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld, b.P[sa],
-                       b.W[sa], b.P[sb], b.W[sb], b.ld, (int64_t)ka * NB, kx0, kx1, tiles, go,
-                       -1, nullptr, b.G, 1);
+  if (npan == 1) {  // (only ever without a skip range)
+    const int s0 = kb % nslot;
+    hipLaunchKernelGGL(k_update, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld, b.P[s0],
+                       b.W[s0], b.W[s0], b.ld, (int64_t)kb * NB, -1, tiles, b.G, go);
+    return hipGetLastError();
   }
+  PanelSet ps;
+  for (int j = 0; j < 4; ++j) {
+    ps.R[j] = j < npan ? b.P[(kb + j) % nslot] : nullptr;
+    ps.C[j] = j < npan ? b.W[(kb + j) % nslot] : nullptr;
+  }
+  hipLaunchKernelGGL(k_update_multi<true>, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld, ps,
+                     npan, b.ld, (int64_t)kb * NB, kx0, kx1, tiles, go, b.G);
   return hipGetLastError();
 }
 

@@ -3,31 +3,31 @@ bucket, against the extended-precision referee (tests/referee_ld.py via
 tests/golden/referee_*.npz) rather than the fp64 oracle, whose own rounding
 (<= 2e-12 here, tests/test_referee_cpu.py) would otherwise hide a kernel's.
 
-The bound is 1e-10 relative with the smoke's 1e-9 * max floor: fifty times
-the fp64 oracle's error, and ten times below the 8.6e-10 the round-4 kernels
-reached on the smoke problem ("numeric drift"), so a change
-that is claimed bit-identical or ulp-level is checked at every PM bucket,
-not only at p = 20."""
+Bounds ("numeric accuracy"): per gradient component
+|g_i - g_i,ref| <= 1e-10 |g_i,ref| + 2e-12 max|g_ref|.  The engine's
+absolute error is ~1e-12 max|g| in every component -- half from the blocked
+inverse, half from the gradient kernel's summation (tools/inverse_analyze.py,
+profiles/r05_*) -- so components 1e-5 of the largest (the smoke problem's
+g_16 = 2.4e-3 against 110) cannot meet 1e-10 relative to themselves; the
+2e-12 floor is 500 times below the 1e-9 max floor of the other parity
+tests and ~10 times above the errors measured at every bucket.  A change
+claimed bit-identical or ulp-level is checked here at every PM bucket, not
+only at p = 20.  Stats 5e-11 relative (measured <= 5e-12); mu 1e-9 relative
+(it cancels: its terms are ~1e5 times mu; measured <= 4e-11)."""
 import numpy as np
 import pytest
 from conftest import golden, golden_names
 
 pytestmark = pytest.mark.gpu
 
-GRAD_TOL = 1e-10
-STATS_TOL = 1e-12
-MU_TOL = 1e-10
+GRAD_REL = 1e-10
+GRAD_FLOOR = 2e-12
+STATS_TOL = 5e-11
+MU_TOL = 1e-9
 
 
 def _ld(d, key):
     return d[key + "_hi"].astype(np.longdouble) + d[key + "_lo"]
-
-
-def _rel(a, ref, floor):
-    a = np.asarray(a, dtype=np.longdouble)
-    den = np.abs(ref) + floor * np.max(np.abs(ref))
-    e = np.abs(a - ref) / den
-    return float(np.max(e)), int(np.argmax(e))
 
 
 @pytest.fixture(scope="module")
@@ -48,9 +48,13 @@ def test_fused_model_matches_extended_precision_referee(A, name, kernel):
     m.set_data(y, X, Z, sy)
     g, st, mu = m.para_update(1, th.copy())
     m.close()
-    eg, ig = _rel(g, _ld(d, kernel + "_g"), 1e-9)
-    es, _ = _rel(st, _ld(d, kernel + "_st"), 0.0)
-    em, _ = _rel([mu], _ld(d, kernel + "_mu"), 0.0)
-    assert eg <= GRAD_TOL, f"gradient rel err {eg:.2e} at index {ig} (P = {g.size})"
+    g_ref, st_ref, mu_ref = _ld(d, kernel + "_g"), _ld(d, kernel + "_st"), _ld(d, kernel + "_mu")[0]
+    err = np.abs(np.asarray(g, dtype=np.longdouble) - g_ref)
+    bound = GRAD_REL * np.abs(g_ref) + GRAD_FLOOR * np.max(np.abs(g_ref))
+    i = int(np.argmax(err / bound))
+    assert np.all(err <= bound), (f"gradient index {i} of {g.size}: error {float(err[i]):.3e} "
+                                  f"> bound {float(bound[i]):.3e} (value {float(g_ref[i]):.3e})")
+    es = float(np.max(np.abs(np.asarray(st, dtype=np.longdouble) - st_ref) / np.abs(st_ref)))
     assert es <= STATS_TOL, f"stats rel err {es:.2e}"
+    em = float(abs(np.longdouble(mu) - mu_ref) / abs(mu_ref))
     assert em <= MU_TOL, f"mu rel err {em:.2e}"
