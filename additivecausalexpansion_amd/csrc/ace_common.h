@@ -42,6 +42,10 @@ struct ace_ctx {
   // next invkernel_dev of the same n instead of a new 2 n^2-byte allocation
   std::vector<std::shared_ptr<SweepWork>> sweep_pool;
   std::shared_ptr<void> dmat_state;  // the handle path's cached inputs (ace_dmat.cpp)
+  // prediction's n x nx scratch (K_xX, the product, K_xx; ace_predict.cpp),
+  // kept between calls -- a fresh 0.5 GB hipMalloc / hipFree pair per call
+  // costs more than the kernels it feeds; dropped when an allocation fails
+  std::shared_ptr<void> pred_state;
 };
 
 extern std::string g_create_err;
@@ -102,9 +106,11 @@ inline void alloc(ace_ctx *ctx, DBuf &b, size_t bytes, const char *what) {
   b.release();
   if (bytes == 0) bytes = 16;
   hipError_t e = hipMalloc(&b.p, bytes);
-  if ((e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) && !ctx->sweep_pool.empty()) {
+  if ((e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) &&
+      (!ctx->sweep_pool.empty() || ctx->pred_state)) {
     (void)hipGetLastError();
     ctx->sweep_pool.clear();
+    ctx->pred_state.reset();  // (a caller allocating into it holds its own reference)
     e = hipMalloc(&b.p, bytes);
   }
   if (e != hipSuccess) b.p = nullptr;

@@ -99,6 +99,7 @@ hipError_t launch_assembly_persist(int kind, int PM, PairSide S, int64_t npad, i
 int assembly_persist_per_cu(int kind, int PM, int B);
 bool pairs_use_mm(int PM, bool grad);
 bool mm_lds_ok(int PM, int B, int kind, bool grad);
+bool cross_mm_lds_ok(int PM, int B, int kind);
 // mode 2 without a cube on the MFMA r2 expansion (k_cross_mm): R.n x C.n, ld
 hipError_t launch_cross_mm(int kind, int PM, PairSide R, PairSide C, int B, int ZS, TabView tab,
                            int b0, int b1, double *out, int64_t ld, hipStream_t st);
@@ -171,7 +172,14 @@ struct SweepBufs {
   const int64_t *moff = nullptr;
   const int *mfront = nullptr, *mtarget = nullptr;
   int *mcnt = nullptr;
+  // small n: per group a bulk work queue of BQ_INTS ints (k_update_multi_r,
+  // zeroed per sweep) and the CUs per shader engine it leaves to the chains
+  int *bq = nullptr;
+  int breserve = 0;
 };
+constexpr int BQ_INTS = 2 + 64;
+int bulk_reserve(int64_t naug);
+bool q_first(int64_t naug);
 // ACE_XMERGE=1: the next group's lookahead cross tiles run at the head of the
 // bulk launch instead of as side-stream launches (merged_bulk_orders)
 bool merge_cross();

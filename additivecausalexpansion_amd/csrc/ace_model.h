@@ -12,6 +12,8 @@ struct SweepWork {
   int Z = 2;  // steps per bulk launch (sweep_group()), panel slots k % 2Z
   DBuf gtiles;                          // handle path: the gradient's tile list (build_grad_tiles)
   DBuf aq;                              // persistent assembly: tile counter, exits, CU claims
+  DBuf bq;                              // small n: the bulk launches' work queues
+  int breserve = 0;
   DBuf gpart, gwork, gsum;              // handle path: gradient partial-sum scratch
   DBuf norms;                           // handle path: slice norms (TabView::norms)
   int64_t ngtiles = 0, ngdiag = -2;     // -2: not built yet
@@ -79,6 +81,9 @@ struct SweepWork {
         alloc(ctx, mcnt, (size_t)round_up((int64_t)mfront.size(), 4) * sizeof(int), "alloc counters");
       }
     }
+    breserve = (Z > 2 && heads_on()) ? bulk_reserve(naug) : 0;
+    if (breserve > 0)
+      alloc(ctx, bq, (size_t)((npad / NB + Z - 1) / Z * BQ_INTS) * sizeof(int), "alloc bulk queues");
     xoff.clear();
     if (cross_update_on_tiles()) {
       const std::vector<Tile> t = cross_update_tiles(naug, (int)(npad / NB), xoff);
@@ -121,6 +126,10 @@ struct SweepWork {
       b.mfront = mfront.data();
       b.mtarget = mtarget.data();
       b.mcnt = mcnt.i();
+    }
+    if (breserve > 0 && bq.p) {
+      b.bq = bq.i();
+      b.breserve = breserve;
     }
     b.SW = SW.d();
     b.S[0] = S0.d();

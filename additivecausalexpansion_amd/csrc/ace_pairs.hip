@@ -672,7 +672,7 @@ hipError_t launch_assembly(int mode, int kind, int PM, PairSide R, PairSide C, i
   if (mode == 0 && pairs_use_mm(PM, false) && mm_lds_ok(PM, B, kind, false))
     return launch_assembly_mm(kind, PM, R, npad, B, ZS, tab, sig, out, ld, cube, st, tiles,
                               ntiles, G, part);
-  if (mode == 2 && !cube && !tiles && pairs_use_mm(PM, false) && mm_lds_ok(PM, B, kind, false))
+  if (mode == 2 && !cube && !tiles && pairs_use_mm(PM, false) && cross_mm_lds_ok(PM, B, kind))
     return launch_cross_mm(kind, PM, R, C, B, ZS, tab, b0, b1, out, ld, st);
   if (part == 2) return hipSuccess;  // the all-VALU path assembles everything in part 1
   switch (PM) {

@@ -345,20 +345,25 @@ __device__ __forceinline__ double sqrt_gs(double x) {
   return fma(s, fma(-h, s, 0.5), s);
 }
 
-// Reference expressions of one slice value (same as ace_pairs.hip kval):
+// One slice value, the reference expressions (same as ace_pairs.hip kval):
 //  SE  (src/kernel_SE_cpp.cpp:96, 119), Matern32 (src/kernel_Matern_cpp.cpp:217-227).
+// Without a slice test: the loops run slice 0 with z = 1 and log|z| = 0 (an
+// LDS row of ones / zeros), which gives the basis slice's value bit for bit
+// (x * 1, x + 0 and 1 * 1 * x are exact).  Every pair of a slice then stays
+// in one basic block (round 5: with a b == 0 branch each pair was its own
+// block -- k_cross_mm at 168 VGPRs with 62 spills for Matern at PM = 20, the
+// assembly tiles one block per pair).  z = 0: SE selects the reference's 0
+// (log|0| = -inf makes the exponential NaN), Matern's product is 0.
 template <int KIND>
-__device__ __forceinline__ double kval_mm(int b, double r2, double lam, double zlo, double zhi,
+__device__ __forceinline__ double kval_nb(double r2, double lam, double zlo, double zhi,
                                           double lzlo, double lzhi, const double *etab) {
   if (KIND == 0) {
-    if (b == 0) return exp_asm(lam - r2, etab);
-    if (zlo == 0.0 || zhi == 0.0) return 0.0;
-    return (sgn_mm(zlo) * sgn_mm(zhi)) * exp_asm(((lam - r2) + lzlo) + lzhi, etab);
+    const double kz = (sgn_mm(zlo) * sgn_mm(zhi)) * exp_asm(((lam - r2) + lzlo) + lzhi, etab);
+    return sel_f64(zlo == 0.0 || zhi == 0.0, 0.0, kz);
   } else {
-    const double t = sqrt_pk_pos(r2);  // r2 >= 1e-300 (k_asm_mm)
+    const double t = sqrt_pk_pos(r2);
     const double e = (1.0 + SQRT3 * t) * exp_asm(lam - SQRT3 * t, etab);
-    if (b == 0) return e;
-    return (e * zlo) * zhi;  // z = 0 gives 0 (the reference's explicit zero test)
+    return (e * zlo) * zhi;
   }
 }
 
@@ -502,7 +507,11 @@ __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS
   // norms: from the per-evaluation table (launch_slice_norms, the same
   // arithmetic once per point instead of once per tile: bit-identical), or
   // task = (side, slice, point), same accumulation order as the per-slice
-  // loops they replace (i ascending, fma(x^2, w, s))
+  // loops they replace (i ascending, fma(x^2, w, s)).  (Round 5: issuing
+  // every staging load before the first LDS store, as in k_panel_split's
+  // prologue, measured 2.47 -> 2.53 ms for the assembly at C2 and left the
+  // gradient tiles' prologue at 13 us -- there the tile's other workgroup
+  // keeps the CU's issue busy, the latency is not exposed; not kept.)
   if (norms) {
     for (int e = tid; e < 2 * NS * 64; e += NT) {
       const int side = e / (NS * 64), rem = e - side * NS * 64;
@@ -673,7 +682,9 @@ __device__ __forceinline__ void asm_mm_tile(double *lds, PairSide S, int B, int 
   auto slices = [&](auto diag) {
     constexpr bool DG = decltype(diag)::value;
     for (int b = 0; b < B; ++b) {
-      double zr = 0.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
+      // issued ahead of GEMM1, which hides the latency; slice 0 as z = 1,
+      // log|z| = 0 (L.Z / L.LZ row -1), so the pairs need no slice test
+      double zr = 1.0, lzr = 0.0;
       if (b > 0) {
         zr = S.Z[r * ZS + b - 1];
         if (KIND == 0) lzr = S.LZ[r * ZS + b - 1];
@@ -693,13 +704,10 @@ __device__ __forceinline__ void asm_mm_tile(double *lds, PairSide S, int B, int 
           constexpr double R2MIN = KIND == 1 ? 1e-300 : 0.0;
           double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), R2MIN);
           if (DG && c == r) r2 = R2MIN;
-          double zc = 0.0, lzc = 0.0;
-          if (b > 0) {
-            zc = L.Z[(b - 1) * 64 + cbase + cl];
-            if (KIND == 0) lzc = L.LZ[(b - 1) * 64 + cbase + cl];
-          }
-          const double kb = (DG && r < c) ? kval_mm<KIND>(b, r2, lam, zr, zc, lzr, lzc, L.E)
-                                          : kval_mm<KIND>(b, r2, lam, zc, zr, lzc, lzr, L.E);
+          const double zc = L.Z[(b - 1) * 64 + cbase + cl];
+          const double lzc = KIND == 0 ? L.LZ[(b - 1) * 64 + cbase + cl] : 0.0;
+          const double kb = (DG && r < c) ? kval_nb<KIND>(r2, lam, zr, zc, lzr, lzc, L.E)
+                                          : kval_nb<KIND>(r2, lam, zc, zr, lzc, lzr, L.E);
           kf[cb][v] += kb;
           MM_PAIR_FENCE(cb, v);
         }
@@ -769,7 +777,7 @@ __global__ __launch_bounds__(ASM_NT, (ACE_ASM_CB == 2 ? 4 : PM <= 32 ? 3 : 2)) v
 // VALU: 10.8 TF/s at n = 16384, nx = 4096).
 // ---------------------------------------------------------------------------
 template <int PM, int KIND>
-__global__ __launch_bounds__(256, PM <= 32 ? 3 : 2) void k_cross_mm(PairSide R, PairSide C, int B,
+__global__ __launch_bounds__(256, PM <= 32 ? 4 : 2) void k_cross_mm(PairSide R, PairSide C, int B,
                                                                    int ZS, TabView tab, int b0,
                                                                    int b1,
                                                                    double *__restrict__ out,
@@ -784,10 +792,13 @@ __global__ __launch_bounds__(256, PM <= 32 ? 3 : 2) void k_cross_mm(PairSide R, 
   const MmLayout o = mm_layout(PM, B, KIND, false);
   double *const E = lds + o.etab, *const XJ = lds + o.xj, *const Zc = lds + o.z + 64,
                *const LZc = lds + o.lz + 64, *const Nc = lds + o.nc, *const Nr = lds + o.nr,
-               *const W = lds + o.w;
+               *const W = lds + o.w, *const XI = lds + o.total;
+  // both sides' points staged (coalesced): the row side's slice norms are
+  // then LDS loops too, not PM dependent global loads per thread
   for (int e = tid; e < 64 * PM; e += 256) {
     const int c = e / PM, i = e - c * PM;
     XJ[c * XP + i] = (C0 + c < C.n) ? C.X[(C0 + c) * PM + i] : 0.0;
+    XI[c * XP + i] = (R0 + c < R.n) ? R.X[(R0 + c) * PM + i] : 0.0;
   }
   for (int e = tid; e < (B - 1) * 64; e += 256) {
     const int bb = e >> 6, c = e & 63;
@@ -815,16 +826,13 @@ __global__ __launch_bounds__(256, PM <= 32 ? 3 : 2) void k_cross_mm(PairSide R, 
         s = fma(x * x, wv[i], s);
       }
       Nc[rem] = s;
-    } else if (R0 + pt < R.n) {
-      const double *xr = R.X + (R0 + pt) * PM;
+    } else {
 #pragma unroll 4
       for (int i = 0; i < PM; ++i) {
-        const double x = xr[i];
+        const double x = XI[pt * XP + i];
         s = fma(x * x, wv[i], s);
       }
       Nr[rem] = s;
-    } else {
-      Nr[rem] = 0.0;
     }
   }
   __syncthreads();
@@ -832,22 +840,25 @@ __global__ __launch_bounds__(256, PM <= 32 ? 3 : 2) void k_cross_mm(PairSide R, 
   const int64_t r = R0 + rl;
   const bool rok = r < R.n;
   RowX<PM> xr;
-  xr.load(R.X + (rok ? r : 0) * PM, lk);
+  xr.load(XI + rl * XP, lk);
   double kf[4][4];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
     for (int v = 0; v < 4; ++v) kf[cb][v] = 0.0;
   for (int b = b0; b < b1; ++b) {
-    double zr = 0.0, lzr = 0.0;
-    if (b > 0 && rok) {
-      zr = R.Z[r * ZS + b - 1];
-      if (KIND == 0) lzr = R.LZ[r * ZS + b - 1];
+    // slice 0 as z = 1, log|z| = 0 (Zc / LZc row -1 holds them): no per-pair
+    // slice test (kval_nb)
+    double zr = 1.0, lzr = 0.0;
+    if (b > 0) {
+      zr = rok ? R.Z[r * ZS + b - 1] : 0.0;
+      if (KIND == 0) lzr = rok ? R.LZ[r * ZS + b - 1] : 0.0;
     }
     d4 acc[4];
     gemm1_mm<XP, 4>(XJ, xr, W + b * PM, lr, lk, acc, 0);
     const double sr = Nr[b * 64 + rl];
     const double *nc = Nc + b * 64;
+    const double *zcol = Zc + (b - 1) * 64, *lzcol = LZc + (b - 1) * 64;
     const double lam = tab.lam[b];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
@@ -856,12 +867,9 @@ __global__ __launch_bounds__(256, PM <= 32 ? 3 : 2) void k_cross_mm(PairSide R, 
         const int cl = 16 * cb + lk + 4 * v;
         constexpr double R2MIN = KIND == 1 ? 1e-300 : 0.0;
         const double r2 = fmax(fma(-2.0, acc[cb][v], sr + nc[cl]), R2MIN);
-        double zc = 0.0, lzc = 0.0;
-        if (b > 0) {
-          zc = Zc[(b - 1) * 64 + cl];
-          if (KIND == 0) lzc = LZc[(b - 1) * 64 + cl];
-        }
-        kf[cb][v] += kval_mm<KIND>(b, r2, lam, zr, zc, lzr, lzc, E);
+        const double zc = zcol[cl];
+        const double lzc = KIND == 0 ? lzcol[cl] : 0.0;
+        kf[cb][v] += kval_nb<KIND>(r2, lam, zr, zc, lzr, lzc, E);
         MM_PAIR_FENCE(cb, v);
       }
   }
@@ -1653,11 +1661,19 @@ hipError_t launch_assembly_persist(int kind, int PM, PairSide S, int64_t npad, i
   }
 }
 
+// k_cross_mm's LDS: the assembly's layout plus the row side's points
+static size_t cross_mm_lds(int PM, int B, int kind) {
+  return (size_t)(mm_layout(PM, B, kind == 0 ? 0 : 1, false).total + 64 * xj_pitch(PM)) *
+         sizeof(double);
+}
+bool cross_mm_lds_ok(int PM, int B, int kind) { return cross_mm_lds(PM, B, kind) <= 160 * 1024; }
+
 template <int PM>
 static hipError_t cross_mm_pm(int kind, PairSide R, PairSide C, int B, int ZS, TabView tab, int b0,
                               int b1, double *out, int64_t ld, hipStream_t st) {
   if (R.n <= 0 || C.n <= 0 || b1 <= b0) return hipSuccess;
-  const size_t lds = (size_t)mm_layout(PM, B, kind == 0 ? 0 : 1, false).total * sizeof(double);
+  const size_t lds = cross_mm_lds(PM, B, kind);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
   const void *f = kind == 0 ? (const void *)k_cross_mm<PM, 0> : (const void *)k_cross_mm<PM, 1>;
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

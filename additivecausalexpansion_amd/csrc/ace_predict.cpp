@@ -40,6 +40,10 @@ namespace {
 // test points per chunk: K_xX and T' are n x 8192 each (4.3 GB at n = 65536)
 constexpr int64_t NXC = 8192;
 
+struct PredScratch {
+  DBuf K, T, Kxx;
+};
+
 // out (n x k, ld n) = A^-1 V, summed over the simulated ranks; on an RCCL
 // rank the caller all-reduces (the partial holds this rank's entries only).
 void symm_resident(ace_model *m, const double *V, int64_t ldv, bool vt, int64_t k, double *out,
@@ -93,7 +97,15 @@ void pred_pipeline(const PredOps &op, int64_t nx, bool marginal, const double *Z
   ace_ctx *ctx = op.ctx;
   hipStream_t st = ctx->stream;
   const int64_t n = op.n;
-  DBuf dKc, dT, dad, dkd, dtmp, dW3, dS3, dU3, dKmxx, dq3, dvt, ddot;
+  // the large buffers live in the context between calls (ctx->pred_state);
+  // this reference keeps them valid if an allocation failure drops it there
+  std::shared_ptr<PredScratch> ps = std::static_pointer_cast<PredScratch>(ctx->pred_state);
+  if (!ps) {
+    ps = std::make_shared<PredScratch>();
+    ctx->pred_state = ps;
+  }
+  DBuf &dKc = ps->K, &dT = ps->T, &dKmxx = ps->Kxx;
+  DBuf dad, dkd, dtmp, dW3, dS3, dU3, dq3, dvt, ddot;
   const int64_t chunk = std::min<int64_t>(NXC, nx);
   alloc(ctx, dT, (size_t)(chunk * n) * sizeof(double), "alloc T");
   alloc(ctx, dad, (size_t)(2 * nx) * sizeof(double), "alloc sums");  // [a | d]

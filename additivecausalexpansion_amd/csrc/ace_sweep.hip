@@ -154,6 +154,15 @@ __device__ __forceinline__ void pivot_sweep(double (&v)[SUB / NW], PivotLds<NW> 
 #ifndef ACE_PIVOT_BLK
 #define ACE_PIVOT_BLK 1
 #endif
+#ifndef ACE_PGEMM_HEAD_DEPTH
+#define ACE_PGEMM_HEAD_DEPTH 1
+#endif
+#ifndef ACE_BULK_RESERVE_N
+#define ACE_BULK_RESERVE_N 8192
+#endif
+#ifndef ACE_PGEMM_HEADQ
+#define ACE_PGEMM_HEADQ 1
+#endif
 
 // broadcast lane T of every 16-lane row to the row (64-bit DPP)
 template <int T>
@@ -346,12 +355,14 @@ __global__ __launch_bounds__(64 * NW) void k_pivot(const double *__restrict__ S,
   double v[CW];
 #pragma unroll
   for (int q = 0; q < CW; ++q) v[q] = S[lane + (s * SUB + CW * w + q) * SUB];
+  ACE_WGT_MARK(0);
   if constexpr (ACE_PIVOT_BLK && NW == 4) {
     __shared__ double M[SUB][SUB + 2];
     pivot_sweep_blk<SUB + 2>(v, M, L.pv, tid);
   } else {
     pivot_sweep<NW>(v, L, tid);
   }
+  ACE_WGT_MARK(1);
   pivot_store<NW>(v, L.pv, tid, SW, piv, p0, flag);
 }
 
@@ -588,12 +599,40 @@ __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int
 #pragma unroll
     for (int ctc = 0; ctc < 4; ++ctc) accs[ctc] = d4{0.0, 0.0, 0.0, 0.0};
   }
-  for (int e = tid; e < SUB * SUB; e += 256) {
-    const int a = e & 63, b = e >> 6;
-    sSW[b][a] = SW[a + b * SUB];
-    if (cc != s) sSt[b][a] = S[a + (cc * SUB + b) * SUB];
+  // Every global load of the prologue is issued before the first LDS store:
+  // the inputs are the previous chain launch's outputs, so this is one
+  // memory round trip instead of one per staging-loop turn (C1 marks: 9.2 us
+  // from entry to the staged operands, profiles/r05_v3_wgt_c1.txt)
+  double bw[SUB / 4];
+  if (!pivrows) {
+    const double *src = s == 0 ? W + row : Xb + (int64_t)(s & 1) * CH + brow;
+    const int64_t lds = s == 0 ? ldp : NB;
+#pragma unroll
+    for (int kk = 0; kk < SUB / 4; ++kk) bw[kk] = src[(int64_t)(4 * kk + lk) * lds];
+  }
+  {
+    constexpr int NQ = SUB * SUB / 512;  // double2 per thread and matrix
+    double2 tw[NQ], ts[NQ];
+    const double *Sc = S + (int64_t)cc * SUB * SUB;  // S(a, 64 cc + b) = Sc[a + 64 b]
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int e = 2 * (tid + 256 * q);
+      tw[q] = *reinterpret_cast<const double2 *>(SW + e);
+      if (cc != s) ts[q] = *reinterpret_cast<const double2 *>(Sc + e);
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int e = 2 * (tid + 256 * q), a = e & 63, b = e >> 6;
+      sSW[b][a] = tw[q].x;
+      sSW[b][a + 1] = tw[q].y;
+      if (cc != s) {
+        sSt[b][a] = ts[q].x;
+        sSt[b][a + 1] = ts[q].y;
+      }
+    }
   }
   __syncthreads();
+  ACE_WGT_MARK(0);
   d4 acc1[4];
   if (pivrows) {
 #pragma unroll
@@ -603,11 +642,6 @@ __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int
   } else {
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) acc1[ct] = d4{0.0, 0.0, 0.0, 0.0};
-    const double *src = s == 0 ? W + row : Xb + (int64_t)(s & 1) * CH + brow;
-    const int64_t lds = s == 0 ? ldp : NB;
-    double bw[SUB / 4];
-#pragma unroll
-    for (int kk = 0; kk < SUB / 4; ++kk) bw[kk] = src[(int64_t)(4 * kk + lk) * lds];
 #pragma unroll
     for (int kk = 0; kk < SUB / 4; ++kk) {
 #pragma unroll
@@ -649,6 +683,7 @@ __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int
       if (xnext) xnext[(int64_t)c * NB] = acc[j];
     }
   }
+  ACE_WGT_MARK(1);
   if (!fusepiv) return;
   // D_{s+1}: accs[ctc][j] = D(srow, 16 ctc + lk + 4 j) -> lane = row layout
   __syncthreads();  // every wave is done with sSW (phase 1)
@@ -661,10 +696,13 @@ __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int
 #pragma unroll
   for (int q = 0; q < SUB / 4; ++q) v[q] = sSW[16 * w + q][lane];
 #if ACE_PIVOT_BLK
+  ACE_WGT_MARK(2);
   pivot_sweep_blk<SLD>(v, sSt, PL.pv, tid);  // sSt is free (the update phase is done)
 #else
+  ACE_WGT_MARK(2);
   pivot_sweep<4>(v, PL, tid);
 #endif
+  ACE_WGT_MARK(3);
   pivot_store<4>(v, PL.pv, tid, SWn, piv, k0 + (int64_t)(s + 1) * SUB, flag);
 }
 
@@ -1426,7 +1464,7 @@ __device__ __forceinline__ const double *psel(const double *const (&p)[4], int j
 // SH (sharded): A holds the rank's block-cyclic columns (tile column C0 at
 // local column lcol(C0, G)) and the operands are swapped, R = Pn, C = W (W
 // is only computed for the rows the rank consumes, its own columns).
-template <bool SH>
+template <bool SH, bool OPQ = false>
 __device__ __forceinline__ void update_multi_tile(int I, int J, double (&sW)[2][BK][LDL],
                                                   double (&sP)[2][BK][LDL], double *__restrict__ A,
                                                   int64_t ld, const PanelSet &ps, int npan,
@@ -1440,7 +1478,11 @@ __device__ __forceinline__ void update_multi_tile(int I, int J, double (&sW)[2][
   const int jm = bi > bj ? bi : bj;  // the latest group block holding the tile
   const int64_t R0 = (int64_t)I * UT, C0 = (int64_t)J * UT;
   const int64_t L0 = SH ? lcol(C0, G) : C0;  // A's local column of the tile
-  const int tid = threadIdx.x;
+  int tid = threadIdx.x;
+  // OPQ (the persistent loop of k_update_multi_r): the lane index opaque per
+  // tile, so the compiler does not hoist every lane-derived address out of
+  // the tile loop (162 VGPRs, one workgroup per CU, without it)
+  if (OPQ) __asm__ volatile("" : "+v"(tid));
   const double *const(&WS)[4] = SH ? ps.C : ps.R;  // the W operands
 
   if (jm == npan - 1) {  // the last block: W of the last step
@@ -1637,6 +1679,88 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_multi(double *__restrict
   }
   if (kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT))) return;
   update_multi_tile<SH>(I, J, sW, sP, A, ld, ps, npan, ldp, ka0, go, G);
+}
+
+// Small n (run_sweep_heads with b.breserve > 0): the bulk launch as a
+// persistent work queue that leaves `reserve` CUs of every shader engine to
+// the panel chains.  At n = 4096 a bulk launch is short beside the chains,
+// but while it runs it holds every CU slot (two 512-thread workgroups of
+// 128 VGPRs per CU), so each chain launch issued meanwhile waited for its end
+// (C1 trace: a 33-us k_update_q took 171 us; a plain launch split into
+// smaller grids only serialised the bulk, profiles/r05_v3_ab_c1_bulkcap.txt).
+// The reservation protocol is k_asm_mm_q's: the first workgroups to land on
+// the first `reserve` CUs of an engine claim them and leave (at most a
+// quarter of the grid per reserved CU), everyone else takes tiles from
+// queue[0] until the list is done -- every workgroup reaches the exit.  Each
+// tile is k_update_multi's (bit-identical).  queue: [next, leavers, 2 x 32
+// CU claims].
+template <bool SH>
+__global__ __launch_bounds__(UTHREADS, 2) void k_update_multi_r(double *__restrict__ A, int64_t ld,
+                                                                PanelSet ps, int npan, int64_t ldp,
+                                                                int64_t ka0, int kx0, int kx1,
+                                                                const Tile *__restrict__ tiles,
+                                                                int64_t ntiles,
+                                                                int *__restrict__ queue,
+                                                                int reserve) {
+  ACE_WGT(5, gridDim.x < 4096 || blockIdx.x % 32 == 0);
+  __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
+  __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
+  __shared__ int next;
+  constexpr int KT = NB / UT;
+  if (reserve > 0) {
+    if (threadIdx.x == 0) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);        // HW_REG_HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7;  // HW_REG_XCC_ID
+      const unsigned se = (hw >> 13) & 3;
+      const int key = (int)((hw >> 8) & 0xff) + 1;  // cu [11:8], sh [12], se [15:13]
+      int mine = 0;
+      for (int r = 0; r < reserve && !mine; ++r) {
+        const int old = atomicCAS(queue + 2 + 2 * (4 * xcc + se) + r, 0, key);
+        mine = old == 0 || old == key;
+      }
+      next = mine ? (atomicAdd(queue + 1, 1) < (int)gridDim.x * reserve / 4) : 0;
+    }
+    __syncthreads();
+    if (next) return;  // the whole workgroup (one CU)
+    __syncthreads();
+  }
+  for (;;) {
+    if (threadIdx.x == 0) next = atomicAdd(queue, 1);
+    __syncthreads();  // also: every wave is done with the previous tile's LDS
+    const int64_t idx = next;
+    __syncthreads();
+    if (idx >= ntiles) break;
+    const Tile tt = tiles[idx];
+    const int I = tt.I, J = tt.J;
+    if (I < 0) continue;  // padding of the XCD order
+    if (kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT))) continue;
+    update_multi_tile<SH, true>(I, J, sW, sP, A, ld, ps, npan, ldp, ka0,
+                                GatherOut{nullptr, nullptr, nullptr, -1, 0}, 1);
+  }
+}
+
+// CUs per shader engine a small-n bulk launch leaves to the panel chains
+// (k_update_multi_r): ACE_BULK_RESERVE (0 .. 2) overrides; default 1 up to
+// n = ACE_BULK_RESERVE_N, none above (there the bulk launches are the
+// critical path and need every CU).
+bool q_first(int64_t naug) {
+  static int v = -2;
+  if (v == -2) {
+    const char *e = getenv("ACE_QFIRST");
+    v = e ? (atoi(e) != 0) : -1;
+  }
+  if (v >= 0) return v != 0;
+  return naug <= ACE_BULK_RESERVE_N + AUG;
+}
+
+int bulk_reserve(int64_t naug) {
+  static int v = -2;
+  if (v == -2) {
+    const char *e = getenv("ACE_BULK_RESERVE");
+    v = e ? std::max(0, std::min(2, atoi(e))) : -1;
+  }
+  if (v >= 0) return v;
+  return naug <= ACE_BULK_RESERVE_N + AUG ? 1 : 0;
 }
 
 // Side stream, merged schedule: wait until *cnt >= target (the merged bulk
@@ -1883,6 +2007,7 @@ __global__ __launch_bounds__(256, 4) void k_update_q(double *__restrict__ A, int
   }
 #undef UQ_LOAD
 #undef UQ_STAGE
+  ACE_WGT_MARK(0);
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
@@ -1923,9 +2048,105 @@ __global__ __launch_bounds__(256, 4) void k_update_q(double *__restrict__ A, int
     double v[SUB / 4];
 #pragma unroll
     for (int q = 0; q < SUB / 4; ++q) v[q] = M[lane][16 * wv + q];
+    ACE_WGT_MARK(1);
     pivot_sweep_blk<SUB + 2>(v, M, pv, tid);
+    ACE_WGT_MARK(2);
     pivot_store<4>(v, pv, tid, pivSW, piv, go.k0, flag);
   }
+}
+
+// The head path's panel GEMM (run_sweep_heads) on 64 x 64 quarters of the
+// 128-tiles: W_I,J = Pn_I W_kk[:, J] as k_panel_gemm_t, a quarter of its work
+// per 256-thread workgroup.  The head launches hold few tiles (the rows of
+// the next group's blocks) and k_panel_gemm_t's 8.4 MFLOP per workgroup is a
+// CU's MFMA peak for ~27 us (C1 marks: K loop 32 us); quartered, four times
+// the CUs share it.  Operand roles (A from W_kk, B from Pn), k order and the
+// zero start are k_panel_gemm_t's: bit-identical.  Grid: (64-row blocks of
+// row tiles [rt0, rt1), NB / 64 column blocks); k_update_q's two-deep load
+// pipeline.
+__global__ __launch_bounds__(256, 4) void k_panel_gemm_q(double *__restrict__ W,
+                                                       const double *__restrict__ Pn,
+                                                       int64_t ldp, int64_t k0, int rt0) {
+  ACE_WGT(3, true);
+  __shared__ __attribute__((aligned(16))) double sW[2][BK][XL];  // Pn rows of the quarter
+  __shared__ __attribute__((aligned(16))) double sP[2][BK][XL];  // W_kk rows c
+  const int64_t R0 = (int64_t)rt0 * UT + (int64_t)blockIdx.x * XT, C0 = (int64_t)blockIdx.y * XT;
+  if (R0 >= k0 && R0 < k0 + NB) return;  // pivot rows are already final
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int wr = wv & 1, wc = wv >> 1;  // rows 32*wr.., cols 32*wc..
+  const int lr = lane & 15, lk = lane >> 4;
+  const int sk = tid >> 4, sm = (tid & 15) * SM64;  // 2nd half at sm + SH64
+  const double *gW = Pn + (R0 + sm) + (int64_t)sk * ldp;
+  const double *gP = W + (k0 + C0 + sm) + (int64_t)sk * ldp;  // W_kk(c, k) = W[k0 + c, k]
+  d4 acc[2][2];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) acc[ci][ri] = d4{0.0, 0.0, 0.0, 0.0};
+  double2 w00, w01, p00, p01, w10, w11, p10, p11;
+#define PQ_LOAD(W0, W1, P0, P1, CH)                                               \
+  do {                                                                            \
+    const int64_t off_ = (int64_t)(CH) * BK * ldp;                                \
+    W0 = *reinterpret_cast<const double2 *>(gW + off_);                           \
+    W1 = *reinterpret_cast<const double2 *>(gW + off_ + SH64);                    \
+    P0 = *reinterpret_cast<const double2 *>(gP + off_);                           \
+    P1 = *reinterpret_cast<const double2 *>(gP + off_ + SH64);                    \
+  } while (0)
+#define PQ_STAGE(W0, W1, P0, P1, BUF)                                             \
+  do {                                                                            \
+    *reinterpret_cast<double2 *>(&sW[BUF][sk][sm]) = W0;                          \
+    *reinterpret_cast<double2 *>(&sW[BUF][sk][sm + SH64]) = W1;                   \
+    *reinterpret_cast<double2 *>(&sP[BUF][sk][sm]) = P0;                          \
+    *reinterpret_cast<double2 *>(&sP[BUF][sk][sm + SH64]) = P1;                   \
+  } while (0)
+  auto mma = [&](int cur) {
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double a[2], b[2];
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci) a[ci] = sP[cur][4 * kk + lk][32 * wc + 16 * ci + lr];
+#pragma unroll
+      for (int ri = 0; ri < 2; ++ri) b[ri] = sW[cur][4 * kk + lk][32 * wr + 16 * ri + lr];
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+        for (int ri = 0; ri < 2; ++ri)
+          acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
+    }
+  };
+  static_assert(NCH % 2 == 0 && NCH >= 4, "two chunks per pipeline turn");
+  PQ_LOAD(w00, w01, p00, p01, 0);
+  PQ_STAGE(w00, w01, p00, p01, 0);
+  PQ_LOAD(w10, w11, p10, p11, 1);
+  PQ_LOAD(w00, w01, p00, p01, 2);
+  __syncthreads();
+  ACE_WGT_MARK(0);
+#pragma unroll 1
+  for (int ch = 0; ch < NCH; ch += 2) {
+    mma(0);
+    PQ_STAGE(w10, w11, p10, p11, 1);
+    if (ch + 3 < NCH) PQ_LOAD(w10, w11, p10, p11, ch + 3);
+    __syncthreads();
+    mma(1);
+    if (ch + 2 < NCH) {
+      PQ_STAGE(w00, w01, p00, p01, 0);
+      if (ch + 4 < NCH) PQ_LOAD(w00, w01, p00, p01, ch + 4);
+    }
+    __syncthreads();
+  }
+#undef PQ_LOAD
+#undef PQ_STAGE
+  ACE_WGT_MARK(1);
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) {
+      const int64_t rr = R0 + 32 * wr + 16 * ri + lr;
+      const int64_t c = C0 + 32 * wc + 16 * ci + lk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) W[rr + (c + 4 * j) * ldp] = acc[ci][ri][j];
+    }
 }
 
 // ---------------------------------------------------------------- sharded panel
@@ -2894,21 +3115,30 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   auto pgemm = [&](int k, int r0, int r1, bool head, hipStream_t s_) {
     const int n = head ? r1 - r0 : (int)nT - (r1 - r0);
     if (n <= 0) return;
-    // the head rows (few workgroups, latency-bound): two chunks in flight
-    if (head)
+    // ACE_PGEMM_HEAD_DEPTH=2 (A/B build): the head rows with two chunks in
+    // flight.  It needs 132 VGPRs: a wave of it fits on a SIMD only after two
+    // of the bulk launch's 128-VGPR waves have left, so under the bulk launch
+    // the head GEMM starves (C2 +4.4 ms same-box, profiles/r05_v3_ab_c2.txt)
+    if (head && ACE_PGEMM_HEAD_DEPTH == 2)
       hipLaunchKernelGGL(k_panel_gemm_t<2>, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, s_,
                          b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, 1, 0, r0, 1 << 30,
                          1 << 30);
+    else if (head && ACE_PGEMM_HEADQ)
+      hipLaunchKernelGGL(k_panel_gemm_q, dim3((unsigned)(n * (UT / XT)), NB / XT), dim3(256), 0, s_,
+                         b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, r0);
     else
-    hipLaunchKernelGGL(k_panel_gemm_t<1>, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, s_,
-                       b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, 1, 0, head ? r0 : 0,
-                       head ? 1 << 30 : r0, head ? 1 << 30 : r1);
+      hipLaunchKernelGGL(k_panel_gemm_t<1>, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, s_,
+                         b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, 1, 0, head ? r0 : 0,
+                         head ? 1 << 30 : r0, head ? 1 << 30 : r1);
   };
   auto chain = [&](int k, hipStream_t s_) {  // [pivot +] sub-steps of panel k (gathered)
     panel_chain(b.P[slot(k)], b.W[slot(k)], b.ld, (int64_t)k * NB, b.SW, b.S, b.piv, b.flag, 1, 0,
                 s_, fused_pivot && k > 0, nullptr, true);
   };
   hipError_t e;
+  if (b.bq && b.breserve > 0 &&
+      (e = hipMemsetAsync(b.bq, 0, (size_t)ng * BQ_INTS * sizeof(int), st)) != hipSuccess)
+    return e;  // the bulk queues (k_update_multi_r), before any bulk launch
   if (!sy->ready_recorded) {
     e = hipEventRecord(sy->ev[2 * steps], st);  // inputs ready
     if (e != hipSuccess) return e;
@@ -2921,17 +3151,37 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   // for every sub-step, 112 registers, 73 KB of LDS -- did not get group 0's
   // chains beside the assembly's second part: neutral,
   // profiles/r03_v5_heads_ab.txt.)
-  auto produce = [&](int G) -> hipError_t {
-    const int kb = Z * G, zb = zsize(G);
-    const Tile *tl;
-    int64_t nt;
+  // Small n (ACE_QFIRST, default up to n = ACE_BULK_RESERVE_N): at a group
+  // boundary the next group's Q launch (its head square, K = Z NB) runs
+  // alone -- the rest of the cross (side2) and the bulk launch (main) wait
+  // for it.  There the chain is the critical path and the bulk is short; Q
+  // beside both took 163 us instead of ~40 (C1 trace, profiles/r05_v4_*).
+  const bool qfirst = q_first(naug);
+  auto Eq = [&](int G) { return sy->ev[2 * steps + 1 + 2 * G]; };  // group G's Q done
+  // group G's first head launch (k_gather / Q); the rest by produce(G)
+  auto produce_q = [&](int G) -> hipError_t {
+    const int kb = Z * G;
     if (G == 0) {
       hipLaunchKernelGGL(k_gather<false>, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, side,
                          b.A, b.ld, (int64_t)0, b.P[slot(0)], b.W[slot(0)], b.ld, b.S[0], nullptr,
                          nullptr, nullptr);
     } else {
+      const Tile *tl;
+      int64_t nt;
       list(G, 0, tl, nt);
       qupd(zsize(G - 1), Z * (G - 1), tl, nt, gout(kb), side);  // Q
+    }
+    return qfirst ? hipEventRecord(Eq(G), side) : hipSuccess;
+  };
+  auto produce = [&](int G) -> hipError_t {
+    const int kb = Z * G, zb = zsize(G);
+    const Tile *tl;
+    int64_t nt;
+    if (G > 0) {
+      if (qfirst) {
+        const hipError_t q = hipStreamWaitEvent(side2, Eq(G), 0);
+        if (q != hipSuccess) return q;
+      }
       list(G, 1, tl, nt);
       upd(zsize(G - 1), Z * (G - 1), -1, -1, tl, nt, gout(kb), side2);  // the rest of the cross
     }
@@ -2982,7 +3232,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   if ((e = hipStreamWaitEvent(side2, sy->tail_after ? sy->tail_after : sy->ev[2 * steps], 0)) !=
       hipSuccess)
     return e;
-  if ((e = produce(0)) != hipSuccess) return e;
+  if ((e = produce_q(0)) != hipSuccess || (e = produce(0)) != hipSuccess) return e;
   int used = 0;
   for (int g = 0; g < ng; ++g) {
     const int kg = Z * g;
@@ -2994,14 +3244,29 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
       if ((e = hipEventRecord(sy->ev[2 * g + 1], st)) != hipSuccess) return e;  // bulk g-1 done
       if ((e = hipStreamWaitEvent(side, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
       if ((e = hipStreamWaitEvent(side2, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
-      if ((e = produce(g + 1)) != hipSuccess) return e;
+      if ((e = produce_q(g + 1)) != hipSuccess) return e;
+      if (qfirst && (e = hipStreamWaitEvent(st, Eq(g + 1), 0)) != hipSuccess) return e;
     }
+    // (the bulk launch is enqueued before the rest of group g+1's lookahead:
+    // at small n the host's enqueue of ~40 launches, not the device, used to
+    // hold it back by ~0.5 ms; the device order is the same either way)
     const bool timed = tm && tm->ev && used + 2 <= tm->nev;
     if (timed) (void)hipEventRecord(tm->ev[used], st);
     const int64_t grid = b.gorder ? b.glen : (b.order ? b.norder : (int64_t)nT * (nT + 1) / 2);
     const Tile *ord = b.gorder ? b.gorder + (int64_t)g * b.glen : b.order;
     const int kx0 = more ? kb : -1, kx1 = more ? kb + zb : -1;
-    upd(zsize(g), kg, kx0, kx1, ord, grid, no_gather(), st);
+    if (b.bq && b.breserve > 0 && ord && zsize(g) > 2) {
+      PanelSet ps;
+      for (int j = 0; j < 4; ++j) {
+        ps.R[j] = j < zsize(g) ? b.W[slot(kg + j)] : nullptr;
+        ps.C[j] = j < zsize(g) ? b.P[slot(kg + j)] : nullptr;
+      }
+      hipLaunchKernelGGL(k_update_multi_r<false>, dim3(2 * 256), dim3(UTHREADS), 0, st, b.A, b.ld,
+                         ps, zsize(g), b.ld, (int64_t)kg * NB, kx0, kx1, ord, grid,
+                         b.bq + (int64_t)g * BQ_INTS, b.breserve);
+    } else {
+      upd(zsize(g), kg, kx0, kx1, ord, grid, no_gather(), st);
+    }
     if (timed) {
       (void)hipEventRecord(tm->ev[used + 1], st);
       if (tm->flops)
@@ -3009,6 +3274,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
             update_gemm_tiles_group(naug, (int64_t)kg * NB, zsize(g), kx0, kx1) * 2.0 * UT * UT * NB;
       used += 2;
     }
+    if (more && (e = produce(g + 1)) != hipSuccess) return e;
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (tm && tm->used) *tm->used = used;

@@ -492,7 +492,11 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     1100, 3+3 / 4+2 at 1500, 3+3+3+2 / 4+4+3 at 2600) are bit-identical too,
     with and without the fused gather, the second side stream and lookahead,
     and so is the head / tail split of the group lookahead (ACE_HEADS=1 at
-    Z = 2, 3, 4)."""
+    Z = 2, 3, 4), with its small-n bulk launches as a persistent queue that
+    leaves 1 (default below n = 8192) or 2 CUs per engine to the chains, or
+    as the plain grid (ACE_BULK_RESERVE=0), and with the next group's Q launch
+    run before (default below n = 8192) or beside (ACE_QFIRST=0) the bulk
+    launch and the rest of the cross."""
     import os
     import subprocess
     import sys
@@ -528,7 +532,11 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
                 "heads4": {"ACE_GROUP": "4", "ACE_HEADS": "1"}, "default": {},
                 "heads4_pair": {"ACE_GROUP": "4", "ACE_HEADS": "1", "ACE_MULTI2": "0"},
                 "heads4_q128": {"ACE_GROUP": "4", "ACE_HEADS": "1", "ACE_HEADQ": "0"},
-                "heads3_q128": {"ACE_GROUP": "3", "ACE_HEADS": "1", "ACE_HEADQ": "0"}}
+                "heads3_q128": {"ACE_GROUP": "3", "ACE_HEADS": "1", "ACE_HEADQ": "0"},
+                "heads4_unreserved": {"ACE_BULK_RESERVE": "0"},
+                "heads4_reserve2": {"ACE_BULK_RESERVE": "2"},
+                "heads4_q_beside": {"ACE_QFIRST": "0"},
+                "heads4_q_beside_unreserved": {"ACE_QFIRST": "0", "ACE_BULK_RESERVE": "0"}}
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)

@@ -1,6 +1,6 @@
 """Per-workgroup timeline of the sweep's kernels in one C2 evaluation, from a
 -DACE_DIAG_WGTIME build (tools/build_variant.sh wgt -DACE_DIAG_WGTIME):
-  ACE_LIB_PATH=tools/libace_wgt.so python tools/wg_timeline.py [n]
+  ACE_LIB_PATH=ab/libace_wgt.so python tools/wg_timeline.py [n [p B kernel]]
 
 For every launch of the chain kernels (k_pivot, k_panel_split) and the head
 launches (k_panel_gemm_t, k_update_q): the launch span (first workgroup
@@ -74,11 +74,35 @@ def wg_end(r):
     return max(ends) if ends else int(r[2])
 
 
+def phases(ls, kid, label):
+    """Median per-phase durations of kid's workgroups (wave 0's marks), per
+    set of marks present: entry -> mark i -> ... -> exit."""
+    groups = defaultdict(list)
+    for k, grid, rs in ls:
+        if k != kid:
+            continue
+        for r in rs:
+            marks = [(i, int(r[12 + i])) for i in range(4) if int(r[12 + i])]
+            key = tuple(i for i, _ in marks)
+            ts = [int(r[2])] + [t for _, t in marks] + [wg_end(r)]
+            groups[key].append(np.diff(ts) * TICK_US)
+    for key, rows in sorted(groups.items()):
+        a = np.asarray(rows)
+        names = ["entry"] + ["m%d" % i for i in key] + ["exit"]
+        segs = "  ".join("%s->%s %.2f" % (names[i], names[i + 1], np.median(a[:, i]))
+                         for i in range(a.shape[1]))
+        print("  %-14s marks %-10s %5d wgs  total %.2f us | %s" % (
+            label, ",".join(map(str, key)) or "-", len(a), np.median(a.sum(axis=1)), segs))
+
+
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+    p = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    B = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+    kern = sys.argv[4] if len(sys.argv) > 4 else "Matern32"
     L = lib()
-    y, X, Z, th, sy = make_problem(n, 20, 10, seed=5)
-    m = ace.DeviceModel("Matern32", n, 20, 10)
+    y, X, Z, th, sy = make_problem(n, p, B, seed=5)
+    m = ace.DeviceModel(kern, n, p, B)
     m.set_data(y, X, Z, sy)
     theta = th.copy()
     for it in (1, 2):
@@ -139,6 +163,10 @@ def main():
               " | prologue share of workgroup time %.1f %% (%d tiles)" % (
                   np.median(a[:, 0]), a[:, 0].mean(), np.median(a[:, 1]), np.median(a[:, 2]),
                   100.0 * a[:, 0].sum() / tot.sum(), len(a)))
+    print("per-workgroup phases (wave 0 marks; us, medians):")
+    phases(ls, 1, "pivot")
+    phases(ls, 2, "panel_split")
+    phases(ls, 4, "update_q")
     bulks = sorted((min(int(r[2]) for r in rs) - t0) * TICK_US for k, g, rs in ls
                    if k == 5 and g == bulk_grid)
     if len(bulks) > 9:
