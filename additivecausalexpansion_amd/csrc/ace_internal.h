@@ -303,7 +303,19 @@ hipError_t shard_update_main(const ShardSweep &b, int k, int buf, int kx, hipStr
 // step kpack (what shard_pack(kpack) would copy; G > 1) and the rank's own
 // rows of panel kpack (slot kpack % nslot)
 hipError_t shard_update_group(const ShardSweep &b, int kb, int npan, int nslot, int kx0, int kx1,
-                              const Tile *tiles, int64_t nt, hipStream_t st, int kpack = -1);
+                              const Tile *tiles, int64_t nt, hipStream_t st, int kpack = -1,
+                              double *lowp = nullptr, int64_t lr0 = 0, int64_t hh = -1);
+// the head schedule's pieces (run_sweep_sharded_heads): a row range of the
+// owner's column block (+ row pieces) into an exchange buffer; a row range of
+// panel k from one; the pivot sub-steps alone; the head or tail panel GEMM
+hipError_t shard_pack_part(const ShardSweep &b, int k, int64_t i_lo, int64_t i_hi, double *low,
+                           int64_t lr0, int64_t hh, bool rows, hipStream_t st);
+hipError_t shard_unpack_part(const ShardSweep &b, int k, int buf, int64_t i_lo, int64_t i_hi,
+                             const double *low, int64_t lr0, int64_t hh, bool own_done,
+                             hipStream_t st);
+hipError_t shard_chain(const ShardSweep &b, int k, int buf, hipStream_t st);
+hipError_t shard_pgemm(const ShardSweep &b, int k, int buf, int rt_lo, int rt_hi, bool head,
+                       hipStream_t st);
 
 // ---- small helpers -----------------------------------------------------------
 // AUG rows of columns j < n: row 0 = y (zeros if y is null), row 1 = 1

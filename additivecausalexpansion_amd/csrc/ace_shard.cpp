@@ -58,6 +58,9 @@ struct Rccl {
   ncclResult_t (*GroupStart)() = nullptr;
   ncclResult_t (*GroupEnd)() = nullptr;
   const char *(*GetErrorString)(ncclResult_t) = nullptr;
+  // optional: the head schedule's second communicator (null: that schedule
+  // is not used over RCCL)
+  ncclResult_t (*CommSplit)(ncclComm_t, int, int, ncclComm_t *, ncclConfig_t *) = nullptr;
 
   Rccl() {
     // an RCCL already in the process (e.g. PyTorch's) is reused by soname
@@ -83,6 +86,7 @@ struct Rccl {
     ACE_SYM(GroupEnd, "ncclGroupEnd");
     ACE_SYM(GetErrorString, "ncclGetErrorString");
 #undef ACE_SYM
+    CommSplit = reinterpret_cast<decltype(CommSplit)>(dlsym(h, "ncclCommSplit"));
     ok = true;
   }
 };
@@ -160,6 +164,10 @@ struct RankState {
   // group g's pair cross, block 2 g first, then block 2 g + 1 minus block 2 g
   DBuf tx, tp;
   std::vector<int64_t> xoff, poff;
+  // head schedule: the own tiles of group_head_tiles' lists (device, host
+  // offsets hoff[G 2Z + m]) and the head part's exchange buffer (Z NB x NB)
+  DBuf th, lowh;
+  std::vector<int64_t> hoff;
   DBuf y, tab, alpha, scal, gpart, gwork, red, sums, augvec;
   SideBufs side;
 };
@@ -183,6 +191,11 @@ struct ShardModel {
   ace_comm_ops ops{};
   HostStage stage;  // pinned staging of the host-callback collectives
   ncclComm_t comm = nullptr;
+  // head schedule (run_sweep_sharded_heads): its tail exchanges run on a
+  // second communicator, so they are never ordered behind the head path's
+  // (one communicator's collectives execute in issue order on any stream)
+  bool heads = false;
+  ncclComm_t comm2 = nullptr;
   std::vector<std::unique_ptr<RankState>> ranks;  // 1 (RCCL) or G (simulated)
   DBuf vote;                                       // shard_any: one double
   std::vector<hipEvent_t> ev;                      // lookahead events
@@ -199,6 +212,7 @@ struct ShardModel {
       if (ev_asm[j]) (void)hipEventDestroy(ev_asm[j]);
       if (ev_grad[j]) (void)hipEventDestroy(ev_grad[j]);
     }
+    if (comm2) (void)rccl().CommDestroy(comm2);
     if (comm) (void)rccl().CommDestroy(comm);
   }
 };
@@ -327,6 +341,35 @@ void build_cross_lists(ace_ctx *ctx, RankState &R, int64_t naug, int steps, int 
   upload_tiles(ctx, R.tp, pr);
 }
 
+// The head schedule's tile lists on rank R: group_head_tiles' lists (the
+// single-GPU head / tail split, ace_sweep.hip) restricted to the rank's own
+// tiles (column block owned), offsets hoff[G 2Z + m].
+void build_head_lists(ace_ctx *ctx, RankState &R, int64_t naug, int steps, int G, int Z) {
+  constexpr int KT = NB / UT;
+  std::vector<int64_t> off;
+  const std::vector<Tile> all = group_head_tiles(naug, steps, Z, off);
+  std::vector<Tile> mine;
+  R.hoff.assign(off.size(), 0);
+  for (size_t m = 0; m + 1 < off.size(); ++m) {
+    for (int64_t i = off[m]; i < off[m + 1]; ++i) {
+      const Tile &t = all[(size_t)i];
+      if (t.I >= 0 && (t.J / KT) % G == R.r) mine.push_back(t);
+    }
+    R.hoff[m + 1] = (int64_t)mine.size();
+  }
+  upload_tiles(ctx, R.th, mine);
+}
+
+// ACE_SHARD_HEADS=0: the sharded sweep keeps the group schedule without the
+// head / tail split (run_sweep_sharded); default on
+bool shard_heads_on() {
+  static const bool v = [] {
+    const char *e = getenv("ACE_SHARD_HEADS");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+
 // ---- collectives over the local ranks -------------------------------------
 // Panel exchange of step k on stream st.
 void exchange(ShardModel &m, int k, hipStream_t st) {
@@ -375,6 +418,59 @@ void exchange(ShardModel &m, int k, hipStream_t st) {
     RankState &R = *Rp;
     if (R.r != root)
       ck(ctx, hipMemcpyAsync(R.low.p, src.low.p, nlow * sizeof(double), hipMemcpyDeviceToDevice, st),
+         "sim broadcast");
+    if (nrow > 0)
+      for (auto &Sp : m.ranks)
+        if (Sp->r != R.r)
+          ck(ctx, hipMemcpyAsync(R.recv.d() + (size_t)Sp->r * nrow, own(*Sp), nrow * sizeof(double),
+                                 hipMemcpyDeviceToDevice, st),
+             "sim all-gather");
+  }
+}
+
+// The head schedule's two exchanges of panel k: head = the owner's column
+// rows [k0, hend) (rows x NB doubles in lowh, broadcast, on the head path's
+// stream); tail = the rows [hend, naug) (in low, broadcast) and the row
+// pieces (all-gather), on the tail path's stream and the second communicator.
+void exchange_part(ShardModel &m, int k, bool head, int64_t rows, hipStream_t st) {
+  ace_ctx *ctx = m.ctx;
+  if (m.G == 1) return;  // one rank: both collectives are the identity
+  const size_t nlow = (size_t)(rows * NB);
+  const size_t nrow = head ? 0 : (size_t)shard_row_slots(k, m.G) * NB * NB;
+  const int root = k % m.G;
+  auto lowp = [&](RankState &R) { return head ? R.lowh.d() : R.low.d(); };
+  auto own = [&](RankState &R) { return R.recv.d() + (size_t)R.r * nrow; };
+  if (m.proxy) {  // the bytes this rank receives, as device copies (timing only)
+    RankState &R = *m.ranks[0];
+    if (R.r != root && nlow > 0) {
+      alloc(ctx, m.proxy_buf, std::max(m.proxy_buf.bytes, nlow * sizeof(double)), "alloc proxy");
+      ck(ctx, hipMemcpyAsync(m.proxy_buf.p, lowp(R), nlow * sizeof(double), hipMemcpyDeviceToDevice, st),
+         "proxy broadcast");
+    }
+    if (nrow > 0)
+      for (int q = 0; q < m.G; ++q)
+        if (q != R.r)
+          ck(ctx, hipMemcpyAsync(R.recv.d() + (size_t)q * nrow, own(R), nrow * sizeof(double),
+                                 hipMemcpyDeviceToDevice, st),
+             "proxy all-gather");
+    return;
+  }
+  if (!m.sim) {
+    RankState &R = *m.ranks[0];
+    ncclComm_t c = head ? m.comm : m.comm2;
+    nck(ctx, rccl().GroupStart(), "ncclGroupStart");
+    if (nlow > 0)
+      nck(ctx, rccl().Broadcast(lowp(R), lowp(R), nlow, ncclDouble, root, c, st), "ncclBroadcast");
+    if (nrow > 0)
+      nck(ctx, rccl().AllGather(own(R), R.recv.p, nrow, ncclDouble, c, st), "ncclAllGather");
+    nck(ctx, rccl().GroupEnd(), "ncclGroupEnd");
+    return;
+  }
+  RankState &src = *m.ranks[(size_t)root];
+  for (auto &Rp : m.ranks) {
+    RankState &R = *Rp;
+    if (R.r != root && nlow > 0)
+      ck(ctx, hipMemcpyAsync(lowp(R), lowp(src), nlow * sizeof(double), hipMemcpyDeviceToDevice, st),
          "sim broadcast");
     if (nrow > 0)
       for (auto &Sp : m.ranks)
@@ -503,10 +599,173 @@ void run_sweep_sharded_steps(ShardModel &m, int which, bool timed) {
 // single-step schedule's MFMA chains in the same order (k_update_multi's
 // per-tile rule): bit-identical to run_sweep_sharded_steps
 // (tests/test_shard_gpu.py).
+// The single-GPU head / tail schedule (run_sweep_heads) on each
+// rank's own tiles, with the exchange split the same way.  Group G = blocks
+// [kb, kb + z), hend = (kb + z) NB:
+//   side (head path): Q over the group's square (own tiles) packs panel kb's
+//     column rows [kb NB, hend) -> head exchange (a broadcast of at most
+//     Z NB x NB doubles from the block's owner) -> unpack -> the pivot
+//     sub-steps -> the panel GEMM of the rows [k0 + NB, hend) -> Q_{j+1}
+//     packs panel k + 1's head rows -> ...
+//   side2 (tail path): the rest of the group's cross packs panel kb's rows
+//     [hend, naug) and the row pieces -> tail exchange (broadcast +
+//     all-gather, second communicator) -> unpack -> [after the sub-steps] the
+//     panel GEMM of the other rows -> [after the head GEMM] T_{j+1} packs
+//     panel k + 1's tail -> ...
+//   main: [ready g, ready2 g] -> the bulk launch of group g.
+// A panel's pivot chain then waits only for its head rows: the full column
+// cross, the row-piece all-gather and the panel GEMM of every other row run
+// beside it.  Every tile sees the same launches' MFMA chains as in
+// run_sweep_heads (the same lists, restricted to the rank's tiles):
+// bit-identical to the single-GPU model (tests/test_shard_gpu.py).
+void run_sweep_sharded_heads(ShardModel &m, int which, bool timed) {
+  ace_ctx *ctx = m.ctx;
+  const int steps = (int)(m.npad / NB);
+  const int Z = m.Z, NS = 2 * Z;
+  const int ng = (steps + Z - 1) / Z;
+  constexpr int KT = NB / UT;
+  const int64_t naug = m.naug;
+  hipStream_t st = ctx->stream, side = ctx->side, side2 = ctx->side2;
+  auto zsize = [&](int g) { return std::min(Z, steps - Z * g); };
+  std::vector<ShardSweep> v;
+  for (auto &R : m.ranks) v.push_back(sweep_view(m, *R, which));
+  auto EV = [&](int i) { return m.ev[(size_t)i]; };
+  const int E_IN = 0;  // recorded by shard_eval: the first group's columns assembled
+  auto E_READY = [&](int g) { return 1 + g; };          // group g's head path done
+  auto E_READY2 = [&](int g) { return 1 + ng + g; };    // group g's tail path done
+  auto E_SP = [&](int k) { return 2 + 3 * ng + 2 * k; };  // panel k's sub-steps done
+  auto E_GH = [&](int k) { return 3 + 3 * ng + 2 * k; };  // panel k's head GEMM done
+  // main, before bulk g: bulk g-1 done and group g's head and tail paths
+  // done -- what group g+1's lists need (its tiles were last touched by bulk
+  // g-1; the W rows of its blocks come from group g's tail panel GEMMs)
+  auto E_PRE = [&](int g) { return 2 + 3 * ng + 2 * steps + g; };
+  auto rec = [&](int i, hipStream_t s_) { ck(ctx, hipEventRecord(EV(i), s_), "event"); };
+  auto wait = [&](hipStream_t s_, int i) { ck(ctx, hipStreamWaitEvent(s_, EV(i), 0), "event wait"); };
+  auto hend_of = [&](int G) { return (int64_t)(Z * G + zsize(G)) * NB; };
+  // own tiles of list m of group G (group_head_tiles' numbering)
+  auto hlist = [&](size_t q, int G, int mm, int64_t &n) {
+    RankState &R = *m.ranks[q];
+    const size_t i = (size_t)G * 2 * Z + (size_t)mm;
+    n = R.hoff[i + 1] - R.hoff[i];
+    return (const Tile *)R.th.p + R.hoff[i];
+  };
+  // a launch on list mm of group G: npan panels from block kb0, packing
+  // panel kp's head (head = true) or tail part
+  auto launch = [&](int G, int mm, int npan, int kb0, int kp, bool head, hipStream_t s_) {
+    const int64_t k0 = (int64_t)kp * NB, he = hend_of(G);
+    for (size_t q = 0; q < v.size(); ++q) {
+      int64_t n;
+      const Tile *tl = hlist(q, G, mm, n);
+      RankState &R = *m.ranks[q];
+      ck(ctx, shard_update_group(v[q], kb0, npan, NS, -1, -1, tl, n, s_, kp,
+                                 head ? R.lowh.d() : R.low.d(), head ? 0 : he - k0,
+                                 head ? he - k0 : naug - he),
+         head ? "shard head update" : "shard tail update");
+    }
+  };
+  // panel k's head rows in: exchange (+ pack when no launch packed them) + unpack
+  auto head_in = [&](int k, int G, bool packed) {
+    const int64_t k0 = (int64_t)k * NB, he = hend_of(G);
+    if (!packed)
+      for (size_t q = 0; q < v.size(); ++q)
+        ck(ctx, shard_pack_part(v[q], k, k0, he, m.ranks[q]->lowh.d(), 0, he - k0, false, side),
+           "shard head pack");
+    exchange_part(m, k, true, he - k0, side);
+    for (size_t q = 0; q < v.size(); ++q)
+      ck(ctx, shard_unpack_part(v[q], k, k % NS, k0, he, m.ranks[q]->lowh.d(), 0, he - k0, packed, side),
+         "shard head unpack");
+  };
+  auto tail_in = [&](int k, int G, bool packed) {
+    const int64_t k0 = (int64_t)k * NB, he = hend_of(G);
+    if (!packed)
+      for (size_t q = 0; q < v.size(); ++q)
+        ck(ctx, shard_pack_part(v[q], k, he, naug, m.ranks[q]->low.d(), he - k0, naug - he, true, side2),
+           "shard tail pack");
+    exchange_part(m, k, false, naug - he, side2);
+    for (size_t q = 0; q < v.size(); ++q) {
+      ck(ctx, shard_unpack_part(v[q], k, k % NS, 0, k0, m.ranks[q]->low.d(), 0, 0, packed, side2),
+         "shard tail unpack");
+      ck(ctx, shard_unpack_part(v[q], k, k % NS, he, naug, m.ranks[q]->low.d(), he - k0, naug - he,
+                                packed, side2),
+         "shard tail unpack");
+    }
+  };
+  // group G's head path (side) and tail path (side2)
+  auto produce = [&](int G) {
+    const int kb = Z * G, zb = zsize(G);
+    const int hT = (int)(hend_of(G) / UT);
+    if (G == 0) {
+      head_in(0, 0, false);
+      tail_in(0, 0, false);
+    } else {
+      launch(G, 0, zsize(G - 1), Z * (G - 1), kb, true, side);    // Q
+      head_in(kb, G, true);
+      launch(G, 1, zsize(G - 1), Z * (G - 1), kb, false, side2);  // the rest of the cross
+      tail_in(kb, G, true);
+    }
+    for (int j = 0; j < zb; ++j) {
+      const int k = kb + j;
+      // head
+      for (auto &b : v) ck(ctx, shard_chain(b, k, k % NS, side), "shard chain");
+      rec(E_SP(k), side);
+      for (auto &b : v) ck(ctx, shard_pgemm(b, k, k % NS, (k + 1) * KT, hT, true, side), "shard head GEMM");
+      rec(E_GH(k), side);
+      if (j + 1 < zb) {
+        launch(G, 2 + j, 1, k, k + 1, true, side);  // panel k on Q_{j+1}
+        head_in(k + 1, G, true);
+      }
+      // tail
+      wait(side2, E_SP(k));
+      for (auto &b : v) ck(ctx, shard_pgemm(b, k, k % NS, (k + 1) * KT, hT, false, side2), "shard tail GEMM");
+      if (j + 1 < zb) {
+        wait(side2, E_GH(k));
+        launch(G, zb + j + 1, j + 1, kb, k + 1, false, side2);  // T_{j+1}
+        tail_in(k + 1, G, true);
+      }
+    }
+    rec(E_READY(G), side);
+    rec(E_READY2(G), side2);
+  };
+  wait(side, E_IN);
+  wait(side2, E_IN);
+  produce(0);
+  m.upd_used = 0;
+  for (int g = 0; g < ng; ++g) {
+    const int kg = Z * g;
+    const bool more = g + 1 < ng;
+    const int kb = Z * (g + 1), zb = more ? zsize(g + 1) : 0;
+    wait(st, E_READY(g));
+    wait(st, E_READY2(g));
+    rec(E_PRE(g), st);
+    const bool tm = timed && m.upd_used + 2 <= (int)m.ev_upd.size();
+    const int kx0 = more ? kb : -1, kx1 = more ? kb + zb : -1;
+    for (size_t j = 0; j < v.size(); ++j) {
+      RankState &R = *m.ranks[j];
+      if (tm && j == 0) ck(ctx, hipEventRecord(m.ev_upd[(size_t)m.upd_used], st), "event");
+      ck(ctx, shard_update_group(v[j], kg, zsize(g), NS, kx0, kx1, (const Tile *)R.tupd.p, R.nupd, st),
+         "shard group update");
+      if (tm && j == 0) {
+        ck(ctx, hipEventRecord(m.ev_upd[(size_t)m.upd_used + 1], st), "event");
+        m.upd_flops[(size_t)m.upd_used / 2] =
+            update_flops_group(R.hupd, m.naug, (int64_t)kg * NB, zsize(g), kx0, kx1);
+        m.upd_used += 2;
+      }
+    }
+    if (!more) break;
+    wait(side, E_PRE(g));
+    wait(side2, E_PRE(g));
+    produce(g + 1);
+  }
+}
+
 void run_sweep_sharded(ShardModel &m, int which, bool timed) {
   ace_ctx *ctx = m.ctx;
   const int steps = (int)(m.npad / NB);
   const int Z = m.Z;
+  if (m.heads && steps >= 2) {
+    run_sweep_sharded_heads(m, which, timed);
+    return;
+  }
   if (!pair_steps() || steps < 2 || Z < 2 || !m.ranks[0]->P[2 * Z - 1].p) {
     run_sweep_sharded_steps(m, which, timed);
     return;
@@ -654,6 +913,12 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
   }
   const int nlocal = m->sim ? world : 1;
   const int steps = (int)(npad / NB);
+  // the head schedule: simulated, proxy and RCCL groups (the host-callback
+  // group keeps the group schedule: its exchanges block the host in turn)
+  m->heads = shard_heads_on() && heads_on() && pair_steps() && steps >= 2 && m->Z >= 2 &&
+             !m->host && (m->sim || m->proxy || rccl().CommSplit);
+  if (m->heads && m->comm)
+    nck(ctx, rccl().CommSplit(m->comm, 0, rank, &m->comm2, nullptr), "ncclCommSplit");
   const int maxslots = shard_row_slots(steps, world);
   const int ncol = s.B * (s.PM + 1);
   for (int j = 0; j < nlocal; ++j) {
@@ -673,6 +938,10 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
     }
     for (int b = 0; b < 2; ++b) alloc(ctx, R->S[b], (size_t)(SUB * NB) * sizeof(double), "alloc S");
     if (nslot > 2) build_cross_lists(ctx, *R, naug, steps, world, m->Z);
+    if (m->heads) {
+      build_head_lists(ctx, *R, naug, steps, world, m->Z);
+      alloc(ctx, R->lowh, (size_t)(m->Z * NB * NB) * sizeof(double), "alloc head exchange");
+    }
     alloc(ctx, R->SW, (size_t)SW_DOUBLES * sizeof(double), "alloc SW");
     alloc(ctx, R->piv, (size_t)npad * sizeof(double), "alloc piv");
     alloc(ctx, R->flag, 16, "alloc flag");
@@ -716,7 +985,9 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
   }
   // lookahead events: the step schedule's 2 steps + 1, the pair schedule's
   // 4 ngroups + 2
-  m->ev.assign((size_t)std::max(2 * steps + 1, 4 * ((steps + 1) / 2) + 2), nullptr);
+  const int ngr = (steps + m->Z - 1) / std::max(1, m->Z);
+  m->ev.assign((size_t)std::max({2 * steps + 1, 4 * ((steps + 1) / 2) + 2, 4 + 4 * ngr + 2 * steps}),
+               nullptr);
   for (auto &e : m->ev) ck(ctx, hipEventCreateWithFlags(&e, ACE_SYNC_EVENT_FLAGS), "event");
   m->ev_upd.assign((size_t)(2 * steps), nullptr);
   m->upd_flops.assign((size_t)steps, 0.0);

@@ -168,7 +168,9 @@ __device__ __forceinline__ void pivot_sweep(double (&v)[SUB / NW], PivotLds<NW> 
 template <int T>
 __device__ __forceinline__ double row_bcast(double x) {
   long v = __builtin_bit_cast(long, x);
-  long b = __builtin_amdgcn_update_dpp((long)0, v, 0x150 + T, 0xf, 0xf, false);  // v_mov_b64_dpp
+  // bound_ctrl set with full masks: every lane is written from a valid source
+  // lane, so the old value is dead and needs no zero-initialising move
+  long b = __builtin_amdgcn_update_dpp((long)0, v, 0x150 + T, 0xf, 0xf, true);  // v_mov_b64_dpp
   return __builtin_bit_cast(double, b);
 }
 
@@ -192,7 +194,7 @@ __device__ __forceinline__ double rep_row(double x) {
 // one scalar pivot t of the 16x16 block in the one-wave layout (see above);
 // the pivot d goes to pv[T] from one lane (rec: wave 0)
 template <int T>
-__device__ __forceinline__ void blk_pivot(double (&x)[4], int r, int g, double *pv, bool rec) {
+__device__ __forceinline__ void blk_pivot(double (&x)[4], int r, int g, double &dk) {
   constexpr int TG = T >> 2, TE = T & 3;
   const double c = rep_row<TG>(x[TE]);  // M(r, t)
   double rw[4];                          // M(t, 4g + e)
@@ -219,7 +221,7 @@ __device__ __forceinline__ void blk_pivot(double (&x)[4], int r, int g, double *
     const double vr = rw[e] * rd;
     x[e] = jt ? (isrow ? -rd : cd) : (isrow ? vr : vn);
   }
-  if (rec && r == T && g == 0) pv[T] = d;
+  dk = r == T ? d : dk;  // lane r keeps pivot r's value (stored once per block)
 }
 
 template <int P>
@@ -252,16 +254,16 @@ __device__ __forceinline__ void pivot_sweep_blk(double (&v)[SUB / 4], double (*M
       x[0] = a.x; x[1] = a.y; x[2] = b.x; x[3] = b.y;
     }
     {
-      double *const p = pv + s0;
-      const bool rec = w == 0;
-      blk_pivot<0>(x, r, g, p, rec);   blk_pivot<1>(x, r, g, p, rec);
-      blk_pivot<2>(x, r, g, p, rec);   blk_pivot<3>(x, r, g, p, rec);
-      blk_pivot<4>(x, r, g, p, rec);   blk_pivot<5>(x, r, g, p, rec);
-      blk_pivot<6>(x, r, g, p, rec);   blk_pivot<7>(x, r, g, p, rec);
-      blk_pivot<8>(x, r, g, p, rec);   blk_pivot<9>(x, r, g, p, rec);
-      blk_pivot<10>(x, r, g, p, rec);  blk_pivot<11>(x, r, g, p, rec);
-      blk_pivot<12>(x, r, g, p, rec);  blk_pivot<13>(x, r, g, p, rec);
-      blk_pivot<14>(x, r, g, p, rec);  blk_pivot<15>(x, r, g, p, rec);
+      double dk = 0.0;
+      blk_pivot<0>(x, r, g, dk);   blk_pivot<1>(x, r, g, dk);
+      blk_pivot<2>(x, r, g, dk);   blk_pivot<3>(x, r, g, dk);
+      blk_pivot<4>(x, r, g, dk);   blk_pivot<5>(x, r, g, dk);
+      blk_pivot<6>(x, r, g, dk);   blk_pivot<7>(x, r, g, dk);
+      blk_pivot<8>(x, r, g, dk);   blk_pivot<9>(x, r, g, dk);
+      blk_pivot<10>(x, r, g, dk);  blk_pivot<11>(x, r, g, dk);
+      blk_pivot<12>(x, r, g, dk);  blk_pivot<13>(x, r, g, dk);
+      blk_pivot<14>(x, r, g, dk);  blk_pivot<15>(x, r, g, dk);
+      if (w == 0 && g == 0) pv[s0 + r] = dk;  // read after the barriers below
     }
     // this sub-step's block update, computed from the old values before the
     // barrier (reads), stored after it (writes of blocks other waves read)
@@ -839,6 +841,10 @@ struct GatherOut {
   double *low = nullptr, *send = nullptr;
   int64_t h = 0;
   int G = 1;
+  // head / tail exchange of the sharded head schedule: low holds only the
+  // column rows from k0 + lr0 on (ld h): the head part [k0, hend) with lr0 = 0,
+  // the tail part [hend, naug) with lr0 = hend - k0
+  int64_t lr0 = 0;
 };
 static inline GatherOut no_gather() { return GatherOut{nullptr, nullptr, nullptr, -1, 0}; }
 static inline GatherOut pack_out(double *low, double *send, double *P, double *W, double *S0,
@@ -860,7 +866,7 @@ __device__ __forceinline__ void gput(const GatherOut &g, int64_t r, int64_t c, d
   const int64_t cc = c - g.k0, rr = r - g.k0;
   if (g.low) {  // pack mode (k_pack_lower / k_pack_rows layouts)
     if ((uint64_t)cc < (uint64_t)NB) {  // column block k: rows >= k0 (r >= c >= k0)
-      g.low[rr + cc * g.h] = v;
+      g.low[(rr - g.lr0) + cc * g.h] = v;
       if ((uint64_t)rr < (uint64_t)NB && r != c) g.low[cc + rr * g.h] = v;  // mirror
     } else if ((uint64_t)rr < (uint64_t)NB) {  // row block k, an own column c < k0
       g.send[(lcol(c, g.G) / NB) * NB * NB + rr + (c % NB) * NB] = v;
@@ -894,7 +900,7 @@ __device__ __forceinline__ void gput_aug_dead(const GatherOut &g, const double *
   for (int e = tid; e < (UT - 16) * UT; e += nthr) {
     const int a = 16 + e % (UT - 16), c = e / (UT - 16);
     const double v = A[(R0 + a) + (lc0 + c) * ld];
-    if (g.low) g.low[(R0 + a - g.k0) + (cc0 + c) * g.h] = v;
+    if (g.low) g.low[(R0 + a - g.k0 - g.lr0) + (cc0 + c) * g.h] = v;
     if (g.P) g.P[(R0 + a) + (cc0 + c) * g.ldp] = -v;
   }
 }
@@ -1701,7 +1707,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_multi_r(double *__restri
                                                                 const Tile *__restrict__ tiles,
                                                                 int64_t ntiles,
                                                                 int *__restrict__ queue,
-                                                                int reserve) {
+                                                                int reserve, GatherOut go) {
   ACE_WGT(5, gridDim.x < 4096 || blockIdx.x % 32 == 0);
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
@@ -1734,8 +1740,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_multi_r(double *__restri
     const int I = tt.I, J = tt.J;
     if (I < 0) continue;  // padding of the XCD order
     if (kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT))) continue;
-    update_multi_tile<SH, true>(I, J, sW, sP, A, ld, ps, npan, ldp, ka0,
-                                GatherOut{nullptr, nullptr, nullptr, -1, 0}, 1);
+    update_multi_tile<SH, true>(I, J, sW, sP, A, ld, ps, npan, ldp, ka0, go, 1);
   }
 }
 
@@ -2154,13 +2159,17 @@ __global__ __launch_bounds__(256, 4) void k_panel_gemm_q(double *__restrict__ W,
 // block k sends rows [k0, naug) of its column block (contiguous, ld naug-k0)
 // by broadcast; every rank sends the NB x NB pieces A[k-block, j-block] of
 // its own blocks j < k (slot q = j / G) by all-gather.
+// (i_base, lr0, h): rows from i_base on, into low at row offset lr0 (the
+// head / tail parts of the head schedule; default: every row >= k0)
 __global__ __launch_bounds__(256) void k_pack_lower(const double *__restrict__ A, int64_t ld,
                                                     int G, int64_t k0, int64_t naug,
-                                                    double *__restrict__ low) {
-  const int64_t i0 = k0 + (int64_t)blockIdx.x * 64;
+                                                    double *__restrict__ low, int64_t i_base = -1,
+                                                    int64_t lr0 = 0, int64_t hh = -1) {
+  const int64_t i0 = (i_base < 0 ? k0 : i_base) + (int64_t)blockIdx.x * 64;
   const int j0 = blockIdx.y * 64;
   const int64_t L = lcol(k0, G);
-  const int64_t h = naug - k0;
+  const int64_t h = hh < 0 ? naug - k0 : hh;
+  low -= lr0;  // row (i - k0) of the column lands at (i - k0 - lr0)
   if (i0 >= k0 + NB || i0 >= k0 + j0 + 64) {  // entirely on / below the diagonal
     for (int e = threadIdx.x; e < 4096; e += 256) {
       const int a = e & 63, b = e >> 6;
@@ -2194,15 +2203,19 @@ __global__ __launch_bounds__(256) void k_pack_rows(const double *__restrict__ A,
 // from the broadcast block, rows i < k0 (block j = i / NB) from all-gather
 // slot (j % G, j / G), transposed: P[i, c] = A[k0 + c, i].  skip_own: the
 // rows of rank r's own blocks are already in place (packing cross launch).
+// (i_base, lr0, hh): rows from i_base on, low holding the column rows from
+// k0 + lr0 on with ld hh (the head / tail parts of the head schedule;
+// default: every row, low = rows >= k0)
 __global__ __launch_bounds__(256) void k_unpack_panel(const double *__restrict__ low,
                                                       const double *__restrict__ recv, int m,
                                                       int G, int64_t k0, int64_t naug,
                                                       double *__restrict__ Pn,
                                                       double *__restrict__ W, int64_t ldp,
                                                       double *__restrict__ S0, int skip_own,
-                                                      int r) {
+                                                      int r, int64_t i_base = 0, int64_t lr0 = 0,
+                                                      int64_t hh = -1) {
   __shared__ double tile[64][65];
-  const int64_t i0 = (int64_t)blockIdx.x * 64;
+  const int64_t i0 = i_base + (int64_t)blockIdx.x * 64;
   const int j0 = blockIdx.y * 64;
   const int tid = threadIdx.x;
   if (skip_own) {  // rows the rank's own (packing) cross launch wrote
@@ -2210,10 +2223,10 @@ __global__ __launch_bounds__(256) void k_unpack_panel(const double *__restrict__
     if (i0 >= k0 ? kb % G == r : (i0 / NB) % G == r) return;
   }
   if (i0 >= k0) {
-    const int64_t h = naug - k0;
+    const int64_t h = hh < 0 ? naug - k0 : hh;
     for (int e = tid; e < 4096; e += 256) {
       const int a = e & 63, b = e >> 6;
-      const double v = low[(i0 - k0 + a) + (int64_t)(j0 + b) * h];
+      const double v = low[(i0 - k0 - lr0 + a) + (int64_t)(j0 + b) * h];
       Pn[(i0 + a) + (int64_t)(j0 + b) * ldp] = -v;
       if (i0 < k0 + NB) W[(i0 + a) + (int64_t)(j0 + b) * ldp] = v;
       if (i0 == k0) S0[a + (int64_t)(j0 + b) * SUB] = v;
@@ -3263,7 +3276,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
       }
       hipLaunchKernelGGL(k_update_multi_r<false>, dim3(2 * 256), dim3(UTHREADS), 0, st, b.A, b.ld,
                          ps, zsize(g), b.ld, (int64_t)kg * NB, kx0, kx1, ord, grid,
-                         b.bq + (int64_t)g * BQ_INTS, b.breserve);
+                         b.bq + (int64_t)g * BQ_INTS, b.breserve, no_gather());
     } else {
       upd(zsize(g), kg, kx0, kx1, ord, grid, no_gather(), st);
     }
@@ -3414,11 +3427,16 @@ hipError_t shard_update_cross(const ShardSweep &b, int k, int buf, hipStream_t s
 }
 
 hipError_t shard_update_group(const ShardSweep &b, int kb, int npan, int nslot, int kx0, int kx1,
-                              const Tile *tiles, int64_t nt, hipStream_t st, int kpack) {
+                              const Tile *tiles, int64_t nt, hipStream_t st, int kpack,
+                              double *lowp, int64_t lr0, int64_t hh) {
   const int sp = kpack >= 0 ? kpack % nslot : 0;
-  const GatherOut go = kpack >= 0 ? pack_out(b.low, send_of(b, kpack), b.P[sp], b.W[sp], b.S[0],
-                                             (int64_t)kpack * NB, b.ld, b.G)
-                                  : no_gather();
+  GatherOut go = kpack >= 0 ? pack_out(lowp ? lowp : b.low, send_of(b, kpack), b.P[sp], b.W[sp],
+                                       b.S[0], (int64_t)kpack * NB, b.ld, b.G)
+                            : no_gather();
+  if (kpack >= 0 && hh >= 0) {  // the head or the tail part of the column (head schedule)
+    go.lr0 = lr0;
+    go.h = hh;
+  }
   if (nt <= 0) return hipGetLastError();
   if (npan == 1) {  // (only ever without a skip range)
     const int s0 = kb % nslot;
@@ -3433,6 +3451,57 @@ hipError_t shard_update_group(const ShardSweep &b, int kb, int npan, int nslot, 
   }
   hipLaunchKernelGGL(k_update_multi<true>, dim3((unsigned)nt), dim3(UTHREADS), 0, st, b.A, b.ld, ps,
                      npan, b.ld, (int64_t)kb * NB, kx0, kx1, tiles, go, b.G);
+  return hipGetLastError();
+}
+
+// ---- the sharded head schedule's pieces (run_sweep_sharded_heads) ---------
+// Owner of block k: column rows [i_lo, i_hi) (>= k0) of its block into low
+// (row offset lr0, ld hh); with rows: also every rank's row pieces A[k, j < k]
+// into its all-gather slot (panel 0 / the unfused path).
+hipError_t shard_pack_part(const ShardSweep &b, int k, int64_t i_lo, int64_t i_hi, double *low,
+                           int64_t lr0, int64_t hh, bool rows, hipStream_t st) {
+  const int64_t k0 = (int64_t)k * NB, naug = b.ld;
+  if (k % b.G == b.r && i_hi > i_lo)
+    hipLaunchKernelGGL(k_pack_lower, dim3((unsigned)((i_hi - i_lo) / 64), NB / 64), dim3(256), 0, st,
+                       b.A, b.ld, b.G, k0, naug, low, i_lo, lr0, hh);
+  const int own = k > b.r ? (k - b.r + b.G - 1) / b.G : 0;
+  if (rows && own > 0)
+    hipLaunchKernelGGL(k_pack_rows, dim3(NB / 64, NB / 64, (unsigned)own), dim3(256), 0, st, b.A,
+                       b.ld, k0, send_of(b, k));
+  return hipGetLastError();
+}
+
+// Rows [i_lo, i_hi) of panel k (slot buf): from low (rows >= k0: offset lr0,
+// ld hh) or from the gathered row pieces (rows < k0); own_done: the rank's
+// own rows were written by its packing launch (skipped; none to do at G = 1).
+hipError_t shard_unpack_part(const ShardSweep &b, int k, int buf, int64_t i_lo, int64_t i_hi,
+                             const double *low, int64_t lr0, int64_t hh, bool own_done,
+                             hipStream_t st) {
+  if (i_hi <= i_lo || (own_done && b.G == 1)) return hipSuccess;
+  const int64_t k0 = (int64_t)k * NB;
+  hipLaunchKernelGGL(k_unpack_panel, dim3((unsigned)((i_hi - i_lo) / 64), NB / 64), dim3(256), 0,
+                     st, low, b.recv, shard_row_slots(k, b.G), b.G, k0, b.ld, b.P[buf], b.W[buf],
+                     b.ld, b.S[0], own_done ? 1 : 0, b.r, i_lo, lr0, hh);
+  return hipGetLastError();
+}
+
+// Panel k's pivot sub-steps (k_pivot + the split sub-steps), no panel GEMM.
+hipError_t shard_chain(const ShardSweep &b, int k, int buf, hipStream_t st) {
+  panel_chain(b.P[buf], b.W[buf], b.ld, (int64_t)k * NB, b.SW, b.S, b.piv, b.flag, b.G, b.r, st,
+              false, nullptr, true);
+  return hipGetLastError();
+}
+
+// Panel k's GEMM W_i = Pn_i W_kk over the rank's rows (k_panel_gemm_t's
+// ownership rule) in row tiles [rt_lo, rt_hi) (head) or outside them (tail).
+hipError_t shard_pgemm(const ShardSweep &b, int k, int buf, int rt_lo, int rt_hi, bool head,
+                       hipStream_t st) {
+  const int nT = (int)(b.ld / UT);
+  const int n = head ? rt_hi - rt_lo : nT - (rt_hi - rt_lo);
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_panel_gemm_t<1>, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, st, b.W[buf],
+                     b.P[buf], b.ld, (int64_t)k * NB, b.G, b.r, head ? rt_lo : 0,
+                     head ? 1 << 30 : rt_lo, head ? 1 << 30 : rt_hi);
   return hipGetLastError();
 }
 

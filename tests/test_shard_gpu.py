@@ -168,7 +168,10 @@ def test_sharded_pair_schedule_is_bitwise_neutral(tmp_path, world, n):
     results: every tile sees the same MFMA chains in the same order; and so
     does the exchange packing fused into the cross launches (default)
     against separate pack launches (ACE_FUSE_PACK=0), and the pair launches
-    on k_update_multi (default) against k_update_pair (ACE_MULTI2=0).  n
+    on k_update_multi (default) against k_update_pair (ACE_MULTI2=0).  The
+    default runs the head / tail schedule (round 5: the single-GPU lists, the
+    exchange split into a head broadcast and a tail broadcast + all-gather);
+    ACE_SHARD_HEADS=0 the group schedule without the split.  n
     gives 8, 7 (an odd last group) and 9 sweep steps; the simulated group
     runs the lookahead with all ranks on the shared streams."""
     import os
@@ -177,12 +180,12 @@ def test_sharded_pair_schedule_is_bitwise_neutral(tmp_path, world, n):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
     variants = {"step": {"ACE_PAIR": "0"}, "pair": {"ACE_FUSE_PACK": "0"}, "fused": {},
-                "pair_kernel": {"ACE_MULTI2": "0"}}
+                "pair_kernel": {"ACE_MULTI2": "0"}, "groups": {"ACE_SHARD_HEADS": "0"}}
     for v, extra in variants.items():
         out = str(tmp_path / f"s{v}.npz")
         env = dict(os.environ, **extra)
         run_child(_SCHED.format(root=root, n=n, world=world, out=out), env=env, timeout=100)
         outs[v] = np.load(out)
-    for v in ("pair", "fused"):
+    for v in ("pair", "fused", "groups"):
         for k in ("g1", "s1", "g2", "s2", "inv"):
             assert np.array_equal(outs["step"][k], outs[v][k]), (v, k)
