@@ -630,7 +630,7 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
     std::vector<double> tab = make_tab(theta, s);
     // pinned staging, async on the stream: the previous evaluation's results
     // were synchronised before this one started, so the region is free
-    double *h = m->hio.ensure(ctx, tab.size() + (size_t)(s.B * (s.PM + 1) + 1) + 4 + 5 + 1);
+    double *h = m->hio.ensure(ctx, tab.size() + m->res.bytes / sizeof(double));
     std::copy(tab.begin(), tab.end(), h);
     ck(ctx, hipMemcpyAsync(m->tab.p, h, tab.size() * sizeof(double), hipMemcpyHostToDevice, st),
        "upload tables");
@@ -670,7 +670,7 @@ void model_pipeline(ace_model *m, SweepWork &w, const double *theta, int use_mu,
   ck(ctx, launch_tile_sums(m->gpart.d(), m->ntiles, ldg, m->gwork.d(), m->gsum.d(), st),
      "tile sums");
   ck(ctx, launch_final_sums(m->y.d(), m->scal.d() + 4, m->alpha.d(), nullptr, sig, m->n,
-                            w.piv.d(), w.npad, m->sums.d(), st, tv.sig),
+                            w.piv.d(), w.npad, m->sums.d(), st, tv.sig, w.flag.i()),
      "final sums");
 }
 
@@ -849,12 +849,13 @@ int ace_model_create(ace_ctx *ctx, int kind, int64_t n, int p, int B, ace_model 
     if (slice_norms_on())
       alloc(ctx, m->norms, (size_t)((s.B + 1) * m->npad) * sizeof(double), "alloc norms");
     alloc(ctx, m->alpha, (size_t)m->npad * sizeof(double), "alloc alpha");
-    alloc(ctx, m->scal, 16 * sizeof(double), "alloc scal");
     const int ldg = grad_part_cols(s.PM, s.B);
     alloc(ctx, m->gpart, (size_t)(m->ntiles * ldg) * sizeof(double), "alloc gpart");
     alloc(ctx, m->gwork, (size_t)tile_sums_work(ldg) * sizeof(double), "alloc tile sums");
-    alloc(ctx, m->gsum, (size_t)ldg * sizeof(double), "alloc gsum");
-    alloc(ctx, m->sums, 8 * sizeof(double), "alloc sums");
+    alloc(ctx, m->res, (size_t)(ldg + 8 + 16) * sizeof(double), "alloc results");
+    m->gsum.p = m->res.d();
+    m->sums.p = m->res.d() + ldg;
+    m->scal.p = m->res.d() + ldg + 8;
     ck(ctx, hipMemsetAsync(m->sw.A.p, 0, m->sw.A.bytes, ctx->stream), "memset A");
     const int steps = (int)(m->npad / NB);
     m->ev_upd.assign((size_t)(4 * steps), nullptr);
@@ -959,19 +960,19 @@ int ace_model_para_update(ace_model *m, int iter, double *theta, double *grad, d
       model_collect_timing(m, m->pend);
       m->pend = -1;
     }
-    // into the pinned region behind the tables, one synchronisation
+    // the result block into the pinned region behind the tables: one copy
+    // and one (bounded) synchronisation -- pinned, so the copy is queued
+    // without draining the stream first as download() does for pageable
+    // memory; four drained small copies cost ~20 us each at C1
     double *h = m->hio.p + (2 * s.B * s.PM + s.B);
-    download(ctx, h, m->gsum.d(), gs.size(), "download gsum");
-    download(ctx, h + gs.size(), m->sums.d(), 4, "download sums");
-    download(ctx, h + gs.size() + 4, m->scal.d(), 5, "download scal");
-    int *hflag = reinterpret_cast<int *>(h + gs.size() + 9);
-    ck(ctx, hipMemcpyAsync(hflag, m->sw.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
-       "download flag");
+    ck(ctx, hipMemcpyAsync(h, m->res.p, m->res.bytes, hipMemcpyDeviceToHost, ctx->stream),
+       "download results");
     sync(ctx);
+    const double *hs = h + (m->sums.d() - m->res.d()), *hc = h + (m->scal.d() - m->res.d());
     std::copy(h, h + gs.size(), gs.begin());
-    std::copy(h + gs.size(), h + gs.size() + 4, sums);
-    std::copy(h + gs.size() + 4, h + gs.size() + 9, scal);
-    flag = *hflag;
+    std::copy(hs, hs + 4, sums);
+    std::copy(hc, hc + 5, scal);
+    flag = hs[4] != 0.0;
     if (timed) {
       m->pend = m->tset;
       m->tset ^= 1;
@@ -1016,10 +1017,11 @@ int ace_model_train_stats(ace_model *m, const double *theta, double *stats) {
   } else {
     m->sw2.ensure(ctx, m->n);
     model_pipeline(m, m->sw2, theta, 0, false);
-    download(ctx, sums, m->sums.d(), 4, "download sums");
-    ck(ctx, hipMemcpyAsync(&flag, m->sw2.flag.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream),
-       "download flag");
+    double hs[5];
+    download(ctx, hs, m->sums.d(), 5, "download sums");
     sync(ctx);
+    std::copy(hs, hs + 4, sums);
+    flag = hs[4] != 0.0;
   }
   stats[0] = m->std_y * std::sqrt(sums[0]) / std::sqrt((double)m->n);
   stats[1] = -0.5 * (m->n * std::log(2.0 * M_PI) + sums[3] + sums[1]);

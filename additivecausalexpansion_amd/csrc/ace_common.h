@@ -86,6 +86,12 @@ struct DBuf {
   int *i() const { return static_cast<int *>(p); }
 };
 
+// A non-owning sub-range of a DBuf.
+struct DView {
+  double *p = nullptr;
+  double *d() const { return p; }
+};
+
 inline void ck(ace_ctx *ctx, hipError_t e, const char *what) {
   if (e == hipSuccess) return;
   ctx->err = std::string(what) + ": " + hipGetErrorString(e);

@@ -209,6 +209,7 @@ bool heads_on();
 // Steps per bulk launch: 2 (k_update_pair, default), ACE_GROUP=3 or 4 selects
 // k_update_multi groups (run_sweep_groups).
 int sweep_group();
+int sweep_group_n(int64_t naug);  // sweep_group() for a model of naug rows
 double update_gemm_tiles_group(int64_t naug, int64_t ka0, int npan, int kx0, int kx1);
 // The lower 128-tiles with I or J in block k+1, for k = 0 .. steps-2,
 // concatenated (each step's list dealt to the XCDs like the bulk order);
@@ -344,11 +345,12 @@ hipError_t launch_colsum(const double *in, int64_t nrows, int ncols,
 // sums[0] = sum (ybar - s)^2, sums[1] = sum y*alpha, sums[2] = sum alpha,
 // sums[3] = sum log(piv[0..npiv)), with ybar = y - *mu (device scalar).
 // s == nullptr: ybar - s = sig * alpha (fused model, A = Kfull + sig I);
-// sigp (device scalar) replaces sig when given.
+// sigp (device scalar) replaces sig when given; flag (device int) is copied
+// to sums[4] when given, so that one read-back carries it.
 hipError_t launch_final_sums(const double *y, const double *mu, const double *alpha,
                              const double *s, double sig, int64_t n, const double *piv,
                              int64_t npiv, double *sums, hipStream_t st,
-                             const double *sigp = nullptr);
+                             const double *sigp = nullptr, const int *flag = nullptr);
 // ---- device-fused training loop (ace_train.hip) -----------------------------
 // theta tables of make_tab (ace_common.h) from a device theta, plus
 // tab[2 B PM + B] = exp(theta[0]) (TabView::sig)

@@ -51,7 +51,7 @@ struct SweepWork {
     }
     poff.clear();
     if (pair_steps() && cross_update_on_tiles() && npad / NB >= 2) {
-      Z = sweep_group();
+      Z = sweep_group_n(naug);
       for (int j = 2; j < 2 * Z; ++j) {
         alloc(ctx, Ps[j], (size_t)(naug * NB) * sizeof(double), "alloc panel");
         alloc(ctx, Ws[j], (size_t)(naug * NB) * sizeof(double), "alloc panel");
@@ -181,7 +181,11 @@ struct ace_model {
   bool has_data = false;
   bool has_inverse = false;  // a para_update has left a resident inverse
   SideBufs side;
-  DBuf y, tab, alpha, scal, gpart, gwork, gsum, sums;
+  DBuf y, tab, alpha, gpart, gwork;
+  // the evaluation's results in one block, read back by one copy:
+  // [gsum: grad_part_cols | sums: 8 (sums[4] = the sweep's flag) | scal: 16]
+  DBuf res;
+  DView gsum, sums, scal;
   DBuf norms;           // per-evaluation slice norms (TabView::norms), (B + 1) x npad
   DBuf gtiles;          // gradient tile list (grad_tile_order), or none
   int64_t ngdiag = -1;  // its leading diagonal tiles

@@ -634,7 +634,7 @@ hipError_t launch_slice_norms(const double *X, int PM, int64_t np, int B, int NS
 // tile columns of the assembly's first part (model_pipeline): the first
 // sweep group's panels' columns (sweep_group() blocks), at most all of them
 static int asm_first_cols(int nt) {
-  const int jb = sweep_group() * NB / AT;
+  const int jb = sweep_group_n((int64_t)nt * AT + AUG) * NB / AT;
   return jb < nt ? jb : nt;
 }
 

@@ -893,7 +893,7 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
   m->ntr = (n + AT - 1) / AT;
   m->G = world;
   m->rank = rank;
-  m->Z = sweep_group();
+  m->Z = sweep_group_n(m->naug);
   m->host = ops != nullptr;
   if (ops) m->ops = *ops;
   m->sim = id == nullptr && !m->host;

@@ -192,7 +192,11 @@ __device__ __forceinline__ double rep_row(double x) {
 }
 
 // one scalar pivot t of the 16x16 block in the one-wave layout (see above);
-// the pivot d goes to pv[T] from one lane (rec: wave 0)
+// the pivot d goes to pv[T] from one lane (rec: wave 0).  The loop is bound
+// by instruction issue, not by its dependency chain: a variant that fetched
+// column t+1 before the update (its permlanes off the pivot chain, bit-
+// identical) has 5 more instructions per pivot and was 0.07 ms slower at C1
+// (profiles/r05_v12_ab_c1.txt).
 template <int T>
 __device__ __forceinline__ void blk_pivot(double (&x)[4], int r, int g, double &dk) {
   constexpr int TG = T >> 2, TE = T & 3;
@@ -2482,6 +2486,15 @@ int sweep_group() {
     v = e ? std::min(4, std::max(2, atoi(e))) : 4;
   }
   return v;
+}
+
+// Z for a model of naug rows: ACE_GROUP when set, else 3 up to n =
+// ACE_BULK_RESERVE_N (the chain-bound sizes: C1 3.90 -> 3.75 ms against Z = 4,
+// 3.87 at Z = 2 -- a shorter last bulk launch and an earlier first one,
+// profiles/r05_v11_ab_c1_group.txt), 4 above
+int sweep_group_n(int64_t naug) {
+  if (getenv("ACE_GROUP")) return sweep_group();
+  return naug <= ACE_BULK_RESERVE_N + AUG ? 3 : 4;
 }
 
 bool merge_cross() {

@@ -257,7 +257,8 @@ __global__ __launch_bounds__(1024) void k_final_sums(const double *__restrict__ 
                                                     const double *__restrict__ s, double sig,
                                                     int64_t n, const double *__restrict__ piv,
                                                     int64_t npiv, double *__restrict__ sums,
-                                                    const double *__restrict__ sigp) {
+                                                    const double *__restrict__ sigp,
+                                                    const int *__restrict__ flag) {
   __shared__ double sh[16];
   const double mu = *mup;
   if (sigp) sig = *sigp;
@@ -279,14 +280,15 @@ __global__ __launch_bounds__(1024) void k_final_sums(const double *__restrict__ 
     sums[1] = ya;
     sums[2] = sa;
     sums[3] = ld;
+    if (flag) sums[4] = (double)*flag;
   }
 }
 
 hipError_t launch_final_sums(const double *y, const double *mu, const double *alpha, const double *s,
                              double sig, int64_t n, const double *piv, int64_t npiv,
-                             double *sums, hipStream_t st, const double *sigp) {
+                             double *sums, hipStream_t st, const double *sigp, const int *flag) {
   hipLaunchKernelGGL(k_final_sums, dim3(1), dim3(1024), 0, st, y, mu, alpha, s, sig, n, piv, npiv,
-                     sums, sigp);
+                     sums, sigp, flag);
   return hipGetLastError();
 }
 
