@@ -174,33 +174,30 @@ __device__ __forceinline__ double row_bcast(double x) {
   return __builtin_bit_cast(double, b);
 }
 
-// replicate 16-lane row G of x into all four rows (v_permlane16/32_swap with
-// both operands x: swap16 -> {rows 0,0,2,2 ; rows 1,1,3,3}, swap32 ->
-// {rows lo,lo ; rows hi,hi})
+// replicate 16-lane row G of x into all four rows, on the LDS crossbar: two
+// ds_bpermute (no LDS memory) instead of four v_permlane16/32_swap and the
+// operand copies they need (x stays live) -- the pivot sweep's column fetch,
+// C1 3.74 -> 3.65 ms (profiles/r05_v13_ab_pivot.txt)
 template <int G>
-__device__ __forceinline__ unsigned rep_row32(unsigned x) {
-  const auto a = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-  const unsigned y = (G & 1) ? a[1] : a[0];
-  const auto b = __builtin_amdgcn_permlane32_swap(y, y, false, false);
-  return (G & 2) ? b[1] : b[0];
-}
-template <int G>
-__device__ __forceinline__ double rep_row(double x) {
+__device__ __forceinline__ double rep_row_bp(double x, int lane) {
+  const int addr = ((lane & 15) | (G << 4)) << 2;
   const unsigned long v = __builtin_bit_cast(unsigned long, x);
-  const unsigned lo = rep_row32<G>((unsigned)v), hi = rep_row32<G>((unsigned)(v >> 32));
+  const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)v);
+  const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)(v >> 32));
   return __builtin_bit_cast(double, ((unsigned long)hi << 32) | lo);
 }
 
 // one scalar pivot t of the 16x16 block in the one-wave layout (see above);
-// the pivot d goes to pv[T] from one lane (rec: wave 0).  The loop is bound
-// by instruction issue, not by its dependency chain: a variant that fetched
-// column t+1 before the update (its permlanes off the pivot chain, bit-
-// identical) has 5 more instructions per pivot and was 0.07 ms slower at C1
-// (profiles/r05_v12_ab_c1.txt).
+// the pivot d goes to pv[T] from one lane (rec: wave 0).  Measured variants
+// (C1, profiles/r05_v12_ab_c1.txt, r05_v13_ab_pivot.txt; all bit-identical):
+// column t+1 fetched before the update (its replication off the pivot chain)
+// with permlanes, +5 instructions per pivot: +0.07 ms; with ds_bpermute: as
+// this form; one FMA per element for the pivot row and the rest (row t with
+// c' = -1, x' = 0; 33 instead of 39 instructions per pivot): as this form.
 template <int T>
 __device__ __forceinline__ void blk_pivot(double (&x)[4], int r, int g, double &dk) {
   constexpr int TG = T >> 2, TE = T & 3;
-  const double c = rep_row<TG>(x[TE]);  // M(r, t)
+  const double c = rep_row_bp<TG>(x[TE], r | (g << 4));  // M(r, t)
   double rw[4];                          // M(t, 4g + e)
 #pragma unroll
   for (int e = 0; e < 4; ++e) rw[e] = row_bcast<T>(x[e]);
@@ -259,14 +256,10 @@ __device__ __forceinline__ void pivot_sweep_blk(double (&v)[SUB / 4], double (*M
     }
     {
       double dk = 0.0;
-      blk_pivot<0>(x, r, g, dk);   blk_pivot<1>(x, r, g, dk);
-      blk_pivot<2>(x, r, g, dk);   blk_pivot<3>(x, r, g, dk);
-      blk_pivot<4>(x, r, g, dk);   blk_pivot<5>(x, r, g, dk);
-      blk_pivot<6>(x, r, g, dk);   blk_pivot<7>(x, r, g, dk);
-      blk_pivot<8>(x, r, g, dk);   blk_pivot<9>(x, r, g, dk);
-      blk_pivot<10>(x, r, g, dk);  blk_pivot<11>(x, r, g, dk);
-      blk_pivot<12>(x, r, g, dk);  blk_pivot<13>(x, r, g, dk);
-      blk_pivot<14>(x, r, g, dk);  blk_pivot<15>(x, r, g, dk);
+#define BP(T) blk_pivot<T>(x, r, g, dk)
+      BP(0);  BP(1);  BP(2);  BP(3);  BP(4);  BP(5);  BP(6);  BP(7);
+      BP(8);  BP(9);  BP(10); BP(11); BP(12); BP(13); BP(14); BP(15);
+#undef BP
       if (w == 0 && g == 0) pv[s0 + r] = dk;  // read after the barriers below
     }
     // this sub-step's block update, computed from the old values before the
