@@ -91,7 +91,7 @@ struct SweepWork {
       if (!t.empty())
         upload_bytes(ctx, xtiles.p, t.data(), t.size() * sizeof(Tile), "upload cross tiles");
     }
-    const size_t need = (size_t)(5 * (npad / NB) + 8);
+    const size_t need = (size_t)(6 * (npad / NB) + 10);
     while (ev.size() < need) {
       hipEvent_t e;
       ck(ctx, hipEventCreateWithFlags(&e, ACE_SYNC_EVENT_FLAGS), "event");

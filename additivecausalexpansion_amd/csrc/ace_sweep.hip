@@ -3072,6 +3072,15 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   auto E2 = [&](int g) { return sy->ev[2 * steps + 2 + 2 * g]; };     // ready2(g)
   auto Egh = [&](int k) { return sy->ev[3 * steps + 3 + 2 * k]; };    // panel k's head GEMM done
   auto Esp = [&](int k) { return sy->ev[3 * steps + 4 + 2 * k]; };    // panel k's sub-steps done
+  // bulk launch g done: the next-but-one group's Q waits for it on the side
+  // stream directly (with the tail path's E2), not through the main stream's
+  // combined event -- one cross-stream hop instead of two before each Q, the
+  // GPU's idle gap at every C1 group boundary 28 -> 10 us, bitwise equal
+  // (profiles/r05_v14_qdirect.txt)
+  // (events 5 steps + 3 .. + 7 belong to assemble_and_sweep)
+  const bool qdirect = sy->nev >= 6 * steps + 9;
+  auto Eb = [&](int g) { return sy->ev[5 * steps + 9 + g]; };  // g = -1: the main stream's
+                                                                // work before the sweep
   auto gout = [&](int k) {
     return GatherOut{b.P[slot(k)], b.W[slot(k)], b.S[0], (int64_t)k * NB, b.ld};
   };
@@ -3252,6 +3261,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
       hipSuccess)
     return e;
   if ((e = produce_q(0)) != hipSuccess || (e = produce(0)) != hipSuccess) return e;
+  if (qdirect && (e = hipEventRecord(Eb(-1), st)) != hipSuccess) return e;
   int used = 0;
   for (int g = 0; g < ng; ++g) {
     const int kg = Z * g;
@@ -3261,7 +3271,14 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
     if ((e = hipStreamWaitEvent(st, E2(g), 0)) != hipSuccess) return e;
     if (more) {
       if ((e = hipEventRecord(sy->ev[2 * g + 1], st)) != hipSuccess) return e;  // bulk g-1 done
-      if ((e = hipStreamWaitEvent(side, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
+      // Q(g+1) needs the tail path of g and bulk g-1 (A's square, the panel
+      // slots it gathers into); at g = 0 the main stream's assembly instead
+      if (qdirect) {
+        if ((e = hipStreamWaitEvent(side, E2(g), 0)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(side, Eb(g - 1), 0)) != hipSuccess) return e;
+      } else if ((e = hipStreamWaitEvent(side, sy->ev[2 * g + 1], 0)) != hipSuccess) {
+        return e;
+      }
       if ((e = hipStreamWaitEvent(side2, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
       if ((e = produce_q(g + 1)) != hipSuccess) return e;
       if (qfirst && (e = hipStreamWaitEvent(st, Eq(g + 1), 0)) != hipSuccess) return e;
@@ -3293,6 +3310,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
             update_gemm_tiles_group(naug, (int64_t)kg * NB, zsize(g), kx0, kx1) * 2.0 * UT * UT * NB;
       used += 2;
     }
+    if (qdirect && g + 2 < ng && (e = hipEventRecord(Eb(g), st)) != hipSuccess) return e;  // Q(g+2)
     if (more && (e = produce(g + 1)) != hipSuccess) return e;
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
