@@ -110,6 +110,8 @@ def main():
     read(L, True)
     m.para_update(3, theta)
     recs = read(L, True)
+    if os.environ.get("WGT_DUMP"):  # raw records for offline analysis (tools/wgt_cu.py)
+        np.save(os.environ["WGT_DUMP"], recs)
     print(f"n={n}: {len(recs)} workgroup records")
     ls = launches(recs)
     t0 = min(int(r[2]) for r in recs)
