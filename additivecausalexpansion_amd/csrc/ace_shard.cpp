@@ -639,6 +639,11 @@ void run_sweep_sharded_heads(ShardModel &m, int which, bool timed) {
   // done -- what group g+1's lists need (its tiles were last touched by bulk
   // g-1; the W rows of its blocks come from group g's tail panel GEMMs)
   auto E_PRE = [&](int g) { return 2 + 3 * ng + 2 * steps + g; };
+  // bulk g done (g = -1: the main stream's work before the sweep): the head
+  // path of group g+2 waits for it and group g+1's tail path directly -- one
+  // cross-stream hop instead of two through E_PRE (single GPU: the same in
+  // run_sweep_heads, profiles/r05_v14_qdirect.txt)
+  auto E_BULK = [&](int g) { return 3 + 4 * ng + 2 * steps + g; };
   auto rec = [&](int i, hipStream_t s_) { ck(ctx, hipEventRecord(EV(i), s_), "event"); };
   auto wait = [&](hipStream_t s_, int i) { ck(ctx, hipStreamWaitEvent(s_, EV(i), 0), "event wait"); };
   auto hend_of = [&](int G) { return (int64_t)(Z * G + zsize(G)) * NB; };
@@ -729,6 +734,7 @@ void run_sweep_sharded_heads(ShardModel &m, int which, bool timed) {
   wait(side, E_IN);
   wait(side2, E_IN);
   produce(0);
+  rec(E_BULK(-1), st);
   m.upd_used = 0;
   for (int g = 0; g < ng; ++g) {
     const int kg = Z * g;
@@ -752,7 +758,9 @@ void run_sweep_sharded_heads(ShardModel &m, int which, bool timed) {
       }
     }
     if (!more) break;
-    wait(side, E_PRE(g));
+    rec(E_BULK(g), st);
+    wait(side, E_READY2(g));
+    wait(side, E_BULK(g - 1));
     wait(side2, E_PRE(g));
     produce(g + 1);
   }
@@ -986,7 +994,7 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
   // lookahead events: the step schedule's 2 steps + 1, the pair schedule's
   // 4 ngroups + 2
   const int ngr = (steps + m->Z - 1) / std::max(1, m->Z);
-  m->ev.assign((size_t)std::max({2 * steps + 1, 4 * ((steps + 1) / 2) + 2, 4 + 4 * ngr + 2 * steps}),
+  m->ev.assign((size_t)std::max({2 * steps + 1, 4 * ((steps + 1) / 2) + 2, 4 + 5 * ngr + 2 * steps}),
                nullptr);
   for (auto &e : m->ev) ck(ctx, hipEventCreateWithFlags(&e, ACE_SYNC_EVENT_FLAGS), "event");
   m->ev_upd.assign((size_t)(2 * steps), nullptr);
