@@ -539,9 +539,10 @@ void assemble_and_sweep(ace_ctx *ctx, SweepWork &w, const Shape &s, const PairSi
   const int R = asm_persist_reserve();
   const bool persist = R > 0 && sy.side && sy.nev >= 5 * steps + 6 && pairs_use_mm(s.PM, false) &&
                        mm_lds_ok(s.PM, s.B, s.kind, false);
-  ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, n, y, st), "aug init");
-  ck(ctx, hipMemsetAsync(w.flag.p, 0, sizeof(int), st), "memset flag");
-  if (persist) ck(ctx, hipMemsetAsync(w.aq.p, 0, (2 + 64) * sizeof(int), st), "memset queue");
+  // (the flag and the persistent assembly's queue are zeroed by the same launch)
+  ck(ctx, launch_aug_init(w.A.d(), w.naug, w.npad, n, y, st, 1, 0, w.flag.i(), 1,
+                          persist ? w.aq.i() : nullptr, persist ? 2 + 64 : 0),
+     "aug init");
   if (ev_asm) ck(ctx, hipEventRecord(ev_asm[0], st), "event");
   ck(ctx, launch_assembly(0, s.kind, s.PM, ps, ps, w.npad, s.B, s.ZS, tv, sig, w.A.d(), w.naug,
                           nullptr, st, nullptr, 0, 1, 1),

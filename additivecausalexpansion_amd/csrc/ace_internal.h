@@ -320,8 +320,11 @@ hipError_t shard_pgemm(const ShardSweep &b, int k, int buf, int rt_lo, int rt_hi
 
 // ---- small helpers -----------------------------------------------------------
 // AUG rows of columns j < n: row 0 = y (zeros if y is null), row 1 = 1
+// z0[0..n0) and z1[0..n1) (device ints, may be null) are zeroed by the same
+// launch: the evaluation's flag and queue resets without fill launches
 hipError_t launch_aug_init(double *A, int64_t ld, int64_t npad, int64_t n,
-                           const double *y, hipStream_t st, int G = 1, int rank = 0);
+                           const double *y, hipStream_t st, int G = 1, int rank = 0,
+                           int *z0 = nullptr, int n0 = 0, int *z1 = nullptr, int n1 = 0);
 // out[0] = sum_j y_j (A^-1 1)_j (AUG row 1), out[1] = 1^T A^-1 1 (corner)
 hipError_t launch_aug_dot(const double *A, int64_t ld, int64_t npad, int64_t n, const double *y,
                           double *out, hipStream_t st);

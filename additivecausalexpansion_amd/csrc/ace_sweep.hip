@@ -40,6 +40,8 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 #ifndef ACE_PIVOT_RCP
 #define ACE_PIVOT_RCP 1
 #endif
+// (3 on them and on the head-path gather k_update_q: C1 -0.06 ms on one box,
+// +0.01 on another, C2 +0.15 ms -- not kept, profiles/r05_v19_ab_prio.txt)
 #ifndef ACE_CHAIN_PRIO
 #define ACE_CHAIN_PRIO 1
 #endif

@@ -42,10 +42,15 @@ __device__ __forceinline__ double block_sum1024(double v, double *sh) {
 // ---------------------------------------------------------------- AUG rows
 // rows npad .. npad+AUG-1 of A: row 0 = y (j < n), row 1 = 1 (j < n), 0 else
 __global__ void k_aug_init(double *__restrict__ A, int64_t ld, int64_t npad, int64_t n,
-                           const double *__restrict__ y, int G, int rank) {
+                           const double *__restrict__ y, int G, int rank, int *__restrict__ z0,
+                           int n0, int *__restrict__ z1, int n1) {
   const int64_t j = blockIdx.x;  // global column
-  if (!owns_col(j, G, rank)) return;
   const int t = threadIdx.x;     // AUG rows
+  if (j == 0) {
+    for (int i = t; i < n0; i += AUG) z0[i] = 0;
+    for (int i = t; i < n1; i += AUG) z1[i] = 0;
+  }
+  if (!owns_col(j, G, rank)) return;
   double v = 0.0;
   if (j < n) {
     if (t == 0) v = y ? y[j] : 0.0;  // y == null: the 1 row only
@@ -55,9 +60,9 @@ __global__ void k_aug_init(double *__restrict__ A, int64_t ld, int64_t npad, int
 }
 
 hipError_t launch_aug_init(double *A, int64_t ld, int64_t npad, int64_t n, const double *y,
-                           hipStream_t st, int G, int rank) {
+                           hipStream_t st, int G, int rank, int *z0, int n0, int *z1, int n1) {
   hipLaunchKernelGGL(k_aug_init, dim3((unsigned)ld), dim3(AUG), 0, st, A, ld, npad, n, y, G,
-                     rank);
+                     rank, z0, n0, z1, n1);
   return hipGetLastError();
 }
 
