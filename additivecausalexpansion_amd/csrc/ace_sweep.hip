@@ -3257,6 +3257,10 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
         if ((r = tail(j)) != hipSuccess) return r;
     }
     if (G == 0 && sy->fill && (r = sy->fill(sy->fill_arg, side2)) != hipSuccess) return r;
+    // (qdirect: E2(G) also stands for the head path, so that the main stream
+    // waits for one event before each bulk launch)
+    if (qdirect && !split && (r = hipStreamWaitEvent(side2, sy->ev[2 * G], 0)) != hipSuccess)
+      return r;
     return hipEventRecord(E2(G), side2);
   };
   if ((e = hipStreamWaitEvent(side2, sy->tail_after ? sy->tail_after : sy->ev[2 * steps], 0)) !=
@@ -3269,19 +3273,23 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
     const int kg = Z * g;
     const bool more = g + 1 < ng;
     const int kb = Z * (g + 1), zb = more ? zsize(g + 1) : 0;
-    if ((e = hipStreamWaitEvent(st, sy->ev[2 * g], 0)) != hipSuccess) return e;
+    if (!qdirect && (e = hipStreamWaitEvent(st, sy->ev[2 * g], 0)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(st, E2(g), 0)) != hipSuccess) return e;
     if (more) {
-      if ((e = hipEventRecord(sy->ev[2 * g + 1], st)) != hipSuccess) return e;  // bulk g-1 done
       // Q(g+1) needs the tail path of g and bulk g-1 (A's square, the panel
-      // slots it gathers into); at g = 0 the main stream's assembly instead
+      // slots it gathers into); at g = 0 the main stream's assembly instead.
+      // The side2 path of g+1 needs the same (its own tail path in order, the
+      // head path through E2).  Without qdirect both wait for ev[2g+1], the
+      // main stream's record after all three.
       if (qdirect) {
         if ((e = hipStreamWaitEvent(side, E2(g), 0)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(side, Eb(g - 1), 0)) != hipSuccess) return e;
-      } else if ((e = hipStreamWaitEvent(side, sy->ev[2 * g + 1], 0)) != hipSuccess) {
-        return e;
+        if ((e = hipStreamWaitEvent(side2, Eb(g - 1), 0)) != hipSuccess) return e;
+      } else {
+        if ((e = hipEventRecord(sy->ev[2 * g + 1], st)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(side, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(side2, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
       }
-      if ((e = hipStreamWaitEvent(side2, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
       if ((e = produce_q(g + 1)) != hipSuccess) return e;
       if (qfirst && (e = hipStreamWaitEvent(st, Eq(g + 1), 0)) != hipSuccess) return e;
     }
