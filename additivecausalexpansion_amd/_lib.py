@@ -107,6 +107,7 @@ SIGNATURES = {
                                                 ctypes.c_char_p, ctypes.POINTER(_vp)]),
     "ace_model_shard_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int),
                                             ctypes.POINTER(ctypes.c_int)]),
+    "ace_model_comm_calls": (ctypes.c_int, [_vp, ctypes.POINTER(_I64)]),
     "ace_model_create_sharded_host": (ctypes.c_int, [_vp, ctypes.c_int, _I64, ctypes.c_int,
                                                      ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                      ctypes.c_void_p, ctypes.POINTER(_vp)]),

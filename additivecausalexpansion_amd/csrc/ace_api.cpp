@@ -1148,6 +1148,13 @@ int ace_model_shard_info(const ace_model *m, int *world, int *rank) {
   return ACE_OK;
 }
 
+int ace_model_comm_calls(const ace_model *m, int64_t *counts) {
+  if (!m || !counts) return ACE_ERR_ARG;
+  for (int j = 0; j < ACE_COMM_KINDS; ++j) counts[j] = 0;
+  if (m->shard) shard_comm_calls(m->shard, counts);
+  return ACE_OK;
+}
+
 int ace_model_train(ace_model *m, int optimizer, double learn_rate, double momentum, double beta1,
                     double beta2, int norm_clip, double clip_at, int maxiter, double tol,
                     double *theta, double *stats, int *iters, int *converged) {

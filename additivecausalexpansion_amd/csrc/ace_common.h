@@ -384,6 +384,7 @@ void shard_eval(ShardModel *m, const double *theta, int use_mu, int which, bool 
 void shard_get_inverse(ShardModel *m, double *inv);
 void shard_collect_timing(ShardModel *m, double *t_ms, int64_t *t_launch, double *t_work);
 int shard_world(const ShardModel *m);
+void shard_comm_calls(const ShardModel *m, int64_t *counts);  // ACE_COMM_KINDS entries
 int shard_any(ShardModel *m, int local);  // collective OR (RCCL), local value (simulated)
 int shard_nlocal(const ShardModel *m);                // ranks simulated in this process (1 with RCCL)
 PairSide shard_train_side(const ShardModel *m);       // the replicated training X, Z, log|Z|

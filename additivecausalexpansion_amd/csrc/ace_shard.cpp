@@ -197,6 +197,13 @@ struct ShardModel {
   bool heads = false;
   ncclComm_t comm2 = nullptr;
   std::vector<std::unique_ptr<RankState>> ranks;  // 1 (RCCL) or G (simulated)
+  // collectives this rank issued (ace_model_comm_calls): RCCL calls or host
+  // callbacks, by ace_comm_kind; simulated and proxy groups issue none
+  int64_t calls[ACE_COMM_KINDS] = {};
+  // a real RCCL communicator: its collectives run at every world size,
+  // world 1 included (the simulated, proxy and host-callback groups treat a
+  // one-rank collective as the identity)
+  bool live() const { return comm != nullptr; }
   DBuf vote;                                       // shard_any: one double
   std::vector<hipEvent_t> ev;                      // lookahead events
   // timing of local rank 0 (update launches, assembly, gradient)
@@ -374,7 +381,7 @@ bool shard_heads_on() {
 // Panel exchange of step k on stream st.
 void exchange(ShardModel &m, int k, hipStream_t st) {
   ace_ctx *ctx = m.ctx;
-  if (m.G == 1) return;  // one rank: both collectives are the identity
+  if (m.G == 1 && !m.live()) return;  // one simulated rank: the identity
   const int64_t k0 = (int64_t)k * NB;
   const size_t nlow = (size_t)((m.naug - k0) * NB);
   const int slots = shard_row_slots(k, m.G);
@@ -385,7 +392,11 @@ void exchange(ShardModel &m, int k, hipStream_t st) {
   if (m.host) {
     RankState &R = *m.ranks[0];
     host_bcast(ctx, m.ops, m.stage, R.low.d(), nlow, root, st);
-    if (nrow > 0) host_allgather(ctx, m.ops, m.stage, own(R), R.recv.d(), nrow, m.G, st);
+    ++m.calls[ACE_COMM_BROADCAST];
+    if (nrow > 0) {
+      host_allgather(ctx, m.ops, m.stage, own(R), R.recv.d(), nrow, m.G, st);
+      ++m.calls[ACE_COMM_ALLGATHER];
+    }
     return;
   }
   if (m.proxy) {  // the bytes this rank receives, as device copies
@@ -408,9 +419,13 @@ void exchange(ShardModel &m, int k, hipStream_t st) {
     nck(ctx, rccl().GroupStart(), "ncclGroupStart");
     nck(ctx, rccl().Broadcast(R.low.p, R.low.p, nlow, ncclDouble, root, m.comm, st),
         "ncclBroadcast");
-    if (nrow > 0)
+    ++m.calls[ACE_COMM_BROADCAST];
+    if (nrow > 0) {
       nck(ctx, rccl().AllGather(own(R), R.recv.p, nrow, ncclDouble, m.comm, st), "ncclAllGather");
+      ++m.calls[ACE_COMM_ALLGATHER];
+    }
     nck(ctx, rccl().GroupEnd(), "ncclGroupEnd");
+    ++m.calls[ACE_COMM_GROUPS];
     return;
   }
   RankState &src = *m.ranks[(size_t)root];
@@ -431,15 +446,30 @@ void exchange(ShardModel &m, int k, hipStream_t st) {
 // The head schedule's two exchanges of panel k: head = the owner's column
 // rows [k0, hend) (rows x NB doubles in lowh, broadcast, on the head path's
 // stream); tail = the rows [hend, naug) (in low, broadcast) and the row
-// pieces (all-gather), on the tail path's stream and the second communicator.
+// pieces (all-gather), on the tail path's stream and the second communicator
+// (host-callback groups: both through the callbacks, each blocking the host
+// between its stream's drain before and after, so the host issues the head
+// and tail exchanges one at a time, in the same order on every rank).
 void exchange_part(ShardModel &m, int k, bool head, int64_t rows, hipStream_t st) {
   ace_ctx *ctx = m.ctx;
-  if (m.G == 1) return;  // one rank: both collectives are the identity
+  if (m.G == 1 && !m.live()) return;  // one simulated rank: the identity
   const size_t nlow = (size_t)(rows * NB);
   const size_t nrow = head ? 0 : (size_t)shard_row_slots(k, m.G) * NB * NB;
   const int root = k % m.G;
   auto lowp = [&](RankState &R) { return head ? R.lowh.d() : R.low.d(); };
   auto own = [&](RankState &R) { return R.recv.d() + (size_t)R.r * nrow; };
+  if (m.host) {
+    RankState &R = *m.ranks[0];
+    if (nlow > 0) {
+      host_bcast(ctx, m.ops, m.stage, lowp(R), nlow, root, st);
+      ++m.calls[ACE_COMM_BROADCAST];
+    }
+    if (nrow > 0) {
+      host_allgather(ctx, m.ops, m.stage, own(R), R.recv.d(), nrow, m.G, st);
+      ++m.calls[ACE_COMM_ALLGATHER];
+    }
+    return;
+  }
   if (m.proxy) {  // the bytes this rank receives, as device copies (timing only)
     RankState &R = *m.ranks[0];
     if (R.r != root && nlow > 0) {
@@ -459,11 +489,16 @@ void exchange_part(ShardModel &m, int k, bool head, int64_t rows, hipStream_t st
     RankState &R = *m.ranks[0];
     ncclComm_t c = head ? m.comm : m.comm2;
     nck(ctx, rccl().GroupStart(), "ncclGroupStart");
-    if (nlow > 0)
+    if (nlow > 0) {
       nck(ctx, rccl().Broadcast(lowp(R), lowp(R), nlow, ncclDouble, root, c, st), "ncclBroadcast");
-    if (nrow > 0)
+      ++m.calls[ACE_COMM_BROADCAST];
+    }
+    if (nrow > 0) {
       nck(ctx, rccl().AllGather(own(R), R.recv.p, nrow, ncclDouble, c, st), "ncclAllGather");
+      ++m.calls[ACE_COMM_ALLGATHER];
+    }
     nck(ctx, rccl().GroupEnd(), "ncclGroupEnd");
+    ++m.calls[ACE_COMM_GROUPS];
     return;
   }
   RankState &src = *m.ranks[(size_t)root];
@@ -485,10 +520,11 @@ void exchange_part(ShardModel &m, int k, bool head, int64_t rows, hipStream_t st
 // (0: augvec, 1: red).
 void allreduce(ShardModel &m, int which, int64_t count, hipStream_t st) {
   ace_ctx *ctx = m.ctx;
-  if (m.G == 1) return;  // one rank: the identity
+  if (m.G == 1 && !m.live()) return;  // one simulated rank: the identity
   auto buf = [&](RankState &R) { return which == 0 ? R.augvec.d() : R.red.d(); };
   if (m.host) {
     host_allreduce(ctx, m.ops, m.stage, buf(*m.ranks[0]), (size_t)count, 0, st);
+    ++m.calls[ACE_COMM_ALLREDUCE];
     return;
   }
   if (m.proxy) {  // a same-size device copy in place of the ring all-reduce
@@ -502,6 +538,7 @@ void allreduce(ShardModel &m, int which, int64_t count, hipStream_t st) {
     double *b = buf(*m.ranks[0]);
     nck(ctx, rccl().AllReduce(b, b, (size_t)count, ncclDouble, ncclSum, m.comm, st),
         "ncclAllReduce");
+    ++m.calls[ACE_COMM_ALLREDUCE];
     return;
   }
   double *acc = buf(*m.ranks[0]);
@@ -511,6 +548,35 @@ void allreduce(ShardModel &m, int which, int64_t count, hipStream_t st) {
     ck(ctx, hipMemcpyAsync(buf(*m.ranks[j]), acc, (size_t)count * sizeof(double),
                            hipMemcpyDeviceToDevice, st),
        "sim all-reduce");
+}
+
+// RCCL connects a communicator's peers at its first collective (host
+// bootstrap exchanges, device buffers).  Each communicator runs here, with
+// no kernel of this library in flight, the grouped broadcast + all-gather
+// the sweep issues on it (and the all-reduce on the first), synchronised: the
+// first evaluation's sweep then finds every connection made.
+void rccl_warmup(ShardModel &m) {
+  ace_ctx *ctx = m.ctx;
+  hipStream_t st = ctx->stream;
+  DBuf w;
+  alloc(ctx, w, (size_t)(m.G + 1) * sizeof(double), "alloc warm-up");
+  ck(ctx, hipMemsetAsync(w.p, 0, w.bytes, st), "memset warm-up");
+  double *b = w.d();
+  for (ncclComm_t c : {m.comm, m.comm2}) {
+    if (!c) continue;
+    nck(ctx, rccl().GroupStart(), "ncclGroupStart");
+    nck(ctx, rccl().Broadcast(b, b, 1, ncclDouble, 0, c, st), "ncclBroadcast (warm-up)");
+    nck(ctx, rccl().AllGather(b + m.rank, b, 1, ncclDouble, c, st), "ncclAllGather (warm-up)");
+    nck(ctx, rccl().GroupEnd(), "ncclGroupEnd");
+    m.calls[ACE_COMM_BROADCAST] += 1;
+    m.calls[ACE_COMM_ALLGATHER] += 1;
+    m.calls[ACE_COMM_GROUPS] += 1;
+    sync_stream(ctx, st, "RCCL warm-up");
+  }
+  nck(ctx, rccl().AllReduce(b + m.G, b + m.G, 1, ncclDouble, ncclSum, m.comm, st),
+      "ncclAllReduce (warm-up)");
+  m.calls[ACE_COMM_ALLREDUCE] += 1;
+  sync_stream(ctx, st, "RCCL warm-up");
 }
 
 // ---- the sharded sweep -------------------------------------------------------
@@ -921,12 +987,13 @@ ShardModel *shard_create_any(ace_ctx *ctx, const Shape &s, int64_t n, int world,
   }
   const int nlocal = m->sim ? world : 1;
   const int steps = (int)(npad / NB);
-  // the head schedule: simulated, proxy and RCCL groups (the host-callback
-  // group keeps the group schedule: its exchanges block the host in turn)
+  // the head schedule in every mode (the host-callback group's head and tail
+  // exchanges block the host one at a time, in issue order)
   m->heads = shard_heads_on() && heads_on() && pair_steps() && steps >= 2 && m->Z >= 2 &&
-             !m->host && (m->sim || m->proxy || rccl().CommSplit);
+             (m->sim || m->proxy || m->host || rccl().CommSplit);
   if (m->heads && m->comm)
     nck(ctx, rccl().CommSplit(m->comm, 0, rank, &m->comm2, nullptr), "ncclCommSplit");
+  if (m->comm) rccl_warmup(*m);
   const int maxslots = shard_row_slots(steps, world);
   const int ncol = s.B * (s.PM + 1);
   for (int j = 0; j < nlocal; ++j) {
@@ -1152,9 +1219,11 @@ void shard_get_inverse(ShardModel *m, double *inv) {
          "gather local columns");
   } else if (m->host) {
     host_allgather(ctx, m->ops, m->stage, m->ranks[0]->A[0].d(), gath.d(), (size_t)slot, m->G, st);
+    ++m->calls[ACE_COMM_ALLGATHER];
   } else {
     nck(ctx, rccl().AllGather(m->ranks[0]->A[0].p, gath.p, (size_t)slot, ncclDouble, m->comm, st),
         "ncclAllGather (inverse)");
+    ++m->calls[ACE_COMM_ALLGATHER];
   }
   alloc(ctx, out, (size_t)(n * n) * sizeof(double), "alloc inverse");
   ck(ctx, launch_sym_from_cyclic(gath.d(), naug, n, m->G, slot, -1.0, out.d(), n, st),
@@ -1191,9 +1260,10 @@ void shard_collect_timing(ShardModel *m, double *t_ms, int64_t *t_launch, double
 // leave the others blocked in the next sweep's collectives.  Simulated
 // groups share the process's poll, so the local value is already common.
 int shard_any(ShardModel *m, int local) {
-  if (m->sim || m->proxy || m->G == 1) return local;
+  if (m->sim || m->proxy || (m->G == 1 && !m->live())) return local;
   ace_ctx *ctx = m->ctx;
   hipStream_t st = ctx->stream;
+  ++m->calls[ACE_COMM_ALLREDUCE];
   if (m->host) {
     double v = local ? 1.0 : 0.0;
     hck(ctx, m->ops.allreduce(m->ops.user, &v, 1, 1), "allreduce (interrupt vote)");
@@ -1219,7 +1289,8 @@ int shard_rank_of(const ShardModel *m, int j) { return m->ranks[(size_t)j]->r; }
 // Sum over ranks of `count` doubles (in place, device).  Simulated groups
 // sum their local partials themselves, so only RCCL has work to do.
 void shard_allreduce_sum(ShardModel *m, double *buf, int64_t count) {
-  if (m->sim || m->proxy || m->G == 1 || count <= 0) return;
+  if (m->sim || m->proxy || (m->G == 1 && !m->live()) || count <= 0) return;
+  ++m->calls[ACE_COMM_ALLREDUCE];
   if (m->host) {
     host_allreduce(m->ctx, m->ops, m->stage, buf, (size_t)count, 0, m->ctx->stream);
     return;
@@ -1230,4 +1301,7 @@ void shard_allreduce_sum(ShardModel *m, double *buf, int64_t count) {
 }
 
 int shard_world(const ShardModel *m) { return m->G; }
+void shard_comm_calls(const ShardModel *m, int64_t *counts) {
+  for (int j = 0; j < ACE_COMM_KINDS; ++j) counts[j] = m->calls[j];
+}
 int shard_rank(const ShardModel *m) { return m->rank; }

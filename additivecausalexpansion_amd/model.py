@@ -142,6 +142,13 @@ class DeviceModel:
                 out[key] = {"map": a[0], "ci": np.array([a[1], a[2]]), "var": a[3]}
         return out
 
+    def comm_calls(self):
+        """ace_model_comm_calls: collectives this rank issued since creation,
+        {"broadcast", "allgather", "allreduce", "groups"} (zeros when simulated)."""
+        c = (ctypes.c_int64 * 4)()
+        check(lib().ace_model_comm_calls(self.handle, c), self.ctx.handle)
+        return dict(zip(("broadcast", "allgather", "allreduce", "groups"), c))
+
     def profile(self, enable):
         check(lib().ace_model_profile(self.handle, 1 if enable else 0), self.ctx.handle)
 

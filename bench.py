@@ -57,6 +57,11 @@ N1 = 16384  # C2
 
 
 def _dist_init():
+    # every launch path (self-launch child, external torchrun, --mode sharded):
+    # RCCL shares buffers across processes by dmabuf IPC, which this host
+    # driver requires; the HSA runtime reads the switch when HIP first
+    # initialises, i.e. after this line
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -401,9 +406,7 @@ def self_launch(a, argv):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1",
            f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL across processes)
-    proc = subprocess.Popen(cmd, env=env)
+    proc = subprocess.Popen(cmd, env=dict(os.environ))  # each rank: _dist_init's environment
     try:
         return proc.wait()
     except KeyboardInterrupt:

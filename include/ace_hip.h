@@ -362,6 +362,24 @@ int ace_model_create_sharded(ace_ctx *ctx, int kind, int64_t n, int p, int B,
 /* world / rank of a model (1 / 0 for ace_model_create models) */
 int ace_model_shard_info(const ace_model *m, int *world, int *rank);
 
+/* Collectives this rank has issued since the model was created, by kind
+ * (counts[ACE_COMM_KINDS]): RCCL calls of an ace_model_create_sharded model
+ * -- at every world size, 1 included -- or host callbacks of an
+ * ace_model_create_sharded_host model.  ACE_COMM_GROUPS counts the RCCL
+ * ncclGroupStart/End launches (a sweep step's broadcast + all-gather).
+ * Simulated groups (id == NULL) and single-GPU models issue none.  Per
+ * evaluation of the head / tail sweep over S = ceil(n / 256) steps: 2 S
+ * broadcasts, the all-gathers of steps with row pieces, 2 all-reduces plus
+ * the interrupt vote; creation adds RCCL's warm-up calls. */
+enum ace_comm_kind {
+  ACE_COMM_BROADCAST = 0,
+  ACE_COMM_ALLGATHER = 1,
+  ACE_COMM_ALLREDUCE = 2,
+  ACE_COMM_GROUPS = 3,
+  ACE_COMM_KINDS = 4
+};
+int ace_model_comm_calls(const ace_model *m, int64_t *counts);
+
 /* Host-callback collectives: the same sharded model with every exchange
  * (panel broadcast + all-gather per sweep step, the two all-reduces per
  * evaluation, the interrupt vote, the inverse gather) routed through

@@ -31,8 +31,12 @@ def main():
                       host_comm=HostComm())
     m.set_data(y, X, Z, sy)
     res = {}
+    keys = ("broadcast", "allgather", "allreduce", "groups")
+    c0 = m.comm_calls()
     th1 = th.copy()
     g1, st1, mu1 = m.para_update(1, th1)
+    # host callbacks of one evaluation (the head / tail exchange split)
+    res["calls_eval1"] = np.array([m.comm_calls()[k] - c0[k] for k in keys])
     th2 = th1 + 0.01 * np.sin(np.arange(th1.size))
     g2, st2, _ = m.para_update(2, th2)
     res.update(theta1=th1, g1=g1, st1=st1, mu1=np.array([mu1]), theta2=th2, g2=g2, st2=st2)

@@ -171,7 +171,11 @@ def test_c4_fullsize_sharded8_and_rccl_match_single(A):
                        sharded=True)
     rc.set_data(y, X, Z, sy)
     t3 = th.copy()
+    c0 = rc.comm_calls()
     g3, s3, _ = rc.para_update(1, t3)
+    # every sweep collective issued over RCCL (256 steps: 512 groups)
+    from test_shard_gpu import eval_calls
+    assert {k: v - c0[k] for k, v in rc.comm_calls().items()} == eval_calls(n, 1)
     close(g3, g1, 1e-9, 1e-11)
     close(s3, s1, 1e-10, 0)
     rc.close()

@@ -62,15 +62,24 @@ def _run_group(world, out, kind, n, p, B):
 @pytest.mark.parametrize("world,kind,n,p,B", [(2, "SE", 700, 3, 4), (3, "Matern32", 900, 5, 5),
                                               (2, "Matern32", 2000, 6, 5)])
 def test_sharded_processes_match_single_gpu_and_oracle(A, O, tmp_path, world, kind, n, p, B):
-    """The pair-step lookahead schedule runs in every rank process: the bulk
+    """The head / tail lookahead schedule runs in every rank process: the bulk
     update of group g is in flight while the rank's host exchanges group
-    g+1's panels (n = 2000: 8 sweep steps, 4 groups).  The processes'
+    g+1's panels, each panel's head rows (head path) and tail rows + row
+    pieces (tail path) in separate blocking exchanges (n = 2000: 8 sweep
+    steps, 3 groups).  The processes'
     inverse equals the in-process simulated group's of the same world size
     bit for bit (same kernels, same operand order; only the transport and the
     concurrency differ), the all-reduced sums to the last bits, and the
     single-GPU model and the oracle to rounding."""
     r = _run_group(world, str(tmp_path / "r.npz"), kind, n, p, B)
     y, X, Z, sy = r["y"], r["X"], r["Z"], float(r["sy"][0])
+    # the processes ran the head / tail schedule: every step's exchange split
+    # into a head broadcast and a tail broadcast (+ all-gather), host callbacks
+    from test_shard_gpu import eval_calls
+    want = eval_calls(n, world)
+    want["groups"] = 0  # RCCL group launches: none over host callbacks
+    assert dict(zip(("broadcast", "allgather", "allreduce", "groups"),
+                    r["calls_eval1"].tolist())) == want, r["calls_eval1"]
     # every rank returned the same gradient
     for q in range(1, world):
         assert np.array_equal(r["g2_all_ranks"][q], r["g2_all_ranks"][0])

@@ -204,10 +204,14 @@ def test_sharded_rccl_world1_predict(A, O):
     sh.set_data(y, X, Z, sy)
     sh.para_update(2, th0.copy())
     X2, Z2 = _test_points(p, B, nx, seed=9)
+    c0 = sh.comm_calls()["allreduce"]
     close(sh.predict(th, X2, Z2, 0.0, 1.0)["map"], single.predict(th, X2, Z2, 0.0, 1.0)["map"],
           1e-8, 1e-9)
+    c1 = sh.comm_calls()["allreduce"]
     V = np.random.default_rng(1).normal(size=(n, 3))
     close(sh.apply_inverse(V), single.apply_inverse(V), 1e-8, 1e-9)
+    # the rank-partial products are summed by RCCL all-reduces (world 1 included)
+    assert c1 > c0 and sh.comm_calls()["allreduce"] > c1
 
 
 @pytest.mark.parametrize("kernel", ["SE", "Matern32"])

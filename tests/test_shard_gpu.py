@@ -6,8 +6,15 @@ every rank has its own local column blocks, panel buffers and tile lists,
 and the broadcast / all-gather / all-reduce are device copies with the
 RCCL semantics, so the packing, ownership maps and redundant pivot chains
 are the ones the multi-process run uses.  A world-size-1 RCCL communicator
-runs the real RCCL code path (dlopen, ncclCommInitRank, grouped broadcast +
-all-gather, all-reduce) on the single card.
+runs the real RCCL code path on the single card: dlopen, ncclCommInitRank,
+ncclCommSplit, the creation warm-up, and every collective of the sweep --
+each step's grouped head broadcast (first communicator, side stream) and
+tail broadcast + all-gather (second communicator, second side stream), the
+two all-reduces and the interrupt vote per evaluation, the inverse's
+all-gather -- counted by ace_model_comm_calls and asserted call for call.
+With one rank those collectives move no bytes between GPUs; results are
+bitwise equal to the simulated one-rank group, whose collectives are the
+identity.
 
 Tolerances as in test_gpu.py: gradients / stats 1e-6 relative (north star),
 inverse 1e-9 of its scale."""
@@ -106,22 +113,63 @@ def test_sharded_train_stats_keeps_inverse(A, O):
     assert np.array_equal(m.inverse(), inv1)  # Q6
 
 
-def test_sharded_rccl_world1_matches_oracle(A, O):
-    """A real RCCL communicator (world size 1): the multi-process code path --
-    RCCL loaded by dlopen, grouped broadcast + all-gather per step,
-    all-reduces -- on one card."""
+def eval_calls(n, world):
+    """Collectives of one para_update of the head / tail sweep on one rank
+    (DESIGN.md §7): per step a head broadcast and a tail broadcast, one
+    RCCL group each; an all-gather of row pieces in every step after the
+    first; the all-reduces of the AUG rows and of the gradient sums, and the
+    interrupt vote."""
+    S = -(-n // 256)
+    return {"broadcast": 2 * S, "allgather": S - 1, "allreduce": 3, "groups": 2 * S}
+
+
+def _delta(after, before):
+    return {k: after[k] - before[k] for k in after}
+
+
+@pytest.mark.parametrize("n", [900, 2300])
+def test_sharded_rccl_world1_matches_oracle(A, O, n):
+    """A real RCCL communicator (world size 1): the multi-process code path
+    on one card, with every sweep collective issued (counted call for call)
+    and results bitwise equal to the simulated one-rank group's (identity
+    collectives).  n = 900: 4 sweep steps in 2 groups; 2300: 9 steps."""
     from additivecausalexpansion_amd.synthetic import make_problem
     uid = A.comm_unique_id()
     assert len(uid) == 128
-    n, p, B = 900, 4, 4
+    p, B = 4, 4
     y, X, Z, th, sy = make_problem(n, p, B, seed=9)
     m = A.DeviceModel("Matern32", n, p, B, world=1, rank=0, unique_id=uid, sharded=True)
+    c0 = m.comm_calls()
+    # creation: the warm-up's grouped broadcast + all-gather on both
+    # communicators and one all-reduce
+    assert c0 == {"broadcast": 2, "allgather": 2, "allreduce": 1, "groups": 2}, c0
     m.set_data(y, X, Z, sy)
-    g, st, _ = m.para_update(1, th.copy())
+    t1 = th.copy()
+    g, st, mu = m.para_update(1, t1)
+    c1 = m.comm_calls()
+    assert _delta(c1, c0) == eval_calls(n, 1), (c1, c0)
+    t2 = th + 0.01
+    g2, st2, _ = m.para_update(2, t2.copy())
+    c2 = m.comm_calls()
+    assert _delta(c2, c1) == eval_calls(n, 1)
+    inv_r = m.inverse()
+    assert _delta(m.comm_calls(), c2) == {"broadcast": 0, "allgather": 1, "allreduce": 0, "groups": 0}
+    # the simulated one-rank group (collectives are the identity, none issued)
+    s = A.DeviceModel("Matern32", n, p, B, world=1, rank=0, sharded=True)
+    s.set_data(y, X, Z, sy)
+    ts1 = th.copy()
+    gs, sts, mus = s.para_update(1, ts1)
+    gs2, sts2, _ = s.para_update(2, t2.copy())
+    assert s.comm_calls() == {"broadcast": 0, "allgather": 0, "allreduce": 0, "groups": 0}
+    assert np.array_equal(g, gs) and np.array_equal(st, sts) and mu == mus
+    assert np.array_equal(t1, ts1)
+    assert np.array_equal(g2, gs2) and np.array_equal(st2, sts2)
+    assert np.array_equal(inv_r, s.inverse())
+    s.close()
     _, g_ref, st_ref, inv = _oracle_eval(O, "Matern32", y, X, Z, th, sy, B, 1)
     close(g, g_ref)
     close(st, st_ref)
-    close(m.inverse(), inv["inv"], 1e-9, 1e-9)
+    m.close()
 
 
 def test_sharded_large_residual(A):
