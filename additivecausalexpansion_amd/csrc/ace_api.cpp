@@ -119,11 +119,8 @@ int ace_create(int device, ace_ctx **out) {
     e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi);
     if (e == hipSuccess) c->nstreams = 2;
     if (e == hipSuccess && nstr >= 3) {
-#ifdef ACE_DIAG_SIDE2_NORMAL  // A/B build: the tail path at the main stream's priority
-      e = hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, 0);
-#else
+      // (at the main stream's priority instead: neutral)
       e = hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, hi);
-#endif
       if (e == hipSuccess) c->nstreams = 3;
     }
   }

@@ -53,12 +53,8 @@ extern std::string g_create_err;
 // Events that only order work on this device (the sweep's cross-stream
 // hand-offs) or time it: no system-scope fence on record / wait -- the
 // default release writes back L2 for host visibility, ~20 us per sweep step.
-#ifndef ACE_EVENT_FENCE
-#define ACE_EVENT_FENCE 0
-#endif
-#define ACE_SYNC_EVENT_FLAGS \
-  (hipEventDisableTiming | (ACE_EVENT_FENCE ? 0u : (unsigned)hipEventDisableSystemFence))
-#define ACE_TIMING_EVENT_FLAGS (ACE_EVENT_FENCE ? 0u : (unsigned)hipEventDisableSystemFence)
+#define ACE_SYNC_EVENT_FLAGS (hipEventDisableTiming | (unsigned)hipEventDisableSystemFence)
+#define ACE_TIMING_EVENT_FLAGS ((unsigned)hipEventDisableSystemFence)
 
 namespace ace_host {
 using namespace ace;

@@ -50,15 +50,6 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 #ifndef ACE_MM_QG2
 #define ACE_MM_QG2 1
 #endif
-// Gradient A/B switches: row sums R_r gathered through LDS (1) or
-// ds_bpermute (0); GEMM2 epilogue row covariates in registers (1: spills at
-// the 4-wave register cap) or read from LDS per slice (0)
-#ifndef ACE_GRAD_RVLDS
-#define ACE_GRAD_RVLDS 0
-#endif
-#ifndef ACE_GRAD_XIREG
-#define ACE_GRAD_XIREG 0
-#endif
 // GEMM2's last column block when PM is not a multiple of 16 (p = 20: 4 live
 // features of 16): on v_mfma_f64_4x4x4_4b_f64 (ACE_GRAD_TAIL4=1, default),
 // one 4-feature group per instruction at 17 cycles instead of a 16-wide
@@ -397,22 +388,14 @@ __device__ __forceinline__ void tile_of(const Tile *tiles, int64_t t, int64_t &I
 // loops read only LDS and registers, apart from the row values z_r, whose
 // load is issued ahead of each slice's GEMM1.
 // ---------------------------------------------------------------------------
-// LDS pitch of the staged column covariates XJ: GEMM1 reads XJ[(cbase + lr)
-// XP + lk + 4 kk] with ds_read_b64, whose 32-lane halves conflict unless the
-// 16 rows lr land on distinct 4-bank groups, i.e. XP = 2 (mod 4)
-// (ACE_XJ_PAD=1; 0, the default: the dense PM + 1 pitch, 2-way conflicts for
-// odd PM + 1).  Measured neutral at C2 (gradient 4.80 / 4.81 ms, assembly
-// 2.35 / 2.35 ms, profiles/r03_grad_ab.txt): the kernels are bound by the
-// fp64 dependency chains, not by LDS.
-#ifndef ACE_XJ_PAD
-#define ACE_XJ_PAD 0
-#endif
-__host__ __device__ constexpr int xj_pitch(int PM) {
-  return ACE_XJ_PAD ? PM + 1 + ((6 - (PM + 1) % 4) % 4) : PM + 1;
-}
+// LDS pitch of the staged column covariates XJ: the dense PM + 1 (a padded
+// pitch without GEMM1's 2-way ds_read_b64 conflicts measured neutral at C2,
+// profiles/r03_grad_ab.txt: the kernels are bound by the fp64 dependency
+// chains, not by LDS)
+__host__ __device__ constexpr int xj_pitch(int PM) { return PM + 1; }
 
 struct MmLayout {
-  int etab, xj, xi, z, lz, nc, nr, w, red, red_slices, rv, total;
+  int etab, xj, xi, z, lz, nc, nr, w, red, red_slices, total;
 };
 
 // Gradient partials: one buffer per slice (no barrier inside the slice
@@ -446,14 +429,12 @@ __host__ __device__ inline MmLayout mm_layout(int PM, int B, int KIND, bool grad
     o.red_slices = (B * per * 8 <= 40 * 1024) ? B : 2;
     off += o.red_slices * per + nwave;
   }
-  o.rv = off;  // gradient, ACE_GRAD_RVLDS: each wave's 16 row sums R_r of the current slice
-  if (grad && ACE_GRAD_RVLDS) off += 16 * nwave;
   o.total = off;
   return o;
 }
 
 struct MmLds {
-  double *E, *XJ, *XI, *Z, *LZ, *Nc, *Nr, *W, *Red, *Rv;
+  double *E, *XJ, *XI, *Z, *LZ, *Nc, *Nr, *W, *Red;
   int red_slices;
 };
 
@@ -478,7 +459,6 @@ __device__ __forceinline__ MmLds mm_stage(double *lds, PairSide S, int B, int ZS
   L.Nr = lds + o.nr;
   L.W = lds + o.w;
   L.Red = lds + o.red;
-  L.Rv = lds + o.rv;
   L.red_slices = o.red_slices;
   for (int e = tid; e < 64 * PM; e += NT) {
     const int c = e / PM, i = e - c * PM;
@@ -958,20 +938,12 @@ __device__ __forceinline__ double rcp_nr_mm(double f) {
   return fma(q, e, q);
 }
 
-// Lane exchanges of the gradient's slice loop without the LDS crossbar
-// (ACE_GRAD_DPP=1): xor 1 / 2 / 4 / 8 inside a 16-lane row by DPP moves
-// (xor 4 = row_half_mirror, then the quad reversal; xor 8 = row_ror 8),
-// and the xor-16 / xor-32 sums by gfx950's v_permlane16/32_swap.  Each lane
-// gets the same partner value as __shfl_xor (ds_bpermute), and a + b is
-// commutative, so the sums are bit-identical.
-#ifndef ACE_GRAD_DPP
-#define ACE_GRAD_DPP 1
-#endif
-// wave priority experiment: 1 = raised around the GEMMs, 2 = around the
-// per-pair VALU section, 0 = none
-#ifndef ACE_GRAD_PRIO
-#define ACE_GRAD_PRIO 1
-#endif
+// Lane exchanges of the gradient's slice loop without the LDS crossbar: xor
+// 1 / 2 / 4 / 8 inside a 16-lane row by DPP moves (xor 4 = row_half_mirror,
+// then the quad reversal; xor 8 = row_ror 8), and the xor-16 / xor-32 sums
+// by gfx950's v_permlane16/32_swap.  Each lane gets the same partner value
+// as __shfl_xor (ds_bpermute), and a + b is commutative, so the sums are
+// bit-identical to the ds_bpermute form they replaced (round 2).
 template <int CTRL>
 __device__ __forceinline__ double dpp64(double v) {
   const unsigned long long u = __double_as_longlong(v);
@@ -981,7 +953,6 @@ __device__ __forceinline__ double dpp64(double v) {
 }
 // v of lane (this lane xor m), m = 1, 2, 4, 8
 __device__ __forceinline__ double xor_row(double v, int m) {
-  if (!ACE_GRAD_DPP) return __shfl_xor(v, m, 64);
   if (m == 1) return dpp64<0xB1>(v);          // quad_perm [1,0,3,2]
   if (m == 2) return dpp64<0x4E>(v);          // quad_perm [2,3,0,1]
   if (m == 4) return dpp64<0x1B>(dpp64<0x141>(v));  // xor 7, then xor 3
@@ -994,7 +965,6 @@ __device__ __forceinline__ double pair_sum(int a_lo, int a_hi, int b_lo, int b_h
 }
 // v + v(lane xor 16), v + v(lane xor 32), in every lane
 __device__ __forceinline__ double add_xor16(double v) {
-  if (!ACE_GRAD_DPP) return v + __shfl_xor(v, 16, 64);
   const unsigned long long u = __double_as_longlong(v);
   const int lo = (int)(unsigned)u, hi = (int)(unsigned)(u >> 32);
   const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
@@ -1002,7 +972,6 @@ __device__ __forceinline__ double add_xor16(double v) {
   return pair_sum(l[0], h[0], l[1], h[1]);
 }
 __device__ __forceinline__ double add_xor32(double v) {
-  if (!ACE_GRAD_DPP) return v + __shfl_xor(v, 32, 64);
   const unsigned long long u = __double_as_longlong(v);
   const int lo = (int)(unsigned)u, hi = (int)(unsigned)(u >> 32);
   const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
@@ -1076,23 +1045,18 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   const int64_t r = R0 + rl;
   const bool rvalid = r < n;
   const double *wlast = (KIND == 1) ? tab.wg + (B - 1) * PM : tab.wk;
-  // the tile's A and alpha values are loaded before the staging (ACE_GRAD_PRELOAD,
-  // default), so their latency overlaps the staging loads and barriers
-#ifndef ACE_GRAD_PRELOAD
-#define ACE_GRAD_PRELOAD 1
-#endif
+  // the tile's A and alpha values are loaded before the staging, so their
+  // latency overlaps the staging loads and barriers
   double av[CB][4], alc[CB][4];
-  if (ACE_GRAD_PRELOAD) {
 #pragma unroll
-    for (int cb = 0; cb < CB; ++cb)
+  for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int64_t c = C0 + cbase + 16 * cb + lk + 4 * v;
-        const bool ok = rvalid && c < n && !(I == J && c > r);
-        av[cb][v] = ok ? A[r + c * ld] : 0.0;
-        alc[cb][v] = ok ? alpha[c] : 0.0;
-      }
-  }
+    for (int v = 0; v < 4; ++v) {
+      const int64_t c = C0 + cbase + 16 * cb + lk + 4 * v;
+      const bool ok = rvalid && c < n && !(I == J && c > r);
+      av[cb][v] = ok ? A[r + c * ld] : 0.0;
+      alc[cb][v] = ok ? alpha[c] : 0.0;
+    }
   const double ar = rvalid ? alpha[r] : 0.0;
   const MmLds L = mm_stage<PM, KIND, true, NT>(lds, S, B, ZS, tab.wk, wlast, R0, C0, tid,
                                                tab.norms, tab.ldn);
@@ -1107,7 +1071,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
       const int64_t c = C0 + cbase + 16 * cb + lk + 4 * v;
       double x = 0.0;
       if (rvalid && c < n && !(I == J && c > r)) {
-        x = ACE_GRAD_PRELOAD ? sA * av[cb][v] - ar * alc[cb][v] : sA * A[r + c * ld] - ar * alpha[c];
+        x = sA * av[cb][v] - ar * alc[cb][v];
         if (c == r) tr += x;
         else x *= 2.0;
       }
@@ -1115,19 +1079,6 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
     }
   RowX<PM, XIL> xr;  // x_r from the staged rows when they are in LDS
   xr.load(XIL ? L.XI + rl * (PM + 1) : S.X + r * PM, lk);
-  // GEMM2 epilogue row covariates x[16 wr + lk + 4 v][16 q + lr]: the same
-  // for every slice, so held in registers (ACE_GRAD_XIREG) where they fit
-  constexpr bool XIR = ACE_GRAD_XIREG && XIL && CB == 2 && NQ <= 2;
-  double xiv[XIR ? NQ : 1][4];
-  if (XIR) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int nn = 16 * q + lr;
-        xiv[q][v] = nn < PM ? L.XI[(16 * wr + lk + 4 * v) * (PM + 1) + nn] : 0.0;
-      }
-  }
   // tail (TAIL4): this lane's output element of group t is row 16 wr + 4 m4
   // + i4, feature 16 NQF + 4 t + j4; its covariate is the same every slice
   const int i4 = lane >> 4, m4 = (lane >> 2) & 3, j4 = lane & 3;
@@ -1198,10 +1149,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
 #define ACE_DIAG_GRAD 0
 #endif
   const int bstop = (ACE_DIAG_GRAD & 3) == 1 ? B : (ACE_DIAG_GRAD & 3) == 2 ? B - 1 : 0;
-#ifndef ACE_GRAD_UNROLL
-#define ACE_GRAD_UNROLL 1
-#endif
-#pragma unroll ACE_GRAD_UNROLL
+#pragma unroll 1
   for (int b = B - 1; b >= bstop; --b) {
     double *red = L.Red + (per_slice ? b : (b & 1)) * PER;
     double zr = 1.0, lzr = 0.0;  // issued ahead of GEMM1, which hides the latency
@@ -1209,10 +1157,10 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
       zr = S.Z[r * ZS + b - 1];
       if (KIND == 0) lzr = S.LZ[r * ZS + b - 1];
     }
-    if (ACE_GRAD_PRIO == 1) __builtin_amdgcn_s_setprio(2);
+    // waves raise their priority while issuing the two GEMM chains
+    __builtin_amdgcn_s_setprio(2);
     gemm1_mm<XP, CB>(L.XJ, xr, L.W + b * PM, lr, lk, acc, cbase);
-    if (ACE_GRAD_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-    if (ACE_GRAD_PRIO == 2) __builtin_amdgcn_s_setprio(2);
+    __builtin_amdgcn_s_setprio(0);
     const double sr = L.Nr[b * 64 + rl];
     const double *nc = L.Nc + b * 64 + cbase;
     const double *zcol = L.Z + (b - 1) * 64 + cbase;
@@ -1265,21 +1213,9 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
     rs = add_xor16(rs);
     rs = add_xor32(rs);
     double Rv[4];
-    if (ACE_GRAD_RVLDS) {
-      // through the wave's LDS slot: one write, four reads (LDS operations of
-      // one wave execute in order) instead of four 64-bit ds_bpermute pairs
-      double *rvs = L.Rv + 16 * w;
-      if (lk == 0) rvs[lr] = rs;
-      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int v = 0; v < 4; ++v) Rv[v] = rvs[lk + 4 * v];
-      __builtin_amdgcn_wave_barrier();
-    } else {
-#pragma unroll
-      for (int v = 0; v < 4; ++v) Rv[v] = __shfl(rs, lk + 4 * v, 64);  // row 16 wr + lk + 4v
-    }
-    if (ACE_GRAD_PRIO == 2) __builtin_amdgcn_s_setprio(0);
-    if (ACE_GRAD_PRIO == 1) __builtin_amdgcn_s_setprio(2);
+    for (int v = 0; v < 4; ++v) Rv[v] = __shfl(rs, lk + 4 * v, 64);  // row 16 wr + lk + 4v
+    __builtin_amdgcn_s_setprio(2);
     // GEMM2: V = U X_J, QG column blocks per pass of the k-loop
 #pragma unroll
     for (int q0 = 0; q0 < ((ACE_DIAG_GRAD & 32) ? 0 : NQF); q0 += QG) {
@@ -1308,8 +1244,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
             const int rr = 16 * wr + lk + 4 * v;
-            const double x = XIR ? xiv[q0 + j][v]
-                                 : XIL ? L.XI[rr * (PM + 1) + nn] : S.X[(R0 + rr) * PM + nn];
+            const double x = XIL ? L.XI[rr * (PM + 1) + nn] : S.X[(R0 + rr) * PM + nn];
             part += fma(x * x, Rv[v], -2.0 * x * a2[j][v]);
           }
         }
@@ -1333,7 +1268,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
         __builtin_amdgcn_sched_barrier(0);
       }
       // R of row 4 m4 + i4 (rs holds row lr's sum in every lane of that lr)
-      const double R4 = ACE_GRAD_RVLDS ? L.Rv[16 * w + 4 * m4 + i4] : __shfl(rs, 4 * m4 + i4, 64);
+      const double R4 = __shfl(rs, 4 * m4 + i4, 64);
 #pragma unroll
       for (int t4 = 0; t4 < NT4; ++t4) {
         const double x = x4[t4];
@@ -1345,7 +1280,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
         if (lane < 4) red[w * RS + 16 * NQF + 4 * t4 + j4] = part;
       }
     }
-    if (ACE_GRAD_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
     // C_c: column sums of U over the wave's 16 rows, reduce-scatter over lr
     {
       // (after GEMM2: U's registers are free again)

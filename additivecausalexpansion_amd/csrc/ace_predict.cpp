@@ -88,12 +88,10 @@ void require_inverse(ace_model *m) {
 
 }  // namespace
 
-// The device prediction pipeline (pred_cpp / pred_marginal_cpp semantics)
-// over abstract operands -- the device model's resident inverse here, and the
-// device-matrix handles of the R6-faithful path in ace_dmat.cpp.
-void pred_pipeline(const PredOps &op, int64_t nx, bool marginal, const double *Z_x, int ate,
-                   double sigma, double mu, double mean_y, double std_y, double std_Z,
-                   double *map, double *ci, double *var, double *avg) {
+namespace {
+void pred_pipeline_once(const PredOps &op, int64_t nx, bool marginal, const double *Z_x, int ate,
+                        double sigma, double mu, double mean_y, double std_y, double std_Z,
+                        double *map, double *ci, double *var, double *avg) {
   ace_ctx *ctx = op.ctx;
   hipStream_t st = ctx->stream;
   const int64_t n = op.n;
@@ -194,6 +192,46 @@ void pred_pipeline(const PredOps &op, int64_t nx, bool marginal, const double *Z
   for (int j = 0; j < 3; ++j) post[(size_t)j] = q3[(size_t)j] - dots[(size_t)j];
   finish_marginal(nx, ad.data(), kd.data(), ad.data() + nx, std_y, std_Z,
                   ate ? zx.data() : nullptr, ate ? post.data() : nullptr, map, ci, var, avg);
+}
+
+// retained scratch above this size is released after the call (n = 16384,
+// nx = 4096 keeps its 1.1 GB; n = 65536 with 8192-point chunks frees 8.6 GB)
+constexpr size_t PRED_KEEP_BYTES = size_t(4) << 30;
+
+void release_pred_state(ace_ctx *ctx) {
+  if (auto ps = std::static_pointer_cast<PredScratch>(ctx->pred_state)) {
+    ps->K.release();
+    ps->T.release();
+    ps->Kxx.release();
+  }
+  ctx->pred_state.reset();
+}
+}  // namespace
+
+// The device prediction pipeline (pred_cpp / pred_marginal_cpp semantics)
+// over abstract operands -- the device model's resident inverse here, and the
+// device-matrix handles of the R6-faithful path in ace_dmat.cpp.  The large
+// scratch (K_xX, T', K_xx chunks) stays in the context between calls; an
+// allocation failure inside the call frees it -- all three buffers, including
+// the ones the failed call still referenced -- and runs the call once more
+// (outputs are written only at its end), and scratch above PRED_KEEP_BYTES
+// is not kept past the call.
+void pred_pipeline(const PredOps &op, int64_t nx, bool marginal, const double *Z_x, int ate,
+                   double sigma, double mu, double mean_y, double std_y, double std_Z,
+                   double *map, double *ci, double *var, double *avg) {
+  ace_ctx *ctx = op.ctx;
+  try {
+    pred_pipeline_once(op, nx, marginal, Z_x, ate, sigma, mu, mean_y, std_y, std_Z, map, ci, var, avg);
+  } catch (const Fail &f) {
+    if (f.code != ACE_ERR_OOM) throw;
+    (void)hipGetLastError();
+    sync(ctx);  // the failed call's launches may still read the scratch
+    release_pred_state(ctx);
+    ctx->sweep_pool.clear();
+    pred_pipeline_once(op, nx, marginal, Z_x, ate, sigma, mu, mean_y, std_y, std_Z, map, ci, var, avg);
+  }
+  if (auto ps = std::static_pointer_cast<PredScratch>(ctx->pred_state))
+    if (ps->K.bytes + ps->T.bytes + ps->Kxx.bytes > PRED_KEEP_BYTES) release_pred_state(ctx);
 }
 
 namespace {

@@ -37,18 +37,10 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // latency-bound work) share CUs with the MFMA-heavy update tiles of the main
 // stream.  Raising their waves' issue priority lets them win the SIMD
 // arbitration instead of getting a 1/5 share of the issue slots.
-#ifndef ACE_PIVOT_RCP
-#define ACE_PIVOT_RCP 1
-#endif
-// (3 on them and on the head-path gather k_update_q: C1 -0.06 ms on one box,
-// +0.01 on another, C2 +0.15 ms -- not kept, profiles/r05_v19_ab_prio.txt)
-#ifndef ACE_CHAIN_PRIO
-#define ACE_CHAIN_PRIO 1
-#endif
-#define CHAIN_PRIO() \
-  do {               \
-    if (ACE_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(ACE_CHAIN_PRIO); \
-  } while (0)
+// (Priority 3 on them and on the head-path gather k_update_q: C1 -0.06 ms
+// on one box, +0.01 on another, C2 +0.15 ms -- not kept,
+// profiles/r05_v19_ab_prio.txt.)
+#define CHAIN_PRIO() __builtin_amdgcn_s_setprio(1)
 
 // ---------------------------------------------------------------- pivot
 // Sweeps the 64x64 sub-block s of the panel's pivot rows:
@@ -95,15 +87,11 @@ __device__ __forceinline__ void pivot_sweep(double (&v)[SUB / NW], PivotLds<NW> 
       // 1/d by v_rcp_f64 + two Newton steps (<= 1 ulp): five dependent fp64
       // operations on the chain's critical path instead of the eleven of
       // the IEEE division sequence
-#if ACE_PIVOT_RCP
       double rd = __builtin_amdgcn_rcp(d);
       double re = fma(-d, rd, 1.0);
       rd = fma(rd, re, rd);
       re = fma(-d, rd, 1.0);
       rd = fma(rd, re, rd);
-#else
-      const double rd = 1.0 / d;
-#endif
       const double dit = L.colb[buf][lane];
       double rt[CW];
 #pragma unroll
@@ -156,9 +144,6 @@ __device__ __forceinline__ void pivot_sweep(double (&v)[SUB / NW], PivotLds<NW> 
 #ifndef ACE_PIVOT_BLK
 #define ACE_PIVOT_BLK 1
 #endif
-#ifndef ACE_PGEMM_HEAD_DEPTH
-#define ACE_PGEMM_HEAD_DEPTH 1
-#endif
 #ifndef ACE_BULK_RESERVE_N
 #define ACE_BULK_RESERVE_N 8192
 #endif
@@ -204,15 +189,11 @@ __device__ __forceinline__ void blk_pivot(double (&x)[4], int r, int g, double &
 #pragma unroll
   for (int e = 0; e < 4; ++e) rw[e] = row_bcast<T>(x[e]);
   const double d = row_bcast<T>(c);      // M(t, t)
-#if ACE_PIVOT_RCP
-  double rd = __builtin_amdgcn_rcp(d);
+  double rd = __builtin_amdgcn_rcp(d);  // + two Newton steps, as in pivot_sweep
   double re = fma(-d, rd, 1.0);
   rd = fma(rd, re, rd);
   re = fma(-d, rd, 1.0);
   rd = fma(rd, re, rd);
-#else
-  const double rd = 1.0 / d;
-#endif
   // branch-free (selects): row t gets M(t, j) / d, column t M(i, t) / d,
   // the pivot -1/d, the rest M(i, j) - M(i, t) M(t, j) / d
   const bool isrow = r == T;
@@ -801,17 +782,13 @@ constexpr int LDL = 144;    // LDS row pitch (doubles): 128 + 16, bank-conflict 
 constexpr int NCH = NB / BK;
 constexpr int UTHREADS = 512;
 // Panel staging (the update / panel-GEMM kernels): each thread moves two
-// double2 of a BK x width chunk row.  ACE_STAGE_SPLIT=1 (default): the two
-// halves of the row (sm and sm + width / 2, sm = 2 (lane % (width / 4))), so
-// each ds_write_b128 lane group of 8 covers 128 contiguous bytes -- all 32
-// write banks -- instead of 8 lanes 32 bytes apart (2-way conflicts,
-// MI355X_MICROARCH.md LDS table).  The LDS layout and the MFMA reads are
-// unchanged: bit-identical.  0: 4 consecutive doubles per thread.
-#ifndef ACE_STAGE_SPLIT
-#define ACE_STAGE_SPLIT 1
-#endif
-constexpr int SM128 = ACE_STAGE_SPLIT ? 2 : 4, SH128 = ACE_STAGE_SPLIT ? 64 : 2;
-constexpr int SM64 = ACE_STAGE_SPLIT ? 2 : 4, SH64 = ACE_STAGE_SPLIT ? 32 : 2;
+// double2 of a BK x width chunk row, the two halves of the row (sm and sm +
+// width / 2, sm = 2 (lane % (width / 4))), so each ds_write_b128 lane group
+// of 8 covers 128 contiguous bytes -- all 32 write banks -- instead of 8
+// lanes 32 bytes apart (2-way conflicts, MI355X_MICROARCH.md LDS table; the
+// round-4 change, -0.3 ms per C2 evaluation, bit-identical).
+constexpr int SM128 = 2, SH128 = 64;
+constexpr int SM64 = 2, SH64 = 32;
 constexpr int XSPLIT_HEAD = 8;  // entries of the split cross's head launch (3 tiles + padding)
 static_assert(BK == 16, "staging maps 512 threads x 4 doubles onto a 128 x 16 chunk");
 
@@ -1093,7 +1070,6 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update(double *__restrict__ A, 
 // update's pipelined 8-wave tile: under the bulk update k_panel_gemm's 64-row
 // strips held 258 update-sized CU slots for ~185 us per panel (skipping it
 // took 6 ms off a C2 evaluation, profiles/r02_chain_ab.txt).
-template <int DEPTH>
 __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict__ W,
                                                               const double *__restrict__ Pn,
                                                               int64_t ldp, int64_t k0, int G,
@@ -1112,20 +1088,12 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
   const int sk = tid >> 5, sm = (tid & 31) * SM128;  // 2nd half at sm + SH128
-#ifdef ACE_DIAG_PGEMM_HOT  // timing diagnostic only (results wrong): every tile reads rows 0..127
-  const double *gW = Pn + sm + (int64_t)sk * ldp;
-#else
   const double *gW = Pn + (R0 + sm) + (int64_t)sk * ldp;
-#endif
   const double *gP = W + (k0 + C0 + sm) + (int64_t)sk * ldp;  // W_kk(c, k) = W[k0 + c, k]
-  // DEPTH = 2 (round 5; the head path's launches): two chunks of loads in
-  // flight -- a chunk is loaded into one of two register sets two iterations
-  // before it is staged, so its latency overlaps two chunks' MFMAs instead
-  // of one.  The head launches have few workgroups, each walking all 16
-  // chunks, and were bound by that latency (C1 trace: 35-45 us for 8.4
-  // MFLOP per workgroup).  DEPTH = 1: one chunk ahead in 108 VGPRs (two
-  // workgroups per CU for the many-workgroup tail launches; the second set
-  // takes 132).  Same MFMA chain in the same k order: bit-identical.
+  // One chunk of loads in flight, in 108 VGPRs (two workgroups per CU).  A
+  // two-deep pipeline (round 5) needed 132 VGPRs: under a bulk launch of
+  // 128-VGPR waves it waited for two of them to leave a SIMD, C2 +4.4 ms
+  // (profiles/r05_v3_ab_c2.txt); the head launches use k_panel_gemm_q.
   const int wr = wv & 1, wc = wv >> 1;
   d4 acc[2][4];
 #pragma unroll
@@ -1134,7 +1102,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
     for (int ri = 0; ri < 4; ++ri) acc[ci][ri] = d4{0.0, 0.0, 0.0, 0.0};
   // the two register sets as named values (arrays passed to helpers ended
   // up in scratch)
-  double2 w00, w01, p00, p01, w10, w11, p10, p11;
+  double2 w00, w01, p00, p01;
 #define PG_LOAD(W0, W1, P0, P1, CH)                                               \
   do {                                                                            \
     const int64_t off_ = (int64_t)(CH) * BK * ldp;                                \
@@ -1165,8 +1133,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
           acc[ci][ri] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ci], b[ri], acc[ci][ri], 0, 0, 0);
     }
   };
-  static_assert(NCH % 2 == 0 && NCH >= 4, "two chunks per pipeline turn");
-  if constexpr (DEPTH == 1) {
+  {
     PG_LOAD(w00, w01, p00, p01, 0);
     PG_STAGE(w00, w01, p00, p01, 0);
     __syncthreads();
@@ -1178,29 +1145,6 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_panel_gemm_t(double *__restrict
       if (ch + 1 < NCH) PG_STAGE(w00, w01, p00, p01, cur ^ 1);
       __syncthreads();
     }
-  } else {
-  PG_LOAD(w00, w01, p00, p01, 0);
-  PG_STAGE(w00, w01, p00, p01, 0);
-  PG_LOAD(w10, w11, p10, p11, 1);
-  PG_LOAD(w00, w01, p00, p01, 2);
-  __syncthreads();
-  ACE_WGT_MARK(0);
-  // turn: chunk ch (even) from LDS 0 while chunk ch+1 (set 1) is staged into
-  // LDS 1 and chunk ch+3 loaded into set 1; then chunk ch+1 from LDS 1 while
-  // chunk ch+2 (set 0) goes to LDS 0 and chunk ch+4 into set 0
-#pragma unroll 1
-  for (int ch = 0; ch < NCH; ch += 2) {
-    mma(0);
-    PG_STAGE(w10, w11, p10, p11, 1);
-    if (ch + 3 < NCH) PG_LOAD(w10, w11, p10, p11, ch + 3);
-    __syncthreads();
-    mma(1);
-    if (ch + 2 < NCH) {
-      PG_STAGE(w00, w01, p00, p01, 0);
-      if (ch + 4 < NCH) PG_LOAD(w00, w01, p00, p01, ch + 4);
-    }
-    __syncthreads();
-  }
   }
 #undef PG_LOAD
 #undef PG_STAGE
@@ -1684,6 +1628,20 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_multi(double *__restrict
   }
   if (kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT))) return;
   update_multi_tile<SH>(I, J, sW, sP, A, ld, ps, npan, ldp, ka0, go, G);
+}
+
+// CUs of the current device, read once per device (the persistent queue's
+// grid: two workgroups per CU; 256 on MI355X, fewer on a harvested part)
+static int device_cu_count() {
+  static int cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
 }
 
 // Small n (run_sweep_heads with b.breserve > 0): the bulk launch as a
@@ -2300,7 +2258,7 @@ static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, dou
   // on the second side stream)
   if (before_gemm) (void)hipStreamWaitEvent(st, before_gemm, 0);
   if (pgemm_tiles())
-    hipLaunchKernelGGL(k_panel_gemm_t<1>, dim3((unsigned)(ld / UT), NB / UT), dim3(UTHREADS), 0, st,
+    hipLaunchKernelGGL(k_panel_gemm_t, dim3((unsigned)(ld / UT), NB / UT), dim3(UTHREADS), 0, st,
                        W, Pn, ld, k0, G, r, 0, 1 << 30, 1 << 30);
   else
     hipLaunchKernelGGL(k_panel_gemm, dim3((unsigned)(ld / SUB)), dim3(512), 0, st, W, Pn, ld, k0,
@@ -3145,19 +3103,11 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   auto pgemm = [&](int k, int r0, int r1, bool head, hipStream_t s_) {
     const int n = head ? r1 - r0 : (int)nT - (r1 - r0);
     if (n <= 0) return;
-    // ACE_PGEMM_HEAD_DEPTH=2 (A/B build): the head rows with two chunks in
-    // flight.  It needs 132 VGPRs: a wave of it fits on a SIMD only after two
-    // of the bulk launch's 128-VGPR waves have left, so under the bulk launch
-    // the head GEMM starves (C2 +4.4 ms same-box, profiles/r05_v3_ab_c2.txt)
-    if (head && ACE_PGEMM_HEAD_DEPTH == 2)
-      hipLaunchKernelGGL(k_panel_gemm_t<2>, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, s_,
-                         b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, 1, 0, r0, 1 << 30,
-                         1 << 30);
-    else if (head && ACE_PGEMM_HEADQ)
+    if (head && ACE_PGEMM_HEADQ)
       hipLaunchKernelGGL(k_panel_gemm_q, dim3((unsigned)(n * (UT / XT)), NB / XT), dim3(256), 0, s_,
                          b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, r0);
     else
-      hipLaunchKernelGGL(k_panel_gemm_t<1>, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, s_,
+      hipLaunchKernelGGL(k_panel_gemm_t, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, s_,
                          b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, 1, 0, head ? r0 : 0,
                          head ? 1 << 30 : r0, head ? 1 << 30 : r1);
   };
@@ -3307,7 +3257,8 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
         ps.R[j] = j < zsize(g) ? b.W[slot(kg + j)] : nullptr;
         ps.C[j] = j < zsize(g) ? b.P[slot(kg + j)] : nullptr;
       }
-      hipLaunchKernelGGL(k_update_multi_r<false>, dim3(2 * 256), dim3(UTHREADS), 0, st, b.A, b.ld,
+      // one workgroup per launch slot: two per CU (k_update_multi_r's occupancy)
+      hipLaunchKernelGGL(k_update_multi_r<false>, dim3(2 * device_cu_count()), dim3(UTHREADS), 0, st, b.A, b.ld,
                          ps, zsize(g), b.ld, (int64_t)kg * NB, kx0, kx1, ord, grid,
                          b.bq + (int64_t)g * BQ_INTS, b.breserve, no_gather());
     } else {
@@ -3533,7 +3484,7 @@ hipError_t shard_pgemm(const ShardSweep &b, int k, int buf, int rt_lo, int rt_hi
   const int nT = (int)(b.ld / UT);
   const int n = head ? rt_hi - rt_lo : nT - (rt_hi - rt_lo);
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_panel_gemm_t<1>, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, st, b.W[buf],
+  hipLaunchKernelGGL(k_panel_gemm_t, dim3((unsigned)n, NB / UT), dim3(UTHREADS), 0, st, b.W[buf],
                      b.P[buf], b.ld, (int64_t)k * NB, b.G, b.r, head ? rt_lo : 0,
                      head ? 1 << 30 : rt_lo, head ? 1 << 30 : rt_hi);
   return hipGetLastError();

@@ -44,6 +44,21 @@ def ref_c():
     return L
 
 
+def record_error(check, measured, bound):
+    """Appends one measured error beside the bound it is held to, as a JSON
+    line to $ACE_ERROR_LOG (unset: nothing is written).  tools/error_table.py
+    turns the log of a GPU run into the committed error table
+    (profiles/r06_error_table.txt), so drift toward a bound is visible."""
+    path = os.environ.get("ACE_ERROR_LOG")
+    if not path:
+        return
+    import json
+    test = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
+    with open(path, "a") as f:
+        f.write(json.dumps({"test": test, "check": check, "measured": float(measured),
+                            "bound": float(bound)}) + "\n")
+
+
 def run_child(code, env=None, timeout=100):
     """Runs a Python snippet in a fresh interpreter (a clean HIP runtime per
     A/B variant).  A child that stalls dumps every thread's Python stack

@@ -16,18 +16,25 @@ import numpy as np
 
 from conftest import run_child
 import pytest
-from conftest import golden, golden_names
+from conftest import golden, golden_names, record_error
 
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-6
 
 
-def close(a, b, rtol=RTOL, atol_rel=1e-9):
+def close(a, b, rtol=RTOL, atol_rel=1e-9, check="close"):
     a = np.asarray(a, dtype=float)
     b = np.asarray(b, dtype=float)
     scale = np.abs(b).max() if b.size else 0.0
-    ok = np.abs(a - b) <= rtol * np.abs(b) + atol_rel * scale
+    bound = rtol * np.abs(b) + atol_rel * scale
+    ok = np.abs(a - b) <= bound
+    if b.size and np.all(np.isfinite(a)) and np.all(np.isfinite(b)):
+        # the fraction of the bound the worst element uses (1 = at the bound)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            use = np.where(bound > 0, np.abs(a - b) / bound, np.where(a == b, 0.0, np.inf))
+        record_error(f"{check} (rtol {rtol:g}, atol {atol_rel:g} max|ref|): bound used",
+                     float(use.max()), 1.0)
     if not np.all(ok):
         i = np.argmax(np.abs(a - b) - rtol * np.abs(b))
         raise AssertionError(f"mismatch at {np.unravel_index(i, b.shape)}: {a.flat[i]} vs "

@@ -14,6 +14,7 @@ import sys
 
 import numpy as np
 import pytest
+from conftest import record_error
 from test_gpu import close
 
 pytestmark = pytest.mark.gpu
@@ -119,10 +120,12 @@ def test_sharded_processes_match_single_gpu_and_oracle(A, O, tmp_path, world, ki
     g1, st1, mu1 = m.para_update(1, th1)
     # the sharded sweep's operand order differs from the single GPU's (R = Pn,
     # C = W): gradient and stats agree to 1e-9
+    record_error("processes theta1[1] (mu): |err| / mu_terms", abs(th1[1] - r["theta1"][1]) / mu_terms, 2e-13)
     assert abs(th1[1] - r["theta1"][1]) <= mu_tol, (th1[1], r["theta1"][1], mu_tol)
     close(np.delete(th1, 1), np.delete(r["theta1"], 1), 1e-9, 1e-12)
     close(g1, r["g1"], 1e-9, 1e-11)
     close(st1, r["st1"], 1e-9, 1e-12)
+    record_error("processes mu_post: |err| / mu_terms", abs(mu1 - float(r["mu1"][0])) / mu_terms, 2e-13)
     assert abs(mu1 - float(r["mu1"][0])) <= mu_tol, (mu1, r["mu1"][0], mu_tol)
     g2, st2, _ = m.para_update(2, r["theta2"].copy())
     close(g2, r["g2"], 1e-9, 1e-11)

@@ -11,7 +11,7 @@ of the cancelled terms std_y^2 (|K_xx,rr| + q_r).
 """
 import numpy as np
 
-from conftest import run_child
+from conftest import record_error, run_child
 import pytest
 from test_gpu import close
 
@@ -72,6 +72,7 @@ def test_device_predict_matches_oracle(A, O, kernel, n, p, B, nx):
     close(got["map"], ref["map"])
     close(got["ci"], ref["ci"], 1e-6, 1e-8)
     terms = _var_terms(O, kernel, X2, Z2, th, 1.7, inv, K_xX, np.exp(th[0]))
+    record_error("predict var: max |err| / terms", np.max(np.abs(got["var"] - ref["var"]) / terms), 1e-6)
     assert np.all(np.abs(got["var"] - ref["var"]) <= 1e-6 * terms)
 
 
@@ -94,6 +95,7 @@ def test_device_predict_marginal_ate_matches_oracle(A, O, kernel, B):
     kxx = np.diag(Km_xx[:, :, sl].sum(axis=2))
     q = np.abs(np.sum((KmX @ inv) * KmX, axis=1))
     terms = (1.7 / 0.8) ** 2 * (np.abs(kxx) + q)
+    record_error("marginal var: max |err| / terms", np.max(np.abs(got["var"] - ref["var"]) / terms), 1e-6)
     assert np.all(np.abs(got["var"] - ref["var"]) <= 1e-6 * terms)
     for k in ("ate", "att", "atu"):
         close(got[k]["map"], ref[k]["map"])
@@ -103,6 +105,9 @@ def test_device_predict_marginal_ate_matches_oracle(A, O, kernel, B):
         # it by the terms it is formed from (as the variance check above)
         sd = np.sqrt(abs(ref[k]["var"]))
         tol = 1e-6 * (abs(ref[k]["map"]) + 1.96 * sd) + 1e-8 * np.abs(ref[k]["ci"]).max()
+        record_error(f"{k} ci: max |err| / tol", np.max(np.abs(got[k]["ci"] - ref[k]["ci"]) / tol), 1.0)
+        record_error(f"{k} ci: max |err| / (|map| + 1.96 sd)",
+                     np.max(np.abs(got[k]["ci"] - ref[k]["ci"])) / (abs(ref[k]["map"]) + 1.96 * sd), 1e-6)
         assert np.all(np.abs(got[k]["ci"] - ref[k]["ci"]) <= tol), (k, got[k]["ci"], ref[k]["ci"], tol)
     plain = m.predict_marginal(th, X2, dZ2, zx, 1.7, 0.8, False)
     assert "ate" not in plain and np.array_equal(plain["map"], got["map"])

@@ -10,7 +10,10 @@ from conftest import golden, golden_names
 
 from referee_ld import para_update_ld
 
-NAMES = golden_names("referee_")
+ALL = golden_names("referee_")
+# fixtures with stored inputs (the multi-group n = 2600 fixture stores a seed
+# and an input digest instead; its check is the GPU test and the digest below)
+NAMES = [n for n in ALL if "gen" not in golden(n)]
 
 
 def _ld(d, key):
@@ -44,6 +47,24 @@ def test_fp64_oracle_matches_referee(name, kernel):
     assert _rel(g, _ld(d, kernel + "_g"), 1e-9) < 1e-11
     assert _rel(st, _ld(d, kernel + "_st"), 0.0) < 1e-12
     assert _rel([t[1]], _ld(d, kernel + "_mu"), 0.0) < 1e-10
+
+
+def test_multigroup_referee_inputs_regenerate():
+    """The n = 2600 fixture's inputs come from the seeded generator: their
+    digest is the one stored beside the referee's outputs."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_referee import input_digest
+    from additivecausalexpansion_amd.synthetic import make_problem
+    big = [n for n in ALL if n not in NAMES]
+    assert big == ["referee_p20_n2600"]
+    d = golden(big[0])
+    n, p, B, seed = (int(v) for v in d["gen"])
+    assert n >= 2600 and -(-n // 256) >= 3 * 3  # at least three groups of Z = 3 steps
+    assert input_digest(*make_problem(n, p, B, seed=seed)) == str(d["input_sha256"][0])
+    for kernel in ("SE", "Matern32"):
+        assert d[kernel + "_g_hi"].size == 2 + B * (p + 1)
 
 
 def test_referee_fixture_regenerates():

@@ -16,7 +16,7 @@ only at p = 20.  Stats 5e-11 relative (measured <= 5e-12); mu 1e-9 relative
 (it cancels: its terms are ~1e5 times mu; measured <= 4e-11)."""
 import numpy as np
 import pytest
-from conftest import golden, golden_names
+from conftest import golden, golden_names, record_error
 
 pytestmark = pytest.mark.gpu
 
@@ -41,7 +41,17 @@ def A():
 @pytest.mark.parametrize("kernel", ["SE", "Matern32"])
 def test_fused_model_matches_extended_precision_referee(A, name, kernel):
     d = golden(name)
-    y, X, Z, th, sy = d["y"], d["X"], d["Z"], d["theta"], float(d["std_y"][0])
+    if "gen" in d:  # inputs regenerated from the seed, pinned by their digest
+        import sys
+        import os
+        sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+        from make_referee import input_digest
+        from additivecausalexpansion_amd.synthetic import make_problem
+        n_, p_, B_, seed = (int(v) for v in d["gen"])
+        y, X, Z, th, sy = make_problem(n_, p_, B_, seed=seed)
+        assert input_digest(y, X, Z, th, sy) == str(d["input_sha256"][0]), "generator drift"
+    else:
+        y, X, Z, th, sy = d["y"], d["X"], d["Z"], d["theta"], float(d["std_y"][0])
     n, p = X.shape
     B = Z.shape[1] + 1
     m = A.DeviceModel(kernel, n, p, B)
@@ -52,9 +62,14 @@ def test_fused_model_matches_extended_precision_referee(A, name, kernel):
     err = np.abs(np.asarray(g, dtype=np.longdouble) - g_ref)
     bound = GRAD_REL * np.abs(g_ref) + GRAD_FLOOR * np.max(np.abs(g_ref))
     i = int(np.argmax(err / bound))
+    gmax = float(np.max(np.abs(g_ref)))
+    record_error("referee gradient: max_i err_i / max|g_ref|", float(err.max()) / gmax, GRAD_FLOOR)
+    record_error("referee gradient: max_i err_i / bound_i", float(np.max(err / bound)), 1.0)
     assert np.all(err <= bound), (f"gradient index {i} of {g.size}: error {float(err[i]):.3e} "
                                   f"> bound {float(bound[i]):.3e} (value {float(g_ref[i]):.3e})")
     es = float(np.max(np.abs(np.asarray(st, dtype=np.longdouble) - st_ref) / np.abs(st_ref)))
+    record_error("referee stats: relative error", es, STATS_TOL)
     assert es <= STATS_TOL, f"stats rel err {es:.2e}"
     em = float(abs(np.longdouble(mu) - mu_ref) / abs(mu_ref))
+    record_error("referee mu: relative error", em, MU_TOL)
     assert em <= MU_TOL, f"mu rel err {em:.2e}"
