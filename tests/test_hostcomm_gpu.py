@@ -111,7 +111,8 @@ def test_sharded_processes_match_single_gpu_and_oracle(A, O, tmp_path, world, ki
     # two inverses that agree to a relative delta give mus that agree to
     # ~delta * that sum, so mu is bounded by the sum, not by mu
     mu_terms = 0.5 * float((np.abs(inv["inv"]) @ np.abs(y)).sum()) / abs(float(inv["inv"].sum()))
-    mu_tol = 2e-13 * mu_terms
+    # <= 5x the largest measured (1.7e-16 mu_terms, profiles/r06_error_table.txt)
+    mu_tol = 8e-16 * mu_terms
     # the single-GPU model on the same data and thetas
     m = A.DeviceModel(kind, n, p, B)
     m.set_data(y, X, Z, sy)
@@ -120,12 +121,12 @@ def test_sharded_processes_match_single_gpu_and_oracle(A, O, tmp_path, world, ki
     g1, st1, mu1 = m.para_update(1, th1)
     # the sharded sweep's operand order differs from the single GPU's (R = Pn,
     # C = W): gradient and stats agree to 1e-9
-    record_error("processes theta1[1] (mu): |err| / mu_terms", abs(th1[1] - r["theta1"][1]) / mu_terms, 2e-13)
+    record_error("processes theta1[1] (mu): |err| / mu_terms", abs(th1[1] - r["theta1"][1]) / mu_terms, 8e-16)
     assert abs(th1[1] - r["theta1"][1]) <= mu_tol, (th1[1], r["theta1"][1], mu_tol)
     close(np.delete(th1, 1), np.delete(r["theta1"], 1), 1e-9, 1e-12)
     close(g1, r["g1"], 1e-9, 1e-11)
     close(st1, r["st1"], 1e-9, 1e-12)
-    record_error("processes mu_post: |err| / mu_terms", abs(mu1 - float(r["mu1"][0])) / mu_terms, 2e-13)
+    record_error("processes mu_post: |err| / mu_terms", abs(mu1 - float(r["mu1"][0])) / mu_terms, 8e-16)
     assert abs(mu1 - float(r["mu1"][0])) <= mu_tol, (mu1, r["mu1"][0], mu_tol)
     g2, st2, _ = m.para_update(2, r["theta2"].copy())
     close(g2, r["g2"], 1e-9, 1e-11)

@@ -4,10 +4,12 @@ the resident inverse of the last para_update (Q6: theta_{T-1}) with kernels
 at the caller's theta_T, against the oracle's pred_cpp / pred_marginal_cpp
 (src/pred_cpp.cpp:8-126) fed the oracle's own kernels and inverse.
 
-Tolerances (north star 1e-6 relative fp64): map / ci relative 1e-6; the
+Tolerances (north star 1e-6 relative fp64): map relative 1e-6; the
 variance is |K_xx - tmp K_xX^T (+ e^sigma)|, a difference of terms up to
-cond x larger than the result under Q6's theta mix, so it is held to 1e-6
-of the cancelled terms std_y^2 (|K_xx,rr| + q_r).
+cond x larger than the result under Q6's theta mix, so it is held to a
+fraction of the cancelled terms std_y^2 (|K_xx,rr| + q_r) -- VAR_TOL, and the
+ATE/ATT/ATU intervals map -+ 1.96 sd to CI_TOL of |map| + 1.96 sd, both set
+at <= 5x the largest error measured (profiles/r06_error_table.txt).
 """
 import numpy as np
 
@@ -16,6 +18,13 @@ import pytest
 from test_gpu import close
 
 pytestmark = pytest.mark.gpu
+
+# Round 6: the variance and interval bounds at <= 5x the largest error
+# measured (profiles/r06_error_table.txt): variances 3.5e-10 of the terms
+# their quadratic forms cancel, ATE/ATT/ATU intervals 5.2e-8 of |map| + 1.96 sd
+# (round 5: 1e-6 of each, the north star's tolerance)
+VAR_TOL = 1.5e-9
+CI_TOL = 2.5e-7
 
 
 @pytest.fixture(scope="module")
@@ -72,8 +81,8 @@ def test_device_predict_matches_oracle(A, O, kernel, n, p, B, nx):
     close(got["map"], ref["map"])
     close(got["ci"], ref["ci"], 1e-6, 1e-8)
     terms = _var_terms(O, kernel, X2, Z2, th, 1.7, inv, K_xX, np.exp(th[0]))
-    record_error("predict var: max |err| / terms", np.max(np.abs(got["var"] - ref["var"]) / terms), 1e-6)
-    assert np.all(np.abs(got["var"] - ref["var"]) <= 1e-6 * terms)
+    record_error("predict var: max |err| / terms", np.max(np.abs(got["var"] - ref["var"]) / terms), VAR_TOL)
+    assert np.all(np.abs(got["var"] - ref["var"]) <= VAR_TOL * terms)
 
 
 @pytest.mark.parametrize("kernel", ["SE", "Matern32"])
@@ -95,8 +104,8 @@ def test_device_predict_marginal_ate_matches_oracle(A, O, kernel, B):
     kxx = np.diag(Km_xx[:, :, sl].sum(axis=2))
     q = np.abs(np.sum((KmX @ inv) * KmX, axis=1))
     terms = (1.7 / 0.8) ** 2 * (np.abs(kxx) + q)
-    record_error("marginal var: max |err| / terms", np.max(np.abs(got["var"] - ref["var"]) / terms), 1e-6)
-    assert np.all(np.abs(got["var"] - ref["var"]) <= 1e-6 * terms)
+    record_error("marginal var: max |err| / terms", np.max(np.abs(got["var"] - ref["var"]) / terms), VAR_TOL)
+    assert np.all(np.abs(got["var"] - ref["var"]) <= VAR_TOL * terms)
     for k in ("ate", "att", "atu"):
         close(got[k]["map"], ref[k]["map"])
         close(got[k]["var"], ref[k]["var"], 1e-6, 1e-10)
@@ -104,10 +113,9 @@ def test_device_predict_marginal_ate_matches_oracle(A, O, kernel, B):
         # bound relative to ci itself is below the inverse's rounding; bound
         # it by the terms it is formed from (as the variance check above)
         sd = np.sqrt(abs(ref[k]["var"]))
-        tol = 1e-6 * (abs(ref[k]["map"]) + 1.96 * sd) + 1e-8 * np.abs(ref[k]["ci"]).max()
-        record_error(f"{k} ci: max |err| / tol", np.max(np.abs(got[k]["ci"] - ref[k]["ci"]) / tol), 1.0)
+        tol = CI_TOL * (abs(ref[k]["map"]) + 1.96 * sd)
         record_error(f"{k} ci: max |err| / (|map| + 1.96 sd)",
-                     np.max(np.abs(got[k]["ci"] - ref[k]["ci"])) / (abs(ref[k]["map"]) + 1.96 * sd), 1e-6)
+                     np.max(np.abs(got[k]["ci"] - ref[k]["ci"])) / (abs(ref[k]["map"]) + 1.96 * sd), CI_TOL)
         assert np.all(np.abs(got[k]["ci"] - ref[k]["ci"]) <= tol), (k, got[k]["ci"], ref[k]["ci"], tol)
     plain = m.predict_marginal(th, X2, dZ2, zx, 1.7, 0.8, False)
     assert "ate" not in plain and np.array_equal(plain["map"], got["map"])

@@ -12,18 +12,25 @@ g_16 = 2.4e-3 against 110) cannot meet 1e-10 relative to themselves; the
 2e-12 floor is 500 times below the 1e-9 max floor of the other parity
 tests and ~10 times above the errors measured at every bucket.  A change
 claimed bit-identical or ulp-level is checked here at every PM bucket, not
-only at p = 20.  Stats 5e-11 relative (measured <= 5e-12); mu 1e-9 relative
-(it cancels: its terms are ~1e5 times mu; measured <= 4e-11)."""
+only at p = 20, and on a multi-group sweep (n = 2600: 11 steps, four
+groups of Z = 3 -- the persistent bulk queue, the fused D_0 pivot at the
+group boundaries, the blocked pivot across groups).  Stats 8e-12 relative
+(measured <= 1.7e-12); mu 1.5e-10 relative (it cancels: its terms are ~1e5
+times mu; measured <= 3.1e-11).  Round 6 set every bound here at <= 5x the
+largest measured error (profiles/r06_error_table.txt)."""
 import numpy as np
 import pytest
 from conftest import golden, golden_names, record_error
 
 pytestmark = pytest.mark.gpu
 
-GRAD_REL = 1e-10
+# round 6: each bound <= 5x the largest error measured over every fixture
+# (profiles/r06_error_table.txt: gradient 1.15e-12 max|g| at the floor, 0.17 of
+# the round-5 combined bound; stats 1.70e-12; mu 3.09e-11)
+GRAD_REL = 5e-11
 GRAD_FLOOR = 2e-12
-STATS_TOL = 5e-11
-MU_TOL = 1e-9
+STATS_TOL = 8e-12
+MU_TOL = 1.5e-10
 
 
 def _ld(d, key):
