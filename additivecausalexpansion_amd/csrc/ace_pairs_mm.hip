@@ -1144,7 +1144,8 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   // every pair its own basic block, running its dependent fp64 chain alone)
   // ACE_DIAG_GRAD (timing diagnostics only, results wrong): 1 runs no slice,
   // 2 only the last slice; bits 4 / 8 / 16 / 32 drop the sqrt / exp /
-  // reciprocal / GEMM2 of the Matern slice loop
+  // reciprocal / GEMM2 of the Matern slice loop; bit 64 the per-slice
+  // partials' combination after the loop (column-sum combine + feature dots)
 #ifndef ACE_DIAG_GRAD
 #define ACE_DIAG_GRAD 0
 #endif
@@ -1335,7 +1336,7 @@ __global__ __launch_bounds__(64 * 4 * (4 / CB), (CB == 2 ? ACE_MM_GRAD_WPE : 2))
   double *str = L.Red + L.red_slices * PER;
   if (lane == 0) str[w] = tr;
   __syncthreads();
-  if (per_slice) {  // all slices' partials at once
+  if (per_slice && !(ACE_DIAG_GRAD & 64)) {  // all slices' partials at once
     // each slice's four row-block column sums added once (same expression,
     // so bit-identical), not once per feature
     for (int e = tid; e < B * 64; e += NT) {
