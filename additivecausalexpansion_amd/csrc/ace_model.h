@@ -82,8 +82,15 @@ struct SweepWork {
       }
     }
     breserve = (Z > 2 && heads_on()) ? bulk_reserve(naug) : 0;
-    if (breserve > 0)
-      alloc(ctx, bq, (size_t)((npad / NB + Z - 1) / Z * BQ_INTS) * sizeof(int), "alloc bulk queues");
+    if (breserve > 0) {
+      // + per sweep step the barrier and exit counters of k_panel_split4: zero
+      // when allocated, reset by each launch's last workgroup (the per-sweep
+      // memset covers the queues only: the first chain can start before it)
+      void *const old = bq.p;
+      alloc(ctx, bq, (size_t)((npad / NB + Z - 1) / Z * BQ_INTS + 2 * (npad / NB)) * sizeof(int),
+            "alloc bulk queues");
+      if (bq.p != old) ck(ctx, hipMemsetAsync(bq.p, 0, bq.bytes, ctx->stream), "memset queues");
+    }
     xoff.clear();
     if (cross_update_on_tiles()) {
       const std::vector<Tile> t = cross_update_tiles(naug, (int)(npad / NB), xoff);

@@ -543,24 +543,17 @@ __global__ __launch_bounds__(256) void k_panel(double *__restrict__ W, int64_t l
 // saves one launch -- and its wait for a free CU slot under the bulk update
 // -- per sub-step.  Every element sees k_panel's / k_pivot's operations in
 // their order: bit-identical.
-__global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int64_t ldp,
-                                                     int64_t k0, int s,
-                                                     const double *__restrict__ SW,
-                                                     const double *__restrict__ S,
-                                                     double *__restrict__ Snext,
-                                                     double *__restrict__ Xb,
-                                                     double *__restrict__ SWn,
-                                                     double *__restrict__ piv,
-                                                     int *__restrict__ flag) {
-  ACE_WGT(2, true);
-  CHAIN_PRIO();
-  __shared__ double sSW[SUB][PLD];  // sSW[b][a] = SW(a, b)
-  __shared__ double sSt[SUB][SLD];  // sSt[c][t] = S(t, 64 cc + c)
-  __shared__ PivotLds<4> PL;
+template <class Mark>
+__device__ __forceinline__ void panel_split_step(
+    double *__restrict__ W, int64_t ldp, int64_t k0, int s, const double *__restrict__ SW,
+    const double *__restrict__ S, double *__restrict__ Snext, double *__restrict__ Xb,
+    double *__restrict__ SWn, double *__restrict__ piv, int *__restrict__ flag,
+    double (&sSW)[SUB][PLD], double (&sSt)[SUB][SLD], PivotLds<4> &PL, int g, int cc,
+    const Mark &mark) {
+  // sSW[b][a] = SW(a, b); sSt[c][t] = S(t, 64 cc + c)
   constexpr int NS = NB / SUB;
   constexpr int64_t CH = (int64_t)NB * SUB;  // one chunk buffer
   double *const V0 = Xb + 2 * CH;
-  const int g = blockIdx.x, cc = blockIdx.y;
   const bool pivrows = g == s;
   const bool nextrows = s + 1 < NS && g == s + 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -614,7 +607,7 @@ __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int
     }
   }
   __syncthreads();
-  ACE_WGT_MARK(0);
+  mark(0);
   d4 acc1[4];
   if (pivrows) {
 #pragma unroll
@@ -665,7 +658,7 @@ __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int
       if (xnext) xnext[(int64_t)c * NB] = acc[j];
     }
   }
-  ACE_WGT_MARK(1);
+  mark(1);
   if (!fusepiv) return;
   // D_{s+1}: accs[ctc][j] = D(srow, 16 ctc + lk + 4 j) -> lane = row layout
   __syncthreads();  // every wave is done with sSW (phase 1)
@@ -678,14 +671,105 @@ __global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int
 #pragma unroll
   for (int q = 0; q < SUB / 4; ++q) v[q] = sSW[16 * w + q][lane];
 #if ACE_PIVOT_BLK
-  ACE_WGT_MARK(2);
+  mark(2);
   pivot_sweep_blk<SLD>(v, sSt, PL.pv, tid);  // sSt is free (the update phase is done)
 #else
-  ACE_WGT_MARK(2);
+  mark(2);
   pivot_sweep<4>(v, PL, tid);
 #endif
-  ACE_WGT_MARK(3);
+  mark(3);
   pivot_store<4>(v, PL.pv, tid, SWn, piv, k0 + (int64_t)(s + 1) * SUB, flag);
+}
+
+
+__global__ __launch_bounds__(256) void k_panel_split(double *__restrict__ W, int64_t ldp,
+                                                     int64_t k0, int s,
+                                                     const double *__restrict__ SW,
+                                                     const double *__restrict__ S,
+                                                     double *__restrict__ Snext,
+                                                     double *__restrict__ Xb,
+                                                     double *__restrict__ SWn,
+                                                     double *__restrict__ piv,
+                                                     int *__restrict__ flag) {
+  ACE_WGT(2, true);
+  CHAIN_PRIO();
+  __shared__ double sSW[SUB][PLD];
+  __shared__ double sSt[SUB][SLD];
+  __shared__ PivotLds<4> PL;
+  auto mark = [&](int i) { (void)i; ACE_WGT_MARK(i); };
+  panel_split_step(W, ldp, k0, s, SW, S, Snext, Xb, SWn, piv, flag, sSW, sSt, PL, (int)blockIdx.x,
+                   (int)blockIdx.y, mark);
+}
+
+// The four sub-steps of the split panel sweep in ONE launch (ACE_CHAIN_FUSE,
+// small n): the same 16 workgroups run sub-step s = 0 .. 3, each the
+// workgroup (g, cc) of k_panel_split's grid, with a grid barrier between the
+// sub-steps instead of a launch boundary -- every workgroup keeps its CU slot
+// across the chain, and the next sub-step's workgroups do not wait for a
+// dispatch.  Every workgroup does exactly k_panel_split's work in the same
+// order: bit-identical.  The barrier: each workgroup drains its stores,
+// releases them at agent scope (they cross the XCDs' L2s) and adds 1 to
+// ctr[0]; sub-step s + 1 starts when ctr[0] reaches 16 (s + 1) and the
+// workgroup has acquired.  The 16 workgroups need not be resident at once
+// to make progress: a waiting one only spins (s_sleep) while the others are
+// dispatched as other launches' workgroups leave.  Bounded: a wait over 0.5 s
+// sets *flag = 2 (read like a non-positive pivot: the evaluation reports NaN)
+// and goes on, so every wave reaches the exit.  ctr[0] (barrier) and ctr[1]
+// (exits) start at zero: the last workgroup out resets both for the next
+// sweep's launch on this panel slot (by then every other workgroup has
+// passed every barrier).
+__device__ __forceinline__ void chain_barrier(int *ctr, int target, int *flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > 50000000ull) {  // 100 MHz counter: 0.5 s
+        __hip_atomic_store(flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256, 2) void k_panel_split4(double *__restrict__ W, int64_t ldp,
+                                                      int64_t k0, double *__restrict__ SW,
+                                                      double *__restrict__ S0,
+                                                      double *__restrict__ S1,
+                                                      double *__restrict__ piv,
+                                                      int *__restrict__ flag, int *ctr) {
+  ACE_WGT(2, true);
+  CHAIN_PRIO();
+  __shared__ double sSW[SUB][PLD];
+  __shared__ double sSt[SUB][SLD];
+  __shared__ PivotLds<4> PL;
+  auto mark = [&](int i) { (void)i; ACE_WGT_MARK(i); };
+  static_assert(NB / SUB == 4, "four sub-steps");
+  double *const Xb = SW + 2 * SUB * SUB, *const SW1 = SW + SUB * SUB;
+  const int g = (int)blockIdx.x, cc = (int)blockIdx.y;
+  const int nwg = (int)(gridDim.x * gridDim.y);
+  // each sub-step inlined with its s a constant (ping-pong buffers as
+  // panel_chain's launches): every copy keeps k_panel_split's registers,
+  // where one loop over a runtime s held 363 (no co-residency beside the
+  // bulk update's 128-register waves)
+  panel_split_step(W, ldp, k0, 0, SW, S0, S1, Xb, SW1, piv, flag, sSW, sSt, PL, g, cc, mark);
+  chain_barrier(ctr, nwg, flag);
+  panel_split_step(W, ldp, k0, 1, SW1, S1, S0, Xb, SW, piv, flag, sSW, sSt, PL, g, cc, mark);
+  chain_barrier(ctr, 2 * nwg, flag);
+  panel_split_step(W, ldp, k0, 2, SW, S0, S1, Xb, SW1, piv, flag, sSW, sSt, PL, g, cc, mark);
+  chain_barrier(ctr, 3 * nwg, flag);
+  panel_split_step(W, ldp, k0, 3, SW1, S1, S0, Xb, SW, piv, flag, sSW, sSt, PL, g, cc, mark);
+  __syncthreads();
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(ctr + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1) {
+    __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ctr + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ---------------------------------------------------------------- panel GEMM
@@ -2218,6 +2302,19 @@ static bool panel_split() {
   return v != 0;
 }
 
+// ACE_CHAIN_FUSE=1 (default): at small n (the bulk-reserve schedule) each
+// panel's four split sub-steps run as one k_panel_split4 launch
+// (bit-identical; C1 3.60 -> 3.52 ms, profiles/r06_chain_fuse_ab.txt); 0: four
+// k_panel_split launches
+static bool chain_fuse() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_CHAIN_FUSE");
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
 // pivot0: sub-block 0 was already swept (by k_gather<true>)
 // ACE_PGEMM_TILES=0 selects the 64-row k_panel_gemm (A/B switch; the tile
 // form k_panel_gemm_t is the default and bit-identical)
@@ -2236,13 +2333,20 @@ static bool pgemm_tiles() {
 #ifndef ACE_DIAG_SKIP
 #define ACE_DIAG_SKIP 0
 #endif
+// fuse_ctr (small n, ACE_CHAIN_FUSE): the four split sub-steps in one
+// k_panel_split4 launch, its grid barrier on *fuse_ctr (zeroed per sweep)
 static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, double *SW,
                         double *const S[2], double *piv, int *flag, int G, int r,
                         hipStream_t st, bool pivot0 = false, hipEvent_t before_gemm = nullptr,
-                        bool no_gemm = false) {
+                        bool no_gemm = false, int *fuse_ctr = nullptr) {
   const bool split = panel_split();
   double *const SWb[2] = {SW, SW + SUB * SUB};  // ping-pong by sub-step
-  for (int s = 0; s < ((ACE_DIAG_SKIP & 1) ? 0 : NB / SUB); ++s) {
+  if (split && fuse_ctr && !(ACE_DIAG_SKIP & 1)) {
+    if (!pivot0) launch_pivot(S[0], 0, SWb[0], piv, k0, flag, st);
+    hipLaunchKernelGGL(k_panel_split4, dim3(NB / SUB, NB / SUB), dim3(256), 0, st, W, ld, k0, SW,
+                       S[0], S[1], piv, flag, fuse_ctr);
+  }
+  for (int s = 0; s < ((ACE_DIAG_SKIP & 1) || (split && fuse_ctr) ? 0 : NB / SUB); ++s) {
     if (!split || (s == 0 && !pivot0))
       launch_pivot(S[s & 1], s, SWb[s & 1], piv, k0 + (int64_t)s * SUB, flag, st);
     if (split)
@@ -3111,9 +3215,12 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
                          b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, 1, 0, head ? r0 : 0,
                          head ? 1 << 30 : r0, head ? 1 << 30 : r1);
   };
+  // small n: each panel's four split sub-steps in one launch (k_panel_split4),
+  // its barrier counter after the bulk queues
+  int *const fctr = (b.bq && b.breserve > 0 && chain_fuse()) ? b.bq + (int64_t)ng * BQ_INTS : nullptr;
   auto chain = [&](int k, hipStream_t s_) {  // [pivot +] sub-steps of panel k (gathered)
     panel_chain(b.P[slot(k)], b.W[slot(k)], b.ld, (int64_t)k * NB, b.SW, b.S, b.piv, b.flag, 1, 0,
-                s_, fused_pivot && k > 0, nullptr, true);
+                s_, fused_pivot && k > 0, nullptr, true, fctr ? fctr + 2 * k : nullptr);
   };
   hipError_t e;
   if (b.bq && b.breserve > 0 &&

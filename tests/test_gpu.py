@@ -503,7 +503,10 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     leaves 1 (default below n = 8192) or 2 CUs per engine to the chains, or
     as the plain grid (ACE_BULK_RESERVE=0), and with the next group's Q launch
     run before (default below n = 8192) or beside (ACE_QFIRST=0) the bulk
-    launch and the rest of the cross."""
+    launch and the rest of the cross.  Round 6: each panel's four split
+    sub-steps in one launch with a grid barrier between them
+    (k_panel_split4, ACE_CHAIN_FUSE=1, default with the small-n bulk
+    queue) against four k_panel_split launches (0)."""
     import os
     import subprocess
     import sys
@@ -543,7 +546,10 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
                 "heads4_unreserved": {"ACE_BULK_RESERVE": "0"},
                 "heads4_reserve2": {"ACE_BULK_RESERVE": "2"},
                 "heads4_q_beside": {"ACE_QFIRST": "0"},
-                "heads4_q_beside_unreserved": {"ACE_QFIRST": "0", "ACE_BULK_RESERVE": "0"}}
+                "heads4_q_beside_unreserved": {"ACE_QFIRST": "0", "ACE_BULK_RESERVE": "0"},
+                "chain_unfused": {"ACE_CHAIN_FUSE": "0"},
+                "chain_fused_reserve2": {"ACE_CHAIN_FUSE": "1", "ACE_BULK_RESERVE": "2"},
+                "heads3_chain_fused": {"ACE_GROUP": "3", "ACE_HEADS": "1", "ACE_CHAIN_FUSE": "1"}}
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)
