@@ -156,6 +156,35 @@ def rocprof_bulk_avg(config="C2"):
     return None, None
 
 
+def rocprof_assembly_ms(config="C2"):
+    """Per-evaluation kernel time of the assembly from the newest committed
+    rocprofv3 summary: every k_asm_mm / k_asm_mm_q launch (the persistent
+    queue's main launch AND the filler that takes its last tiles on the tail
+    stream after group 0's lookahead), over the evaluations of that run (one
+    k_aug_init per evaluation).  The HIP-event interval `assembly_kernel`
+    brackets the main stream's launches only."""
+    import csv
+    import glob
+    if config != "C2":
+        return None, None
+    files = _newest_first_last(glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats_split.csv")))
+    if not files:
+        return None, None
+    try:
+        asm_ns, evals = 0.0, 0
+        for row in csv.DictReader(open(files[-1])):
+            name = row["Name"]
+            if "k_asm_mm<" in name or "k_asm_mm_q<" in name:
+                asm_ns += float(row["TotalDurationNs"])
+            elif "k_aug_init(" in name:
+                evals += int(row["Calls"])
+        if evals == 0 or asm_ns == 0.0:
+            return None, None
+        return asm_ns / evals / 1e6, os.path.relpath(files[-1], ROOT)
+    except (KeyError, ValueError, OSError):
+        return None, None
+
+
 def pair_hbm_gbs(asm_ms, grad_ms, config="C2"):
     """HBM GB/s of the fused assembly and gradient phases (SURVEY §8d asks for
     them beside their VALU/MFMA rates): PMC bytes per eval from the newest
@@ -515,6 +544,7 @@ def main():
         if traffic is None:  # a summary from before the multi-panel kernel
             traffic, traffic_src = pmc_traffic("k_update_pair_bulk", a.config)
         rp_ms, rp_src = rocprof_bulk_avg(a.config)
+        asm_rp_ms, asm_rp_src = rocprof_assembly_ms(a.config)
         naug = -(-n // 256) * 256 + 128
         nt = naug // 128
         # sweep steps per bulk launch, from the launch count (steps / groups)
@@ -582,7 +612,14 @@ def main():
                 "assembly_end_to_first_bulk": lead_ms / lead_n if lead_n else None,
                 "device_span": span_ms / span_n if span_n else None},
             "pair_kernels_tflops": {
+                # (HIP events around the main stream's assembly launches: the
+                # filler's share of the tiles runs after them on the tail
+                # stream, so this overstates the rate; assembly_rocprof below
+                # charges every assembly launch)
                 "assembly": asm_work / (asm_ms * 1e-3) / 1e12 if asm_ms else None,
+                "assembly_rocprof": (asm_work / a.steps / (asm_rp_ms * 1e-3) / 1e12) if asm_rp_ms else None,
+                "assembly_rocprof_ms_per_eval": asm_rp_ms,
+                "assembly_rocprof_source": asm_rp_src,
                 "gradient": grad_work / (grad_ms * 1e-3) / 1e12 if grad_ms else None},
             "pair_kernels_hbm_gbs": pair_hbm_gbs(asm_ms / a.steps, grad_ms / a.steps, a.config),
             "last_stats": [float(stats[0]), float(stats[1])],
