@@ -221,6 +221,11 @@ std::vector<Tile> cross_update_tiles(int64_t naug, int steps, std::vector<int64_
 // b % 8 (dispatch is round-robin).  Entries with I < 0 are padding.
 std::vector<Tile> xcd_update_order(const std::vector<Tile> &tl, int S,
                                    const std::function<double(const Tile &)> &cost = nullptr);
+// The tiles along a Hilbert curve cut into 8 equal-work pieces, one per XCD
+// (ACE_BULK_CURVE=1: the bulk orders of pair_bulk_orders)
+bool bulk_curve();
+std::vector<Tile> curve_update_order(const std::vector<Tile> &tl,
+                                     const std::function<double(const Tile &)> &cost = nullptr);
 // per group of two steps, the bulk order with each XCD's cheap tiles last
 // (ACE_TAIL_SORT=1): ngroups lists of *len entries
 bool tail_sort();

@@ -2506,6 +2506,7 @@ std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len, int G,
   const std::vector<Tile> base = own_tiles(nT, UT, G, r);
   const int S = std::max(1, update_order_block());
   std::vector<Tile> all;
+  std::vector<std::vector<Tile>> lists;
   *len = 0;
   for (int g = 0; g < ng; ++g) {
     const int z = std::min(Z, steps - Z * g);
@@ -2526,8 +2527,13 @@ std::vector<Tile> pair_bulk_orders(int64_t naug, int steps, int64_t *len, int G,
       const double rows = (I == nT - 1) ? 16.0 / UT : 1.0;
       return rows * (jm >= 0 ? z - 1 - jm : z);
     };
-    const std::vector<Tile> o = xcd_update_order(base, S, cost);
-    *len = (int64_t)o.size();
+    lists.push_back(bulk_curve() ? curve_update_order(base, cost) : xcd_update_order(base, S, cost));
+    *len = std::max<int64_t>(*len, (int64_t)lists.back().size());
+  }
+  // one length for every group (padding: whole rows of 8, so the XCD dealing
+  // of each list stands)
+  for (auto &o : lists) {
+    o.resize((size_t)*len, Tile{-1, -1});
     all.insert(all.end(), o.begin(), o.end());
   }
   return all;
@@ -2783,6 +2789,70 @@ std::vector<Tile> xcd_update_order(const std::vector<Tile> &tl, int S,
     q[x].insert(q[x].end(), kv.second.begin(), kv.second.end());
   }
   if (cost)  // each XCD's dearest tiles first: its launch tail is the cheap ones
+    for (auto &v : q)
+      std::stable_sort(v.begin(), v.end(),
+                       [&](const Tile &a, const Tile &b) { return cost(a) > cost(b); });
+  size_t len = 0;
+  for (auto &v : q) len = std::max(len, v.size());
+  std::vector<Tile> out(len * X, Tile{-1, -1});
+  for (int x = 0; x < X; ++x)
+    for (size_t i = 0; i < q[x].size(); ++i) out[i * X + x] = q[x][i];
+  return out;
+}
+
+// Index of (x, y) along the Hilbert curve of an n x n grid (n a power of 2)
+static int64_t hilbert_index(int64_t n, int64_t x, int64_t y) {
+  int64_t d = 0;
+  for (int64_t s = n / 2; s > 0; s /= 2) {
+    const int64_t rx = (x & s) ? 1 : 0, ry = (y & s) ? 1 : 0;
+    d += s * s * ((3 * rx) ^ ry);
+    if (ry == 0) {
+      if (rx == 1) {
+        x = n - 1 - x;
+        y = n - 1 - y;
+      }
+      std::swap(x, y);
+    }
+  }
+  return d;
+}
+
+bool bulk_curve() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("ACE_BULK_CURVE");
+    v = e ? (atoi(e) != 0) : 0;
+  }
+  return v != 0;
+}
+
+std::vector<Tile> curve_update_order(const std::vector<Tile> &tl,
+                                     const std::function<double(const Tile &)> &cost) {
+  // The tiles along a Hilbert curve over the tile grid, cut into 8 pieces of
+  // equal estimated work, one per XCD: an XCD's ~64 tiles in flight are
+  // neighbours on the curve, a compact patch whose row and column panel
+  // blocks its L2 shares (the S x S super-blocks of xcd_update_order are
+  // dealt round-robin, so an XCD's in-flight tiles span ~16 super-columns)
+  constexpr int X = 8;
+  int64_t n = 1, m = 0;
+  for (const Tile &t : tl) m = std::max<int64_t>(m, std::max(t.I, t.J) + 1);
+  while (n < m) n *= 2;
+  std::vector<std::pair<int64_t, size_t>> key(tl.size());
+  for (size_t i = 0; i < tl.size(); ++i) key[i] = {hilbert_index(n, tl[i].J, tl[i].I), i};
+  std::sort(key.begin(), key.end());
+  // work estimate: the cost (segments) plus a launch-slot overhead
+  auto wt = [&](const Tile &t) { return (cost ? cost(t) : 1.0) + 0.02; };
+  double total = 0.0;
+  for (const Tile &t : tl) total += wt(t);
+  std::vector<std::vector<Tile>> q(X);
+  double acc = 0.0;
+  for (const auto &kv : key) {
+    const Tile &t = tl[kv.second];
+    const int x = std::min(X - 1, (int)(acc / total * X));
+    q[x].push_back(t);
+    acc += wt(t);
+  }
+  if (cost)  // each XCD's dearest tiles first (stable: curve order within a class)
     for (auto &v : q)
       std::stable_sort(v.begin(), v.end(),
                        [&](const Tile &a, const Tile &b) { return cost(a) > cost(b); });

@@ -506,7 +506,8 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     launch and the rest of the cross.  Round 6: each panel's four split
     sub-steps in one launch with a grid barrier between them
     (k_panel_split4, ACE_CHAIN_FUSE=1, default with the small-n bulk
-    queue) against four k_panel_split launches (0)."""
+    queue) against four k_panel_split launches (0); the bulk tiles in
+    Hilbert-curve pieces per XCD (ACE_BULK_CURVE=1)."""
     import os
     import subprocess
     import sys
@@ -549,7 +550,9 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
                 "heads4_q_beside_unreserved": {"ACE_QFIRST": "0", "ACE_BULK_RESERVE": "0"},
                 "chain_unfused": {"ACE_CHAIN_FUSE": "0"},
                 "chain_fused_reserve2": {"ACE_CHAIN_FUSE": "1", "ACE_BULK_RESERVE": "2"},
-                "heads3_chain_fused": {"ACE_GROUP": "3", "ACE_HEADS": "1", "ACE_CHAIN_FUSE": "1"}}
+                "heads3_chain_fused": {"ACE_GROUP": "3", "ACE_HEADS": "1", "ACE_CHAIN_FUSE": "1"},
+                "bulk_curve": {"ACE_BULK_CURVE": "1"},
+                "bulk_curve_unreserved": {"ACE_BULK_CURVE": "1", "ACE_BULK_RESERVE": "0"}}
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)
