@@ -177,9 +177,7 @@ struct SweepBufs {
   int *bq = nullptr;
   int breserve = 0;
 };
-// [next, leavers, 2 x 32 CU claims, the merged cross's done count (ACE_HMERGE), pad]
-constexpr int BQ_INTS = 2 + 64 + 2;
-constexpr int BQ_XCNT = 2 + 64;
+constexpr int BQ_INTS = 2 + 64;
 int bulk_reserve(int64_t naug);
 bool q_first(int64_t naug);
 // ACE_XMERGE=1: the next group's lookahead cross tiles run at the head of the

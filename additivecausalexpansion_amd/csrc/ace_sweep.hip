@@ -1748,10 +1748,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_multi_r(double *__restri
                                                                 const Tile *__restrict__ tiles,
                                                                 int64_t ntiles,
                                                                 int *__restrict__ queue,
-                                                                int reserve, GatherOut go,
-                                                                const Tile *__restrict__ xt = nullptr,
-                                                                int64_t nx = 0,
-                                                                GatherOut xgo = GatherOut{nullptr, nullptr, nullptr, -1, 0}) {
+                                                                int reserve, GatherOut go) {
   ACE_WGT(5, gridDim.x < 4096 || blockIdx.x % 32 == 0);
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
@@ -1774,34 +1771,17 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_multi_r(double *__restri
     if (next) return;  // the whole workgroup (one CU)
     __syncthreads();
   }
-  // merged cross (ACE_HMERGE): the next group's rest-of-cross tiles lead the
-  // queue, with their gather; each one is published to the tail path's
-  // k_wait_count at the top of the workgroup's next turn -- every wave's
-  // stores drained, one barrier, released at agent scope, counted -- so that
-  // no barrier sits under a tile-dependent branch
-  bool pub = false;
   for (;;) {
-    if (pub) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) next = atomicAdd(queue, 1);
     __syncthreads();  // also: every wave is done with the previous tile's LDS
-    if (threadIdx.x == 0) {
-      if (pub) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_fetch_add(queue + BQ_XCNT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      next = atomicAdd(queue, 1);
-    }
-    __syncthreads();
     const int64_t idx = next;
     __syncthreads();
-    if (idx >= nx + ntiles) break;
-    const bool cross = idx < nx;
-    pub = cross;
-    const Tile tt = cross ? xt[idx] : tiles[idx - nx];
+    if (idx >= ntiles) break;
+    const Tile tt = tiles[idx];
     const int I = tt.I, J = tt.J;
     if (I < 0) continue;  // padding of the XCD order
-    if (!cross && kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT)))
-      continue;
-    update_multi_tile<SH, true>(I, J, sW, sP, A, ld, ps, npan, ldp, ka0, cross ? xgo : go, 1);
+    if (kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT))) continue;
+    update_multi_tile<SH, true>(I, J, sW, sP, A, ld, ps, npan, ldp, ka0, go, 1);
   }
 }
 
@@ -1817,19 +1797,6 @@ bool q_first(int64_t naug) {
   }
   if (v >= 0) return v != 0;
   return naug <= ACE_BULK_RESERVE_N + AUG;
-}
-
-// ACE_HMERGE=1 (small n, with the bulk queue): the next group's rest of the
-// cross runs at the head of the bulk queue instead of as its own launch on
-// side2, so that it keeps off the CUs the queue leaves to the chains; the
-// tail path waits for it with k_wait_count
-static int hmerge_on() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("ACE_HMERGE");
-    v = e ? std::max(0, atoi(e)) : 0;
-  }
-  return v;
 }
 
 int bulk_reserve(int64_t naug) {
@@ -2371,19 +2338,12 @@ static bool pgemm_tiles() {
 static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, double *SW,
                         double *const S[2], double *piv, int *flag, int G, int r,
                         hipStream_t st, bool pivot0 = false, hipEvent_t before_gemm = nullptr,
-                        bool no_gemm = false, int *fuse_ctr = nullptr, unsigned xlds = 0) {
+                        bool no_gemm = false, int *fuse_ctr = nullptr) {
   const bool split = panel_split();
   double *const SWb[2] = {SW, SW + SUB * SUB};  // ping-pong by sub-step
   if (split && fuse_ctr && !(ACE_DIAG_SKIP & 1)) {
     if (!pivot0) launch_pivot(S[0], 0, SWb[0], piv, k0, flag, st);
-    if (xlds) {
-      static unsigned set = 0;
-      if (set != xlds && hipFuncSetAttribute((const void *)k_panel_split4,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)xlds) == hipSuccess)
-        set = xlds;
-    }
-    hipLaunchKernelGGL(k_panel_split4, dim3(NB / SUB, NB / SUB), dim3(256), xlds, st, W, ld, k0, SW,
+    hipLaunchKernelGGL(k_panel_split4, dim3(NB / SUB, NB / SUB), dim3(256), 0, st, W, ld, k0, SW,
                        S[0], S[1], piv, flag, fuse_ctr);
   }
   for (int s = 0; s < ((ACE_DIAG_SKIP & 1) || (split && fuse_ctr) ? 0 : NB / SUB); ++s) {
@@ -3328,15 +3288,9 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   // small n: each panel's four split sub-steps in one launch (k_panel_split4),
   // its barrier counter after the bulk queues
   int *const fctr = (b.bq && b.breserve > 0 && chain_fuse()) ? b.bq + (int64_t)ng * BQ_INTS : nullptr;
-  // (ACE_CHAIN_XLDS: extra LDS bytes for a group's first chain, G >= 1)
-  static const unsigned xlds = [] {
-    const char *e = getenv("ACE_CHAIN_XLDS");
-    return e ? (unsigned)std::max(0, atoi(e)) : 0u;
-  }();
-  auto chain = [&](int k, hipStream_t s_, unsigned xl) {  // [pivot +] sub-steps of panel k (gathered)
+  auto chain = [&](int k, hipStream_t s_) {  // [pivot +] sub-steps of panel k (gathered)
     panel_chain(b.P[slot(k)], b.W[slot(k)], b.ld, (int64_t)k * NB, b.SW, b.S, b.piv, b.flag, 1, 0,
-                s_, fused_pivot && k > 0, nullptr, true, fctr ? fctr + 2 * k : nullptr,
-                fctr ? xl : 0u);
+                s_, fused_pivot && k > 0, nullptr, true, fctr ? fctr + 2 * k : nullptr);
   };
   hipError_t e;
   if (b.bq && b.breserve > 0 &&
@@ -3361,11 +3315,6 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   // beside both took 163 us instead of ~40 (C1 trace, profiles/r05_v4_*).
   const bool qfirst = q_first(naug);
   auto Eq = [&](int G) { return sy->ev[2 * steps + 1 + 2 * G]; };  // group G's Q done
-  const bool hm = hmerge_on() && qfirst;
-  // bulk launch g is the persistent queue carrying group g+1's rest of the cross
-  auto merged = [&](int g) {
-    return hm && b.bq && b.breserve > 0 && (b.gorder || b.order) && zsize(g) > 2 && g + 1 < ng;
-  };
   // group G's first head launch (k_gather / Q); the rest by produce(G)
   auto produce_q = [&](int G) -> hipError_t {
     const int kb = Z * G;
@@ -3391,17 +3340,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
         if (q != hipSuccess) return q;
       }
       list(G, 1, tl, nt);
-      if (merged(G - 1)) {  // the rest of the cross leads bulk launch G-1's queue
-        if (hmerge_on() == 2) {  // (diagnostic: the whole bulk launch)
-          const hipError_t q = hipStreamWaitEvent(side2, Eb(G - 1), 0);
-          if (q != hipSuccess) return q;
-        } else if (nt > 0) {
-          hipLaunchKernelGGL(k_wait_count, dim3(1), dim3(64), 0, side2,
-                             b.bq + (int64_t)(G - 1) * BQ_INTS + BQ_XCNT, (int)nt, b.flag);
-        }
-      } else {
-        upd(zsize(G - 1), Z * (G - 1), -1, -1, tl, nt, gout(kb), side2);  // the rest of the cross
-      }
+      upd(zsize(G - 1), Z * (G - 1), -1, -1, tl, nt, gout(kb), side2);  // the rest of the cross
     }
     hipError_t r;
     const int hend = (kb + zb) * KT;  // head rows end (row tiles)
@@ -3411,7 +3350,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
     const bool split = G == 0 && sy->tail_split;
     auto head = [&](int j) -> hipError_t {
       const int k = kb + j;
-      chain(k, side, (G > 0 && j == 0 && qfirst) ? xlds : 0u);
+      chain(k, side);
       hipError_t q;
       if ((q = hipEventRecord(Esp(k), side)) != hipSuccess) return q;
       pgemm(k, (k + 1) * KT, hend, true, side);
@@ -3496,28 +3435,9 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
         ps.C[j] = j < zsize(g) ? b.P[slot(kg + j)] : nullptr;
       }
       // one workgroup per launch slot: two per CU (k_update_multi_r's occupancy)
-      const Tile *xt = nullptr;
-      int64_t nx = 0;
-      if (merged(g)) list(g + 1, 1, xt, nx);
-      // ACE_BULK_GRID=N (experiment): N workgroups and no CU claims, each
-      // with ACE_BULK_XLDS extra LDS bytes (alone on its CU when large)
-      static const int bgrid = [] {
-        const char *e = getenv("ACE_BULK_GRID");
-        return e ? std::max(0, atoi(e)) : 0;
-      }();
-      static const unsigned bxlds = [] {
-        const char *e = getenv("ACE_BULK_XLDS");
-        const unsigned v = e ? (unsigned)std::max(0, atoi(e)) : 0u;
-        if (v)
-          (void)hipFuncSetAttribute((const void *)k_update_multi_r<false>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)v);
-        return v;
-      }();
-      hipLaunchKernelGGL(k_update_multi_r<false>, dim3(bgrid > 0 ? bgrid : 2 * device_cu_count()),
-                         dim3(UTHREADS), bxlds, st, b.A, b.ld,
+      hipLaunchKernelGGL(k_update_multi_r<false>, dim3(2 * device_cu_count()), dim3(UTHREADS), 0, st, b.A, b.ld,
                          ps, zsize(g), b.ld, (int64_t)kg * NB, kx0, kx1, ord, grid,
-                         b.bq + (int64_t)g * BQ_INTS, bgrid > 0 ? 0 : b.breserve, no_gather(), xt, nx,
-                         merged(g) ? gout(kb) : no_gather());
+                         b.bq + (int64_t)g * BQ_INTS, b.breserve, no_gather());
     } else {
       upd(zsize(g), kg, kx0, kx1, ord, grid, no_gather(), st);
     }
@@ -3528,9 +3448,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
             update_gemm_tiles_group(naug, (int64_t)kg * NB, zsize(g), kx0, kx1) * 2.0 * UT * UT * NB;
       used += 2;
     }
-    if (qdirect && (g + 2 < ng || (merged(g) && hmerge_on() == 2)) &&
-        (e = hipEventRecord(Eb(g), st)) != hipSuccess)
-      return e;  // Q(g+2)
+    if (qdirect && g + 2 < ng && (e = hipEventRecord(Eb(g), st)) != hipSuccess) return e;  // Q(g+2)
     if (more && (e = produce(g + 1)) != hipSuccess) return e;
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
