@@ -164,14 +164,6 @@ struct SweepBufs {
   const Tile *htiles = nullptr;  // group_head_tiles lists (run_sweep_heads), offsets hoff
   const int64_t *hoff = nullptr;
   int64_t glen = 0;
-  // merged schedule (merge_cross()): group g's bulk launch runs the list
-  // morder[moff[g], moff[g+1]) = [group g+1's cross tiles (mfront[g]
-  // entries, mtarget[g] of them real) | the bulk order]; the front tiles
-  // count into mcnt[g] (device; zeroed per sweep); null: not merged
-  const Tile *morder = nullptr;
-  const int64_t *moff = nullptr;
-  const int *mfront = nullptr, *mtarget = nullptr;
-  int *mcnt = nullptr;
   // small n: per group a bulk work queue of BQ_INTS ints (k_update_multi_r,
   // zeroed per sweep) and the CUs per shader engine it leaves to the chains
   int *bq = nullptr;
@@ -180,14 +172,6 @@ struct SweepBufs {
 constexpr int BQ_INTS = 2 + 64;
 int bulk_reserve(int64_t naug);
 bool q_first(int64_t naug);
-// ACE_XMERGE=1: the next group's lookahead cross tiles run at the head of the
-// bulk launch instead of as side-stream launches (merged_bulk_orders)
-bool merge_cross();
-// per group g: [group g+1's pair cross tiles | group g's bulk order (gorder)]
-// (g + 1 < ngroups; the last group has no front), offsets off (ngroups + 1),
-// front entries and real front tiles per group
-std::vector<Tile> merged_bulk_orders(int64_t naug, int steps, std::vector<int64_t> &off,
-                                     std::vector<int> &front, std::vector<int> &target);
 // Two sweep steps per bulk update launch (k_update_pair, K = 2 NB per tile;
 // default): ACE_PAIR=0 selects one step per launch (A/B switch).
 bool pair_steps();
@@ -200,7 +184,6 @@ bool pair_steps();
 // blocks and not in the first.
 std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t> &off,
                                    int Z = 2);
-double update_gemm_tiles_pair(int64_t naug, int64_t ka0, int kx0, int kx1);
 // Head / tail lists of the group schedule's lookahead (run_sweep_heads):
 // 2Z lists per group at off[G 2Z + m] (see ace_sweep.hip).  heads_on():
 // ACE_HEADS switch.

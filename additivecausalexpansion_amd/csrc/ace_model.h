@@ -8,7 +8,7 @@
 
 // Buffers of one Gauss-Jordan sweep and its lookahead events.
 struct SweepWork {
-  DBuf A, Ps[8], Ws[8], SW, S0, S1, piv, flag, order, xtiles, ptiles, gorder, morder, mcnt, htiles;
+  DBuf A, Ps[8], Ws[8], SW, S0, S1, piv, flag, order, xtiles, ptiles, gorder, htiles;
   int Z = 2;  // steps per bulk launch (sweep_group()), panel slots k % 2Z
   DBuf gtiles;                          // handle path: the gradient's tile list (build_grad_tiles)
   DBuf aq;                              // persistent assembly: tile counter, exits, CU claims
@@ -17,8 +17,7 @@ struct SweepWork {
   DBuf gpart, gwork, gsum;              // handle path: gradient partial-sum scratch
   DBuf norms;                           // handle path: slice norms (TabView::norms)
   int64_t ngtiles = 0, ngdiag = -2;     // -2: not built yet
-  std::vector<int64_t> xoff, poff, moff, hoff;
-  std::vector<int> mfront, mtarget;
+  std::vector<int64_t> xoff, poff, hoff;
   int64_t glen = 0;
   std::vector<hipEvent_t> ev;
   int64_t n = 0, npad = 0, naug = 0, norder = 0;
@@ -73,13 +72,6 @@ struct SweepWork {
         if (!h.empty())
           upload_bytes(ctx, htiles.p, h.data(), h.size() * sizeof(Tile), "upload head tiles");
       }
-      moff.clear();
-      if (glen > 0 && merge_cross() && Z == 2) {
-        const std::vector<Tile> m = merged_bulk_orders(naug, (int)(npad / NB), moff, mfront, mtarget);
-        alloc(ctx, morder, m.size() * sizeof(Tile), "alloc merged orders");
-        upload_bytes(ctx, morder.p, m.data(), m.size() * sizeof(Tile), "upload merged orders");
-        alloc(ctx, mcnt, (size_t)round_up((int64_t)mfront.size(), 4) * sizeof(int), "alloc counters");
-      }
     }
     breserve = (Z > 2 && heads_on()) ? bulk_reserve(naug) : 0;
     if (breserve > 0) {
@@ -126,13 +118,6 @@ struct SweepWork {
     if (!hoff.empty()) {
       b.htiles = reinterpret_cast<const Tile *>(htiles.p);
       b.hoff = hoff.data();
-    }
-    if (!moff.empty()) {
-      b.morder = reinterpret_cast<const Tile *>(morder.p);
-      b.moff = moff.data();
-      b.mfront = mfront.data();
-      b.mtarget = mtarget.data();
-      b.mcnt = mcnt.i();
     }
     if (breserve > 0 && bq.p) {
       b.bq = bq.i();

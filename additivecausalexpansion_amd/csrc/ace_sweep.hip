@@ -356,15 +356,10 @@ static void launch_pivot(const double *S, int s, double *SW, double *piv, int64_
 // ---------------------------------------------------------------- gather
 // P = -A[:, k] for every row; W = A[:, k] only on the pivot rows (k_panel
 // sweeps them; k_panel_gemm forms every other row of W from P).
-// PIV: the workgroup of the pivot block's first 64 x 64 diagonal block
-// (sub-block 0) then runs k_pivot's sub-sweep of it (into SW0, piv, flag):
-// one chain launch less per panel.
-template <bool PIV>
 __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, int64_t ld,
                                                 int64_t k0, double *__restrict__ P,
                                                 double *__restrict__ W, int64_t ldp,
-                                                double *__restrict__ S0, double *__restrict__ SW0,
-                                                double *__restrict__ pivs, int *__restrict__ flag) {
+                                                double *__restrict__ S0) {
   __shared__ double tile[64][65];
   const int64_t i0 = (int64_t)blockIdx.x * 64;
   const int j0 = blockIdx.y * 64;
@@ -393,14 +388,12 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
       if (piv) W[(i0 + a) + (int64_t)(j0 + b) * ldp] = v;
     }
   } else {
-    const bool diag0 = PIV && i0 == k0 && j0 == 0;  // D_0 itself
     for (int e = tid; e < 4096; e += 256) {
       const int a = e & 63, b = e >> 6;
       const int64_t i = i0 + a, c = col0 + b;
       const double v = (i >= c) ? A[i + c * ld] : A[c + i * ld];
       P[i + (int64_t)(j0 + b) * ldp] = -v;
       if (piv) W[i + (int64_t)(j0 + b) * ldp] = v;
-      if (diag0) tile[a][b] = v;
     }
   }
   if (i0 == k0) {  // pivot rows of sub-block 0: snapshot for k_pivot / k_panel
@@ -408,21 +401,6 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ A, in
       const int a = e & 63, b = e >> 6;
       S0[a + (int64_t)(j0 + b) * SUB] = W[(i0 + a) + (int64_t)(j0 + b) * ldp];
     }
-  }
-  if (PIV && i0 == k0 && j0 == 0) {
-    __shared__ PivotLds<4> L;
-    __syncthreads();
-    const int lane = tid & 63, w = tid >> 6;
-    double v[SUB / 4];
-#pragma unroll
-    for (int q = 0; q < SUB / 4; ++q) v[q] = tile[lane][16 * w + q];
-#if ACE_PIVOT_BLK
-    __syncthreads();  // tile becomes the sweep's matrix
-    pivot_sweep_blk<65>(v, tile, L.pv, tid);
-#else
-    pivot_sweep<4>(v, L, tid);
-#endif
-    pivot_store<4>(v, L.pv, tid, SW0, pivs, k0, flag);
   }
 }
 
@@ -873,7 +851,6 @@ constexpr int UTHREADS = 512;
 // round-4 change, -0.3 ms per C2 evaluation, bit-identical).
 constexpr int SM128 = 2, SH128 = 64;
 constexpr int SM64 = 2, SH64 = 32;
-constexpr int XSPLIT_HEAD = 8;  // entries of the split cross's head launch (3 tiles + padding)
 static_assert(BK == 16, "staging maps 512 threads x 4 doubles onto a 128 x 16 chunk");
 
 // A tiles are read and written once per sweep step, by whichever XCD runs
@@ -1428,18 +1405,13 @@ __device__ __forceinline__ void update_pair_tile(
   }
 }
 
-// nfront < 0: every entry of the list is a plain tile (skip rule [kx0, kx1),
-// gather go on all of them).  nfront >= 0 (ACE_XMERGE, the merged bulk
-// launch): entries [0, nfront) are the next group's lookahead cross tiles,
-// run first, never skipped, gathered into go; each one, once its stores are
-// done, releases them at agent scope and adds 1 to *cnt, which the side
-// stream's k_wait_count polls before that group's panel chain.
-// The rest of the list is the bulk order, with the skip rule and no gather.
+// Two sweep steps per launch on a tile list (skip rule [kx0, kx1), gather
+// go on every tile).
 __global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
     double *__restrict__ A, int64_t ld, const double *__restrict__ Ra,
     const double *__restrict__ Ca, const double *__restrict__ Rb, const double *__restrict__ Cb,
     int64_t ldp, int64_t ka0, int kx0, int kx1, const Tile *__restrict__ tiles, GatherOut go,
-    int nfront, int *cnt, int G, int wcol) {
+    int G, int wcol) {
   __shared__ __attribute__((aligned(16))) double sW[2][BK][LDL];
   __shared__ __attribute__((aligned(16))) double sP[2][BK][LDL];
   constexpr int KT = NB / UT;
@@ -1448,7 +1420,7 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
     const Tile tt = tiles[blockIdx.x];
     I = tt.I;
     J = tt.J;
-    if (I < 0) return;  // padding of the XCD order (not counted by the host's target)
+    if (I < 0) return;  // padding of the XCD order
   } else {
     const int t = blockIdx.x;
     int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
@@ -1457,23 +1429,8 @@ __global__ __launch_bounds__(UTHREADS, 2) void k_update_pair(
     I = i;
     J = t - i * (i + 1) / 2;
   }
-  const bool front = nfront >= 0 && (int)blockIdx.x < nfront;
-  if (!front && kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT)))
-    return;
-  GatherOut g = go;
-  if (nfront >= 0 && !front) g.k0 = -1;
-  update_pair_tile(I, J, sW, sP, A, ld, Ra, Ca, Rb, Cb, ldp, ka0, g, G, wcol != 0);
-  if (front && cnt) {
-    // publish (cdna_hip_programming.md §6 Guideline 16, counter form): every
-    // wave drains its stores, then one lane releases at agent scope and adds
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  if (kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT))) return;
+  update_pair_tile(I, J, sW, sP, A, ld, Ra, Ca, Rb, Cb, ldp, ka0, go, G, wcol != 0);
 }
 
 // Z sweep steps per launch (sweep_group() = 3 or 4; k_update_pair is Z = 2):
@@ -1809,24 +1766,6 @@ int bulk_reserve(int64_t naug) {
   return naug <= ACE_BULK_RESERVE_N + AUG ? 1 : 0;
 }
 
-// Side stream, merged schedule: wait until *cnt >= target (the merged bulk
-// launch's front tiles are stored and released), then acquire.  One lane
-// polls relaxed with s_sleep; bounded: after ~0.5 s it gives up and sets
-// *flag = 2 (read like a non-positive pivot: the evaluation reports NaN
-// instead of hanging).
-__global__ __launch_bounds__(64) void k_wait_count(int *cnt, int target, int *flag) {
-  if (threadIdx.x == 0) {
-    const uint64_t t0 = wall_clock64();
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(4);
-      if (wall_clock64() - t0 > 50000000ull) {  // 100 MHz counter: 0.5 s
-        __hip_atomic_store(flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-}
 
 // Lookahead update: only the tiles with I or J in block kx (the next panel).
 // About 2 n/128 tiles -- one workgroup per CU at 128 x 128 -- so it uses
@@ -2315,7 +2254,6 @@ static bool chain_fuse() {
   return v != 0;
 }
 
-// pivot0: sub-block 0 was already swept (by k_gather<true>)
 // ACE_PGEMM_TILES=0 selects the 64-row k_panel_gemm (A/B switch; the tile
 // form k_panel_gemm_t is the default and bit-identical)
 static bool pgemm_tiles() {
@@ -2333,12 +2271,13 @@ static bool pgemm_tiles() {
 #ifndef ACE_DIAG_SKIP
 #define ACE_DIAG_SKIP 0
 #endif
-// fuse_ctr (small n, ACE_CHAIN_FUSE): the four split sub-steps in one
-// k_panel_split4 launch, its grid barrier on *fuse_ctr (zeroed per sweep)
+// pivot0: sub-block 0 was already swept (by the k_update_q launch that
+// gathered the panel); fuse_ctr (small n, ACE_CHAIN_FUSE): the four split
+// sub-steps in one k_panel_split4 launch, its grid barrier on *fuse_ctr
 static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, double *SW,
                         double *const S[2], double *piv, int *flag, int G, int r,
-                        hipStream_t st, bool pivot0 = false, hipEvent_t before_gemm = nullptr,
-                        bool no_gemm = false, int *fuse_ctr = nullptr) {
+                        hipStream_t st, bool pivot0 = false, bool no_gemm = false,
+                        int *fuse_ctr = nullptr) {
   const bool split = panel_split();
   double *const SWb[2] = {SW, SW + SUB * SUB};  // ping-pong by sub-step
   if (split && fuse_ctr && !(ACE_DIAG_SKIP & 1)) {
@@ -2358,29 +2297,12 @@ static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, dou
                          S[s & 1], S[(s + 1) & 1], k0);
   }
   if ((ACE_DIAG_SKIP & 2) || no_gemm) return;
-  // (split cross: the panel rows outside the pivot block come from a launch
-  // on the second side stream)
-  if (before_gemm) (void)hipStreamWaitEvent(st, before_gemm, 0);
   if (pgemm_tiles())
     hipLaunchKernelGGL(k_panel_gemm_t, dim3((unsigned)(ld / UT), NB / UT), dim3(UTHREADS), 0, st,
                        W, Pn, ld, k0, G, r, 0, 1 << 30, 1 << 30);
   else
     hipLaunchKernelGGL(k_panel_gemm, dim3((unsigned)(ld / SUB)), dim3(512), 0, st, W, Pn, ld, k0,
                        G, r);
-}
-
-// ACE_GATHER_PIV=1: sub-block 0's sweep inside k_gather's D_0 workgroup
-// instead of its own k_pivot launch (A/B switch, bit-identical).  Off: the
-// chain is no longer the critical path, and the fused kernel's 98 VGPRs in
-// all 1040 gather workgroups cost the bulk update more than the saved launch
-// (79.76 / 79.65 vs 79.53 / 79.51 ms per C2 evaluation, profiles/r02_chain_ab.txt).
-static bool gather_pivot() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("ACE_GATHER_PIV");
-    v = e ? (atoi(e) != 0) : 0;
-  }
-  return v != 0;
 }
 
 // ACE_XGATHER: pair steps fuse each panel's gather into the lookahead cross
@@ -2396,21 +2318,14 @@ static bool xgather() {
 
 // gathered: P, W and S[0] of this panel were written by the cross launch
 static hipError_t panel_sweep(const SweepBufs &b, int buf, int64_t k0, hipStream_t st,
-                              bool gathered = false, hipEvent_t before_gemm = nullptr) {
+                              bool gathered = false) {
   const int64_t naug = b.ld;
-  // with the split panel, k_gather's D_0 workgroup sweeps sub-block 0 too
-  const bool gp = !gathered && panel_split() && gather_pivot();
-  if (gathered)
-    ;
-  else if (gp)
-    hipLaunchKernelGGL(k_gather<true>, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st, b.A,
-                       b.ld, k0, b.P[buf], b.W[buf], b.ld, b.S[0], b.SW, b.piv, b.flag);
-  else
-    hipLaunchKernelGGL(k_gather<false>, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st,
-                       b.A, b.ld, k0, b.P[buf], b.W[buf], b.ld, b.S[0], nullptr, nullptr, nullptr);
+  if (!gathered)
+    hipLaunchKernelGGL(k_gather, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, st, b.A, b.ld,
+                       k0, b.P[buf], b.W[buf], b.ld, b.S[0]);
   // sweep the NB x NB pivot block in place, then every other panel row:
   // W_i = Pn_i W_kk
-  panel_chain(b.P[buf], b.W[buf], b.ld, k0, b.SW, b.S, b.piv, b.flag, 1, 0, st, gp, before_gemm);
+  panel_chain(b.P[buf], b.W[buf], b.ld, k0, b.SW, b.S, b.piv, b.flag, 1, 0, st);
   return hipGetLastError();
 }
 
@@ -2560,41 +2475,6 @@ int sweep_group_n(int64_t naug) {
   return naug <= ACE_BULK_RESERVE_N + AUG ? 3 : 4;
 }
 
-bool merge_cross() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("ACE_XMERGE");
-    v = e ? (atoi(e) != 0) : 0;
-  }
-  return v != 0;
-}
-
-std::vector<Tile> merged_bulk_orders(int64_t naug, int steps, std::vector<int64_t> &off,
-                                     std::vector<int> &front, std::vector<int> &target) {
-  const int ng = (steps + 1) / 2;
-  std::vector<int64_t> poff;
-  const std::vector<Tile> cross = pair_cross_tiles(naug, steps, poff);
-  int64_t glen = 0;
-  const std::vector<Tile> bulk = pair_bulk_orders(naug, steps, &glen);
-  std::vector<Tile> all;
-  off.assign(1, 0);
-  front.assign(ng, 0);
-  target.assign(ng, 0);
-  for (int g = 0; g < ng; ++g) {
-    if (g + 1 < ng) {  // group g+1's two cross lists (each XCD-dealt, padded to 8)
-      const int64_t a = poff[2 * (g + 1)], z = poff[2 * (g + 1) + 2];
-      for (int64_t i = a; i < z; ++i) {
-        all.push_back(cross[i]);
-        if (cross[i].I >= 0) ++target[g];
-      }
-      front[g] = (int)(z - a);
-    }
-    all.insert(all.end(), bulk.begin() + g * glen, bulk.begin() + (g + 1) * glen);
-    off.push_back((int64_t)all.size());
-  }
-  return all;
-}
-
 bool pair_steps() {
   static int v = -1;
   if (v < 0) {
@@ -2616,24 +2496,11 @@ static bool side2_on() {
   return v != 0;
 }
 
-// ACE_XSPLIT=1: the pair cross of block 2g+2 runs as two launches -- the
-// pivot block's 3 tiles on the panel stream (its chain starts right after
-// them), the rest on the second side stream, which the panel GEMM waits for
-bool xsplit_cross() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("ACE_XSPLIT");
-    v = e ? (atoi(e) != 0) : 0;
-  }
-  return v != 0;
-}
-
 std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t> &off, int Z) {
   const int64_t nT = naug / UT;
   constexpr int KT = NB / UT;
   const int ng = (steps + Z - 1) / Z;
   const int S = update_order_block();
-  const bool xs = Z == 2 && xsplit_cross();
   std::vector<Tile> all;
   off.assign(3, 0);  // group 0 has no cross lists
   auto in_blk = [&](int64_t t, int blk) { return t >= (int64_t)blk * KT && t < (int64_t)(blk + 1) * KT; };
@@ -2652,21 +2519,8 @@ std::vector<Tile> pair_cross_tiles(int64_t naug, int steps, std::vector<int64_t>
             break;
           }
       }
-    if (xs) {
-      // the pivot block's own tiles (I and J in block b0) lead block b0's
-      // list, padded to XSPLIT_HEAD entries: the split schedule launches
-      // them alone so the pivot chain can start before the rest is done
-      std::vector<Tile> head, rest;
-      for (const Tile &t : ta) (in_blk(t.I, b0) && in_blk(t.J, b0) ? head : rest).push_back(t);
-      head.resize(XSPLIT_HEAD, Tile{-1, -1});
-      const std::vector<Tile> o = S > 0 ? xcd_update_order(rest, S) : rest;
-      head.insert(head.end(), o.begin(), o.end());
-      ta.swap(head);
-    }
-    bool first = true;
     for (auto *t : {&ta, &tb}) {
-      const std::vector<Tile> o = (S > 0 && !(first && xs)) ? xcd_update_order(*t, S) : *t;
-      first = false;
+      const std::vector<Tile> o = S > 0 ? xcd_update_order(*t, S) : *t;
       all.insert(all.end(), o.begin(), o.end());
       off.push_back((int64_t)all.size());
     }
@@ -2741,25 +2595,6 @@ double update_gemm_tiles_group(int64_t naug, int64_t ka0, int npan, int kx0, int
       const int jm = std::max(bi, bj);
       if (jm == npan - 1) continue;
       cnt += ((I == nT - 1) ? 16.0 / UT : 1.0) * (jm >= 0 ? npan - 1 - jm : npan);
-    }
-  return cnt;
-}
-
-// GEMM tiles of one k_update_pair launch over every lower tile, in units of
-// one full tile x NB (a tile of the AUG row block computes 16 of 128 rows).
-double update_gemm_tiles_pair(int64_t naug, int64_t ka0, int kx0, int kx1) {
-  const int64_t nT = naug / UT;
-  constexpr int KT = NB / UT;
-  const int64_t ta0 = ka0 / UT, tb0 = ta0 + KT;
-  double cnt = 0.0;
-  for (int64_t I = 0; I < nT; ++I)
-    for (int64_t J = 0; J <= I; ++J) {
-      if (kx0 >= 0 && ((I >= kx0 * KT && I < kx1 * KT) || (J >= kx0 * KT && J < kx1 * KT)))
-        continue;
-      const bool Ia = I >= ta0 && I < tb0, Ja = J >= ta0 && J < tb0;
-      const bool Ib = I >= tb0 && I < tb0 + KT, Jb = J >= tb0 && J < tb0 + KT;
-      if (Ib || Jb) continue;
-      cnt += ((I == nT - 1) ? 16.0 / UT : 1.0) * ((Ia || Ja) ? 1.0 : 2.0);
     }
   return cnt;
 }
@@ -2864,169 +2699,6 @@ std::vector<Tile> curve_update_order(const std::vector<Tile> &tl,
   return out;
 }
 
-// Step k: the main stream runs only the bulk update of step k (every tile
-// outside the cross of block k+1).  The high-priority side stream, once the
-// bulk update of step k-1 is done, updates the cross of block k+1 with panel
-// k and then gathers and sweeps panel k+1 -- all of it under the main
-// stream's update k.  P/W are double-buffered by step parity.
-// Two sweep steps per bulk launch.  Group g = steps 2g, 2g + 1 (the last
-// group may be one step); panels in slots k & 3.
-//   side:  wait(bulk g-1 done) -> pair cross of group g+1's blocks with
-//          group g's panels (k_update_pair on its tile list) -> panel 2g+2
-//          -> cross of block 2g+3 with panel 2g+2 (k_update on 128-tiles)
-//          -> panel 2g+3 -> ready(g+1)
-//   main:  wait(ready g) -> k_update_pair (every tile outside group g+1's
-//          cross), or k_update for a last single step.
-// Every element sees the single-step schedule's MFMA chains in the same
-// order: bit-identical to it (tests/test_gpu.py).
-static hipError_t run_sweep_pairs(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
-                                  const SweepTiming *tm) {
-  const int64_t naug = b.ld;
-  const unsigned nT = (unsigned)(naug / UT);
-  const int steps = (int)(b.npad / NB);
-  const int ng = (steps + 1) / 2;
-  const bool two = sy && sy->side && sy->nev >= 2 * steps + 1;
-  hipStream_t side = two ? sy->side : st;
-  auto zsize = [&](int g) { return std::min(2, steps - 2 * g); };
-  auto slot = [](int k) { return k & 3; };
-  hipError_t e;
-  // a second side stream runs group g+1's second-block cross concurrently
-  // with the first panel's chain (events 2 steps + 1 ..: E1 / E2 per group)
-  const bool two2 = two && side2_on() && sy->side2 && sy->nev >= 4 * steps + 4;
-  hipStream_t side2 = two2 ? sy->side2 : side;
-  auto E1 = [&](int g) { return sy->ev[2 * steps + 1 + 2 * g]; };
-  auto E2 = [&](int g) { return sy->ev[2 * steps + 2 + 2 * g]; };
-  // group g's panels, on `side`; wait2 (g >= 1): the second block's cross,
-  // launched on side2, must be done before the single cross below
-  const bool xg = xgather();
-  auto gout = [&](int k) {
-    return xg ? GatherOut{b.P[slot(k)], b.W[slot(k)], b.S[0], (int64_t)k * NB, b.ld} : no_gather();
-  };
-  // split cross (xsplit_cross): E3(g) = the rest of block 2g's cross done
-  const bool xs = two2 && xsplit_cross() && sy->nev >= 5 * steps + 5;
-  auto E3 = [&](int g) { return sy->ev[4 * steps + 4 + g]; };
-  auto produce = [&](int g, bool wait2) -> hipError_t {
-    const int k = 2 * g;
-    hipError_t r = panel_sweep(b, slot(k), (int64_t)k * NB, side, xg && g > 0,
-                               xs && g > 0 ? E3(g) : nullptr);
-    // (g = 0: the caller may have signalled "inputs ready" after assembling
-    // only the first two panels' columns (model_pipeline) -- every tile the
-    // cross of block 1 reads or writes, disjoint from the rest of the
-    // assembly, which runs on under this group's chains)
-    if (r != hipSuccess || zsize(g) < 2) return r;
-    if (wait2 && two2 && (r = hipStreamWaitEvent(side, E2(g), 0)) != hipSuccess) return r;
-    const int64_t x0 = b.xoff[k], nx = (ACE_DIAG_SKIP & 4) ? 0 : b.xoff[k + 1] - x0;  // cross of block k+1, panel k
-    if (nx > 0) hipLaunchKernelGGL(k_update, dim3((unsigned)nx), dim3(UTHREADS), 0, side, b.A, b.ld,
-                       b.W[slot(k)], b.P[slot(k)], b.W[slot(k)], b.ld, (int64_t)k * NB, -1,
-                       b.xtiles + x0, 1, gout(k + 1));
-    return panel_sweep(b, slot(k + 1), (int64_t)(k + 1) * NB, side, xg);
-  };
-  int used = 0;
-  // merged schedule (ACE_XMERGE): group g+1's cross tiles lead bulk launch g
-  // and count into mcnt[g]; every group's counter starts at 0
-  const bool merged = two && b.morder && b.mcnt;
-  if (merged) {
-    e = hipMemsetAsync(b.mcnt, 0, (size_t)((ng + 3) / 4 * 4) * sizeof(int), st);
-    if (e != hipSuccess) return e;
-  }
-  if (two) {
-    if (!sy->ready_recorded) {
-      e = hipEventRecord(sy->ev[2 * steps], st);  // inputs ready
-      if (e != hipSuccess) return e;
-    }
-    e = hipStreamWaitEvent(side, sy->ev[2 * steps], 0);
-    if (e != hipSuccess) return e;
-  }
-  e = produce(0, false);
-  if (e != hipSuccess) return e;
-  if (two && (e = hipEventRecord(sy->ev[0], side)) != hipSuccess) return e;
-  for (int g = 0; g < ng; ++g) {
-    const int k = 2 * g;
-    const int64_t ka0 = (int64_t)k * NB;
-    const bool more = g + 1 < ng;
-    if (two && (e = hipStreamWaitEvent(st, sy->ev[2 * g], 0)) != hipSuccess) return e;
-    if (more) {
-      if (two) {
-        if ((e = hipEventRecord(sy->ev[2 * g + 1], st)) != hipSuccess) return e;  // bulk g-1 done
-        if ((e = hipStreamWaitEvent(side, sy->ev[2 * g + 1], 0)) != hipSuccess) return e;
-      }
-      if (merged) {
-        // the cross tiles lead bulk launch g: the chain of panel 2g+2 starts
-        // once they are stored (both blocks' -- the single cross of block
-        // 2g+3 below reads the second block's)
-        hipLaunchKernelGGL(k_wait_count, dim3(1), dim3(64), 0, side, b.mcnt + g, b.mtarget[g],
-                           b.flag);
-        if ((e = produce(g + 1, false)) != hipSuccess) return e;
-      } else {
-        // group g+1's cross with group g's panels: block 2g+2 first (its
-        // panel's chain waits for it), block 2g+3 on side2 meanwhile
-        const int64_t pa = b.poff[2 * (g + 1)], na = (ACE_DIAG_SKIP & 4) ? 0 : b.poff[2 * (g + 1) + 1] - pa;
-        const int64_t pb = b.poff[2 * (g + 1) + 1], nb = (ACE_DIAG_SKIP & 4) ? 0 : b.poff[2 * (g + 1) + 2] - pb;
-        const int64_t nah = xs ? std::min<int64_t>(na, XSPLIT_HEAD) : na;  // head on `side`
-        if (xs) {  // side2 starts with `side` (bulk g-1 done), not after the head
-          if ((e = hipEventRecord(E1(g + 1), side)) != hipSuccess) return e;
-          if ((e = hipStreamWaitEvent(side2, E1(g + 1), 0)) != hipSuccess) return e;
-        }
-        if (nah > 0) hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nah), dim3(UTHREADS), 0, side, b.A, b.ld,
-                           b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0,
-                           -1, -1, b.ptiles + pa, gout(k + 2), -1, nullptr, 1, 0);
-        if (xs) {  // the rest of block 2g+2's cross on side2; its panel GEMM waits for E3
-          if (na > nah)
-            hipLaunchKernelGGL(k_update_pair, dim3((unsigned)(na - nah)), dim3(UTHREADS), 0, side2,
-                               b.A, b.ld, b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)],
-                               b.P[slot(k + 1)], b.ld, ka0, -1, -1, b.ptiles + pa + nah, gout(k + 2),
-                               -1, nullptr, 1, 0);
-          if ((e = hipEventRecord(E3(g + 1), side2)) != hipSuccess) return e;
-        }
-        if (nb > 0) {
-          if (two2 && !xs) {
-            if ((e = hipEventRecord(E1(g + 1), side)) != hipSuccess) return e;
-            if ((e = hipStreamWaitEvent(side2, E1(g + 1), 0)) != hipSuccess) return e;
-          }
-          hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nb), dim3(UTHREADS), 0, side2, b.A, b.ld,
-                             b.W[slot(k)], b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld,
-                             ka0, -1, -1, b.ptiles + pb, no_gather(), -1, nullptr, 1, 0);
-          if (two2 && (e = hipEventRecord(E2(g + 1), side2)) != hipSuccess) return e;
-        }
-        if ((e = produce(g + 1, nb > 0)) != hipSuccess) return e;
-      }
-      if (two && (e = hipEventRecord(sy->ev[2 * (g + 1)], side)) != hipSuccess) return e;
-    }
-    const bool timed = tm && tm->ev && used + 2 <= tm->nev;
-    if (timed) (void)hipEventRecord(tm->ev[used], st);
-    unsigned grid = b.gorder ? (unsigned)b.glen
-                             : (b.order ? (unsigned)b.norder : nT * (nT + 1) / 2);
-    const Tile *ord = b.gorder ? b.gorder + (int64_t)g * b.glen : b.order;
-    const int kx0 = more ? 2 * (g + 1) : -1, kx1 = more ? 2 * (g + 1) + zsize(g + 1) : -1;
-    // merged: [group g+1's cross tiles | the bulk order]
-    const bool mfront = merged && more && zsize(g) == 2;
-    if (mfront) {
-      grid = (unsigned)(b.moff[g + 1] - b.moff[g]);
-      ord = b.morder + b.moff[g];
-    }
-    if (zsize(g) == 2)
-      hipLaunchKernelGGL(k_update_pair, dim3(grid), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[slot(k)],
-                         b.P[slot(k)], b.W[slot(k + 1)], b.P[slot(k + 1)], b.ld, ka0, kx0, kx1,
-                         ord, mfront ? gout(k + 2) : no_gather(), mfront ? b.mfront[g] : -1,
-                         mfront ? b.mcnt + g : nullptr, 1, 0);
-    else
-      hipLaunchKernelGGL(k_update, dim3(grid), dim3(UTHREADS), 0, st, b.A, b.ld, b.W[slot(k)],
-                         b.P[slot(k)], b.W[slot(k)], b.ld, ka0, -1, ord, 1, no_gather());
-    if (timed) {
-      (void)hipEventRecord(tm->ev[used + 1], st);
-      if (tm->flops)
-        tm->flops[used / 2] = (zsize(g) == 2 ? update_gemm_tiles_pair(naug, ka0, mfront ? -1 : kx0,
-                                                                      mfront ? -1 : kx1)
-                                             : update_gemm_tiles(naug, ka0, -1, false)) *
-                              2.0 * UT * UT * NB;
-      used += 2;
-    }
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-  }
-  if (tm && tm->used) *tm->used = used;
-  return hipSuccess;
-}
-
 // Two-panel launches on k_update_multi (default; ACE_MULTI2=0: k_update_pair)
 static bool multi2_on() {
   static int v = -1;
@@ -3085,7 +2757,7 @@ static hipError_t run_sweep_groups(const SweepBufs &b, hipStream_t st, const Swe
     } else if (npan == 2 && !multi2) {
       hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nt), dim3(UTHREADS), 0, s_, b.A, b.ld,
                          b.W[slot(kb)], b.P[slot(kb)], b.W[slot(kb + 1)], b.P[slot(kb + 1)], b.ld,
-                         ka0, kx0, kx1, tl, go, -1, nullptr, 1, 0);
+                         ka0, kx0, kx1, tl, go, 1, 0);
     } else {
       PanelSet ps;
       for (int j = 0; j < 4; ++j) {
@@ -3234,7 +2906,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
     } else if (npan == 2 && !multi2) {
       hipLaunchKernelGGL(k_update_pair, dim3((unsigned)nt), dim3(UTHREADS), 0, s_, b.A, b.ld,
                          b.W[slot(kb)], b.P[slot(kb)], b.W[slot(kb + 1)], b.P[slot(kb + 1)], b.ld,
-                         ka0, kx0, kx1, tl, go, -1, nullptr, 1, 0);
+                         ka0, kx0, kx1, tl, go, 1, 0);
     } else {
       PanelSet ps;
       for (int j = 0; j < 4; ++j) {
@@ -3290,7 +2962,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   int *const fctr = (b.bq && b.breserve > 0 && chain_fuse()) ? b.bq + (int64_t)ng * BQ_INTS : nullptr;
   auto chain = [&](int k, hipStream_t s_) {  // [pivot +] sub-steps of panel k (gathered)
     panel_chain(b.P[slot(k)], b.W[slot(k)], b.ld, (int64_t)k * NB, b.SW, b.S, b.piv, b.flag, 1, 0,
-                s_, fused_pivot && k > 0, nullptr, true, fctr ? fctr + 2 * k : nullptr);
+                s_, fused_pivot && k > 0, true, fctr ? fctr + 2 * k : nullptr);
   };
   hipError_t e;
   if (b.bq && b.breserve > 0 &&
@@ -3319,9 +2991,8 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   auto produce_q = [&](int G) -> hipError_t {
     const int kb = Z * G;
     if (G == 0) {
-      hipLaunchKernelGGL(k_gather<false>, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, side,
-                         b.A, b.ld, (int64_t)0, b.P[slot(0)], b.W[slot(0)], b.ld, b.S[0], nullptr,
-                         nullptr, nullptr);
+      hipLaunchKernelGGL(k_gather, dim3((unsigned)(naug / 64), NB / 64), dim3(256), 0, side, b.A,
+                         b.ld, (int64_t)0, b.P[slot(0)], b.W[slot(0)], b.ld, b.S[0]);
     } else {
       const Tile *tl;
       int64_t nt;
@@ -3458,20 +3129,13 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
 
 hipError_t run_sweep(const SweepBufs &b, hipStream_t st, const SweepSync *sy,
                      const SweepTiming *tm) {
-  if (pair_steps() && b.ptiles && b.xtiles && b.P[2] && b.npad / NB >= 2) {
-    // the group schedule (any Z); ACE_GROUP_SCHED=0 -- and the merged /
-    // split-cross variants, which only it implements -- select the round-2
-    // pair schedule (Z = 2, k_update_pair)
-    static const bool gs = [] {
-      const char *e = getenv("ACE_GROUP_SCHED");
-      return !(e && atoi(e) == 0);
-    }();
-    if (b.P[2 * b.Z - 1] && b.htiles && heads_on() && sy && sy->side && sy->side2 &&
+  if (pair_steps() && b.ptiles && b.xtiles && b.P[2 * b.Z - 1] && b.npad / NB >= 2) {
+    // the group schedules (Z steps per bulk launch): head / tail lookahead
+    // (default) or the round-3 group lookahead (ACE_HEADS=0)
+    if (b.htiles && heads_on() && sy && sy->side && sy->side2 &&
         sy->nev >= 5 * (int)(b.npad / NB) + 3)
       return run_sweep_heads(b, st, sy, tm);
-    if (b.P[2 * b.Z - 1] && (b.Z > 2 || (gs && !b.morder && !xsplit_cross())))
-      return run_sweep_groups(b, st, sy, tm);
-    return run_sweep_pairs(b, st, sy, tm);
+    return run_sweep_groups(b, st, sy, tm);
   }
   const int64_t naug = b.ld;
   const unsigned nT = (unsigned)(naug / UT);
@@ -3650,7 +3314,7 @@ hipError_t shard_unpack_part(const ShardSweep &b, int k, int buf, int64_t i_lo, 
 // Panel k's pivot sub-steps (k_pivot + the split sub-steps), no panel GEMM.
 hipError_t shard_chain(const ShardSweep &b, int k, int buf, hipStream_t st) {
   panel_chain(b.P[buf], b.W[buf], b.ld, (int64_t)k * NB, b.SW, b.S, b.piv, b.flag, b.G, b.r, st,
-              false, nullptr, true);
+              false, true);
   return hipGetLastError();
 }
 

@@ -492,9 +492,7 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     the panel stream), the cost-sorted bulk order (ACE_TAIL_SORT=1), the
     gather fused into the cross launches (ACE_XGATHER=0: k_gather), one
     stream for everything (ACE_LOOKAHEAD=0), the panel GEMM on 128-tiles
-    (ACE_PGEMM_TILES=0: the 64-row k_panel_gemm) and the next group's cross
-    tiles at the head of the bulk launch (ACE_XMERGE=1, with and without the
-    fused gather) instead of side-stream launches.  Three and four steps per
+    (ACE_PGEMM_TILES=0: the 64-row k_panel_gemm).  Three and four steps per
     bulk launch (ACE_GROUP=3 / 4, k_update_multi; groups 3+2 / 4+1 at n =
     1100, 3+3 / 4+2 at 1500, 3+3+3+2 / 4+4+3 at 2600) are bit-identical too,
     with and without the fused gather, the second side stream and lookahead,
@@ -526,12 +524,7 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
                 "one_stream": {"ACE_PAIR": "1", "ACE_LOOKAHEAD": "0", **z2},
                 "pgemm_rows": {"ACE_PAIR": "1", "ACE_PGEMM_TILES": "0", **z2},
                 "single_pgemm_rows": {"ACE_PAIR": "0", "ACE_PGEMM_TILES": "0"},
-                "merged": {"ACE_PAIR": "1", "ACE_XMERGE": "1", **z2},
-                "merged_gather": {"ACE_PAIR": "1", "ACE_XMERGE": "1", "ACE_XGATHER": "0", **z2},
-                "unmerged": {"ACE_PAIR": "1", "ACE_XMERGE": "0", **z2},
-                "xsplit": {"ACE_PAIR": "1", "ACE_XSPLIT": "1", **z2},
                 "pair_kernel": {"ACE_MULTI2": "0", **z2},
-                "pair_schedule": {"ACE_GROUP_SCHED": "0", **z2},
                 "group3": {"ACE_GROUP": "3", "ACE_HEADS": "0"},
                 "group4": {"ACE_GROUP": "4", "ACE_HEADS": "0"},
                 "group4_gather": {"ACE_GROUP": "4", "ACE_HEADS": "0", "ACE_XGATHER": "0"},
@@ -560,24 +553,6 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
         outs[name] = np.load(out)
     for name in variants:
         assert np.array_equal(outs["single"], outs[name]), name
-
-
-def test_gather_pivot_is_bitwise_neutral(A, tmp_path):
-    """Sub-block 0's sweep inside k_gather (ACE_GATHER_PIV=1) and as its own
-    k_pivot launch (default) give the same inverse bit for bit."""
-    import os
-    import subprocess
-    import sys
-    from additivecausalexpansion_amd.synthetic import make_problem
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    y, X, Z, th, _ = make_problem(1300, 4, 5, seed=29)
-    K = A.kernmat_SE_symmetric_cpp(X, Z, th)["full"]
-    inp = str(tmp_path / "k.npz")
-    np.savez(inp, K=K, s=th[0])
-    out = str(tmp_path / "inv0.npy")
-    env = dict(os.environ, ACE_GATHER_PIV="1")
-    run_child(_ORDER_SNIPPET.format(root=root, inp=inp, out=out), env=env, timeout=100)
-    assert np.array_equal(A.invkernel_cpp(K, th[0])["inv"], np.load(out))
 
 
 def test_split_panel_is_bitwise_neutral(A, tmp_path):
@@ -618,34 +593,31 @@ np.save({out!r}, np.concatenate(outs))
 
 
 @pytest.mark.parametrize("n", [2000, 2600])
-def test_merged_cross_model_is_bitwise_neutral(tmp_path, n):
-    """The fused model's para_update with the next group's cross tiles at the
-    head of the bulk launch (ACE_XMERGE=1: device counter + side-stream wait
-    kernel) gives the same gradient and stats bit for bit as the side-stream
-    cross launches, over two evaluations (the per-sweep counter reset).
-    n = 2000: 8 steps; 2600: 11 (a last single step).  Also the default
-    schedule under the smaller stream budgets (ACE_STREAMS=2: the tail path
-    on the panel stream; 1: everything on the main stream), which run the
-    same launch graph serialised in host order."""
+def test_model_schedules_are_bitwise_neutral(tmp_path, n):
+    """The fused model's para_update gives the same gradient and stats bit
+    for bit, over two evaluations, under the group schedule at two and four
+    steps per bulk launch (ACE_HEADS=0) and the head / tail lookahead at four
+    (the default above n = 8192) and two.  n = 2000: 8 steps; 2600: 11 (a
+    last single step).  Also the default schedule under the smaller stream
+    budgets (ACE_STREAMS=2: the tail path on the panel stream; 1: everything
+    on the main stream), which run the same launch graph serialised in host
+    order.  (Round 6 removed the round-2 pair schedule's merged
+    and split cross variants this test covered before.)"""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
-    z2 = dict(ACE_GROUP="2", ACE_HEADS="0")  # the merged / split cross are Z = 2 schedules
-    for v in ("0", "1", "split", "group4", "heads4", "heads2", "streams2", "streams1"):
+    for v in ("0", "group4", "heads4", "heads2", "streams2", "streams1"):
         out = str(tmp_path / f"m{v}.npy")
-        env = (dict(os.environ, ACE_XSPLIT="1", **z2) if v == "split" else
-               dict(os.environ, ACE_STREAMS=v[-1]) if v.startswith("streams") else
+        env = (dict(os.environ, ACE_STREAMS=v[-1]) if v.startswith("streams") else
                dict(os.environ, ACE_GROUP="4", ACE_HEADS="0") if v == "group4" else
                dict(os.environ, ACE_GROUP="4", ACE_HEADS="1") if v == "heads4" else
                dict(os.environ, ACE_GROUP="2", ACE_HEADS="1") if v == "heads2" else
-               dict(os.environ, ACE_XMERGE=v, **z2))
+               dict(os.environ, ACE_GROUP="2", ACE_HEADS="0"))
         run_child(_MODEL_SNIPPET.format(root=root, n=n, out=out), env=env, timeout=100)
         outs[v] = np.load(out)
-    assert np.all(np.isfinite(outs["1"]))
-    assert np.array_equal(outs["0"], outs["1"])
-    assert np.array_equal(outs["0"], outs["split"])  # the split cross (ACE_XSPLIT=1)
+    assert np.all(np.isfinite(outs["0"]))
     # four steps per bulk launch: the assembly's first part covers the first
     # group's four panels, its side path runs under the rest
     assert np.array_equal(outs["0"], outs["group4"])
