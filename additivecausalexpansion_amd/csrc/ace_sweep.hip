@@ -2267,7 +2267,7 @@ static bool pgemm_tiles() {
 
 // ACE_DIAG_SKIP (compile-time, timing diagnostics only -- the results are
 // wrong): bit 1 skips the pivot sub-sweeps and panel updates, bit 2 the panel
-// GEMM, bit 4 the lookahead cross launches of the pair schedule
+// GEMM
 #ifndef ACE_DIAG_SKIP
 #define ACE_DIAG_SKIP 0
 #endif
@@ -2709,7 +2709,7 @@ static bool multi2_on() {
   return v != 0;
 }
 
-// Z = b.Z sweep steps per bulk launch (run_sweep_pairs: the round-2 Z = 2 form).
+// Z = b.Z sweep steps per bulk launch (Z = 2 is the round-2 pair form).
 // Group g = steps Z g .. Z g + z_g - 1 (the last one may be shorter), panels
 // in slots k % 2Z.
 //   side:  wait(bulk g-1 done) -> cross of group g+1's first block kb with
