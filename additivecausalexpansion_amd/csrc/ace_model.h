@@ -75,11 +75,12 @@ struct SweepWork {
     }
     breserve = (Z > 2 && heads_on()) ? bulk_reserve(naug) : 0;
     if (breserve > 0) {
-      // + per sweep step the barrier and exit counters of k_panel_split4: zero
+      // + per sweep step the barrier and exit counters of k_panel_split4 and
+      // the D_0 counter of k_update_q4 (ACE_QSPLIT): zero
       // when allocated, reset by each launch's last workgroup (the per-sweep
       // memset covers the queues only: the first chain can start before it)
       void *const old = bq.p;
-      alloc(ctx, bq, (size_t)((npad / NB + Z - 1) / Z * BQ_INTS + 2 * (npad / NB)) * sizeof(int),
+      alloc(ctx, bq, (size_t)((npad / NB + Z - 1) / Z * BQ_INTS + 3 * (npad / NB)) * sizeof(int),
             "alloc bulk queues");
       if (bq.p != old) ck(ctx, hipMemsetAsync(bq.p, 0, bq.bytes, ctx->stream), "memset queues");
     }

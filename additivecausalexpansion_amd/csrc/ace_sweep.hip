@@ -2040,6 +2040,129 @@ __global__ __launch_bounds__(256, 4) void k_update_q(double *__restrict__ A, int
   }
 }
 
+// k_update_q with every 64 x 64 quarter split into four 32 x 32 pieces,
+// one per 256-thread workgroup (each wave one 16 x 16 MFMA block), for the
+// latency-critical head launches of small n (ACE_QSPLIT): four times the
+// workgroups, a quarter of each one's K loop.  Every element's MFMA chain
+// (operands, k order, accumulator start) is k_update_q's: bit-identical.
+// The quarter holding D_0 of a gathered panel is finished by its last
+// piece: each piece stores (and gathers) its part, releases it at agent
+// scope and counts into *qctr; the piece that counts last acquires, reads
+// D_0 back from the gathered snapshot S0 -- the values k_update_q's fused
+// sweep reads from its registers -- runs the sub-sweep and resets *qctr.
+// No workgroup waits for another.
+__global__ __launch_bounds__(256, 4) void k_update_q4(double *__restrict__ A, int64_t ld, PanelSet ps,
+                                                   int npan, int64_t ldp,
+                                                   const Tile *__restrict__ tiles, GatherOut go,
+                                                   double *__restrict__ pivSW,
+                                                   double *__restrict__ piv,
+                                                   int *__restrict__ flag, int *__restrict__ qctr) {
+  ACE_WGT(4, true);
+  constexpr int QT = XT / 2;        // 32: the piece
+  constexpr int QL = QT + 8;        // LDS pitch
+  __shared__ __attribute__((aligned(16))) double sbuf[SUB * (SUB + 2)];  // staging, then D_0
+  static_assert(2 * 2 * BK * QL <= SUB * (SUB + 2), "staging fits");
+  double (*sW)[BK][QL] = reinterpret_cast<double (*)[BK][QL]>(sbuf);
+  double (*sP)[BK][QL] = reinterpret_cast<double (*)[BK][QL]>(sbuf + 2 * BK * QL);
+  __shared__ int last;
+  const Tile tt = tiles[blockIdx.x >> 4];
+  if (tt.I < 0) return;  // padding of the XCD order
+  const int q = (blockIdx.x >> 2) & 3, pc = blockIdx.x & 3;
+  const int64_t Rq = (int64_t)tt.I * UT + XT * (q & 1), Cq = (int64_t)tt.J * UT + XT * (q >> 1);
+  const int64_t R0 = Rq + QT * (pc & 1), C0 = Cq + QT * (pc >> 1);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int wr = wv & 1, wc = wv >> 1;  // rows 16*wr.., cols 16*wc.. of the piece
+  const int lr = lane & 15, lk = lane >> 4;
+  d4 acc;
+  {
+    const int64_t r = R0 + 16 * wr + lr;
+    const int64_t c = C0 + 16 * wc + lk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = A[r + (c + 4 * j) * ld];
+  }
+  const int sk = tid >> 4, sm = (tid & 15) * 2;  // one double2 of each operand per chunk
+  double2 w0, p0, w1, p1;
+  const int T = npan * NCH;
+#define UQ4_LOAD(W, P, TT)                                                         \
+  do {                                                                             \
+    const int pj_ = (TT) / NCH, ch_ = (TT) - pj_ * NCH;                            \
+    const int64_t off_ = (int64_t)ch_ * BK * ldp;                                  \
+    W = *reinterpret_cast<const double2 *>(psel(ps.R, pj_) + (R0 + sm) + (int64_t)sk * ldp + off_); \
+    P = *reinterpret_cast<const double2 *>(psel(ps.C, pj_) + (C0 + sm) + (int64_t)sk * ldp + off_); \
+  } while (0)
+#define UQ4_STAGE(W, P, BUF)                                                       \
+  do {                                                                             \
+    *reinterpret_cast<double2 *>(&sW[BUF][sk][sm]) = W;                            \
+    *reinterpret_cast<double2 *>(&sP[BUF][sk][sm]) = P;                            \
+  } while (0)
+  auto mma = [&](int cur) {
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      const double a = sP[cur][4 * kk + lk][16 * wc + lr];
+      const double b = sW[cur][4 * kk + lk][16 * wr + lr];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+  };
+  static_assert(NCH % 2 == 0 && NCH >= 4, "two chunks per pipeline turn");
+  UQ4_LOAD(w0, p0, 0);
+  UQ4_STAGE(w0, p0, 0);
+  UQ4_LOAD(w1, p1, 1);
+  UQ4_LOAD(w0, p0, 2);
+  __syncthreads();
+#pragma unroll 1
+  for (int t = 0; t < T; t += 2) {
+    mma(0);
+    UQ4_STAGE(w1, p1, 1);
+    if (t + 3 < T) UQ4_LOAD(w1, p1, t + 3);
+    __syncthreads();
+    mma(1);
+    if (t + 2 < T) {
+      UQ4_STAGE(w0, p0, 0);
+      if (t + 4 < T) UQ4_LOAD(w0, p0, t + 4);
+    }
+    __syncthreads();
+  }
+#undef UQ4_LOAD
+#undef UQ4_STAGE
+  ACE_WGT_MARK(0);
+  {
+    const int64_t r = R0 + 16 * wr + lr;
+    const int64_t c = C0 + 16 * wc + lk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      A[r + (c + 4 * j) * ld] = acc[j];
+      if (go.k0 >= 0) gput(go, r, c + 4 * j, acc[j]);
+    }
+  }
+  if (!(pivSW && go.k0 >= 0 && Rq == go.k0 && Cq == go.k0)) return;
+  // the D_0 quarter: the last of its four pieces runs the sub-sweep
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    last = __hip_atomic_fetch_add(qctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(qctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  __shared__ double pv[SUB];
+  double(*M)[SUB + 2] = reinterpret_cast<double(*)[SUB + 2]>(sbuf);
+  double v[SUB / 4];
+  // D_0 = S0[0:64, 0:64] (row a, column c at a + c SUB), as k_pivot reads it
+#pragma unroll
+  for (int qq = 0; qq < SUB / 4; ++qq)
+    v[qq] = __hip_atomic_load(go.S0 + lane + (16 * wv + qq) * SUB, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+  ACE_WGT_MARK(1);
+  pivot_sweep_blk<SUB + 2>(v, M, pv, tid);
+  ACE_WGT_MARK(2);
+  pivot_store<4>(v, pv, tid, pivSW, piv, go.k0, flag);
+}
+
 // The head path's panel GEMM (run_sweep_heads) on 64 x 64 quarters of the
 // 128-tiles: W_I,J = Pn_I W_kk[:, J] as k_panel_gemm_t, a quarter of its work
 // per 256-thread workgroup.  The head launches hold few tiles (the rows of
@@ -2132,6 +2255,74 @@ __global__ __launch_bounds__(256, 4) void k_panel_gemm_q(double *__restrict__ W,
 #pragma unroll
       for (int j = 0; j < 4; ++j) W[rr + (c + 4 * j) * ldp] = acc[ci][ri][j];
     }
+}
+
+// k_panel_gemm_q on 32 x 32 pieces (ACE_QSPLIT, small n): each wave one
+// 16 x 16 MFMA block, four times the workgroups; every element's chain is
+// k_panel_gemm_q's (bit-identical).  Grid: (2 x 64-row blocks, 2 NB / 64).
+__global__ __launch_bounds__(256, 4) void k_panel_gemm_q4(double *__restrict__ W,
+                                                        const double *__restrict__ Pn,
+                                                        int64_t ldp, int64_t k0, int rt0) {
+  ACE_WGT(3, true);
+  constexpr int QT = XT / 2, QL = QT + 8;
+  __shared__ __attribute__((aligned(16))) double sW[2][BK][QL];  // Pn rows of the piece
+  __shared__ __attribute__((aligned(16))) double sP[2][BK][QL];  // W_kk rows c
+  const int64_t R0 = (int64_t)rt0 * UT + (int64_t)blockIdx.x * QT, C0 = (int64_t)blockIdx.y * QT;
+  if (R0 >= k0 && R0 < k0 + NB) return;  // pivot rows are already final
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int wr = wv & 1, wc = wv >> 1;  // rows 16*wr.., cols 16*wc..
+  const int lr = lane & 15, lk = lane >> 4;
+  const int sk = tid >> 4, sm = (tid & 15) * 2;
+  const double *gW = Pn + (R0 + sm) + (int64_t)sk * ldp;
+  const double *gP = W + (k0 + C0 + sm) + (int64_t)sk * ldp;  // W_kk(c, k) = W[k0 + c, k]
+  d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+  double2 w0, p0, w1, p1;
+#define PQ4_LOAD(WW, PP, CH)                                                        \
+  do {                                                                              \
+    const int64_t off_ = (int64_t)(CH) * BK * ldp;                                  \
+    WW = *reinterpret_cast<const double2 *>(gW + off_);                             \
+    PP = *reinterpret_cast<const double2 *>(gP + off_);                             \
+  } while (0)
+#define PQ4_STAGE(WW, PP, BUF)                                                      \
+  do {                                                                              \
+    *reinterpret_cast<double2 *>(&sW[BUF][sk][sm]) = WW;                            \
+    *reinterpret_cast<double2 *>(&sP[BUF][sk][sm]) = PP;                            \
+  } while (0)
+  auto mma = [&](int cur) {
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      const double a = sP[cur][4 * kk + lk][16 * wc + lr];
+      const double b = sW[cur][4 * kk + lk][16 * wr + lr];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+  };
+  PQ4_LOAD(w0, p0, 0);
+  PQ4_STAGE(w0, p0, 0);
+  PQ4_LOAD(w1, p1, 1);
+  PQ4_LOAD(w0, p0, 2);
+  __syncthreads();
+  ACE_WGT_MARK(0);
+#pragma unroll 1
+  for (int ch = 0; ch < NCH; ch += 2) {
+    mma(0);
+    PQ4_STAGE(w1, p1, 1);
+    if (ch + 3 < NCH) PQ4_LOAD(w1, p1, ch + 3);
+    __syncthreads();
+    mma(1);
+    if (ch + 2 < NCH) {
+      PQ4_STAGE(w0, p0, 0);
+      if (ch + 4 < NCH) PQ4_LOAD(w0, p0, ch + 4);
+    }
+    __syncthreads();
+  }
+#undef PQ4_LOAD
+#undef PQ4_STAGE
+  ACE_WGT_MARK(1);
+  const int64_t rr = R0 + 16 * wr + lr;
+  const int64_t c = C0 + 16 * wc + lk;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) W[rr + (c + 4 * j) * ldp] = acc[j];
 }
 
 // ---------------------------------------------------------------- sharded panel
@@ -2926,7 +3117,22 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   // panels k >= 1 are gathered by k_update_q launches, which sweep their D_0
   // (the blocked pivot only: the same code as k_pivot's, bit-identical)
   const bool fused_pivot = hq && ACE_PIVOT_BLK;
-  auto qupd = [&](int npan, int kb, const Tile *tl, int64_t nt, GatherOut go, hipStream_t s_) {
+  // Small n (with the bulk queue): the latency-critical launches on 32 x 32
+  // pieces (k_update_q4 / k_panel_gemm_q4, bit-identical): every Q launch,
+  // the head panel GEMMs and each group's last tail panel GEMM -- C1 3.59 ->
+  // 3.41 ms (profiles/r06_qsplit_ab.txt).  ACE_QSPLIT: 1 (default) all of
+  // them, 3 the Q launches only, 2 the group-boundary Q only, 0 none.  One
+  // D_0 counter per panel after the chain counters (zero when allocated,
+  // reset by the last piece).
+  static const int qsplit = [] {
+    const char *e = getenv("ACE_QSPLIT");
+    return e ? atoi(e) : 1;
+  }();
+  int *const qctr = (qsplit > 0 && b.bq && b.breserve > 0)
+                        ? b.bq + (int64_t)((steps + Z - 1) / Z) * BQ_INTS + 2 * steps
+                        : nullptr;
+  auto qupd = [&](int npan, int kb, const Tile *tl, int64_t nt, GatherOut go, hipStream_t s_,
+                  bool boundary = false) {
     if (nt <= 0) return;
     if (!hq) {
       upd(npan, kb, -1, -1, tl, nt, go, s_);
@@ -2940,16 +3146,36 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
     // a launch that gathers a panel also sweeps its D_0 (k_update_q's fused
     // pivot): that panel's chain then starts at sub-step 0's panel update
     const bool fp = fused_pivot && go.k0 >= 0;
-    hipLaunchKernelGGL(k_update_q, dim3((unsigned)(4 * nt)), dim3(256), 0, s_, b.A, b.ld, ps, npan,
-                       b.ld, tl, go, fp ? b.SW : nullptr, fp ? b.piv : nullptr,
-                       fp ? b.flag : nullptr);
+    if (qctr && (qsplit != 2 || boundary))  // small n: 32 x 32 pieces (k_update_q4)
+      hipLaunchKernelGGL(k_update_q4, dim3((unsigned)(16 * nt)), dim3(256), 0, s_, b.A, b.ld, ps,
+                         npan, b.ld, tl, go, fp ? b.SW : nullptr, fp ? b.piv : nullptr,
+                         fp ? b.flag : nullptr, qctr + (go.k0 >= 0 ? go.k0 / NB : 0));
+    else
+      hipLaunchKernelGGL(k_update_q, dim3((unsigned)(4 * nt)), dim3(256), 0, s_, b.A, b.ld, ps, npan,
+                         b.ld, tl, go, fp ? b.SW : nullptr, fp ? b.piv : nullptr,
+                         fp ? b.flag : nullptr);
   };
   // panel k's GEMM W_i = Pn_i W_kk over row tiles [r0, r1) (head) or all the
   // others (tail); the kernel itself skips the pivot block's rows
-  auto pgemm = [&](int k, int r0, int r1, bool head, hipStream_t s_) {
+  auto pgemm = [&](int k, int r0, int r1, bool head, hipStream_t s_, bool last = false) {
     const int n = head ? r1 - r0 : (int)nT - (r1 - r0);
     if (n <= 0) return;
-    if (head && ACE_PGEMM_HEADQ)
+    if (!head && last && qctr && qsplit == 1) {
+      // the group's last tail GEMM is on the path to the next group's Q: on
+      // 32 x 32 pieces (k_panel_gemm_q's chain, k_panel_gemm_t's result), the
+      // rows before and after the head
+      if (r0 > 0)
+        hipLaunchKernelGGL(k_panel_gemm_q4, dim3((unsigned)(2 * r0 * (UT / XT)), 2 * (NB / XT)),
+                           dim3(256), 0, s_, b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, 0);
+      if ((int)nT > r1)
+        hipLaunchKernelGGL(k_panel_gemm_q4, dim3((unsigned)(2 * ((int)nT - r1) * (UT / XT)), 2 * (NB / XT)),
+                           dim3(256), 0, s_, b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, r1);
+      return;
+    }
+    if (head && ACE_PGEMM_HEADQ && qctr && qsplit == 1)
+      hipLaunchKernelGGL(k_panel_gemm_q4, dim3((unsigned)(2 * n * (UT / XT)), 2 * (NB / XT)), dim3(256),
+                         0, s_, b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, r0);
+    else if (head && ACE_PGEMM_HEADQ)
       hipLaunchKernelGGL(k_panel_gemm_q, dim3((unsigned)(n * (UT / XT)), NB / XT), dim3(256), 0, s_,
                          b.W[slot(k)], b.P[slot(k)], b.ld, (int64_t)k * NB, r0);
     else
@@ -2997,7 +3223,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
       const Tile *tl;
       int64_t nt;
       list(G, 0, tl, nt);
-      qupd(zsize(G - 1), Z * (G - 1), tl, nt, gout(kb), side);  // Q
+      qupd(zsize(G - 1), Z * (G - 1), tl, nt, gout(kb), side, true);  // Q
     }
     return qfirst ? hipEventRecord(Eq(G), side) : hipSuccess;
   };
@@ -3036,7 +3262,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
       const int k = kb + j;
       hipError_t q;
       if ((q = hipStreamWaitEvent(side2, Esp(k), 0)) != hipSuccess) return q;
-      pgemm(k, (k + 1) * KT, hend, false, side2);
+      pgemm(k, (k + 1) * KT, hend, false, side2, j + 1 == zb);
       if (j + 1 < zb) {
         if ((q = hipStreamWaitEvent(side2, Egh(k), 0)) != hipSuccess) return q;
         list(G, zb + j + 1, tl, nt);

@@ -505,7 +505,9 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     sub-steps in one launch with a grid barrier between them
     (k_panel_split4, ACE_CHAIN_FUSE=1, default with the small-n bulk
     queue) against four k_panel_split launches (0); the bulk tiles in
-    Hilbert-curve pieces per XCD (ACE_BULK_CURVE=1)."""
+    Hilbert-curve pieces per XCD (ACE_BULK_CURVE=1); the small-n head
+    launches on 32 x 32 pieces (ACE_QSPLIT, default 1) against 64 x 64 (0),
+    the Q launches only (3) and the group-boundary Q only (2)."""
     import os
     import subprocess
     import sys
@@ -545,7 +547,10 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
                 "chain_fused_reserve2": {"ACE_CHAIN_FUSE": "1", "ACE_BULK_RESERVE": "2"},
                 "heads3_chain_fused": {"ACE_GROUP": "3", "ACE_HEADS": "1", "ACE_CHAIN_FUSE": "1"},
                 "bulk_curve": {"ACE_BULK_CURVE": "1"},
-                "bulk_curve_unreserved": {"ACE_BULK_CURVE": "1", "ACE_BULK_RESERVE": "0"}}
+                "bulk_curve_unreserved": {"ACE_BULK_CURVE": "1", "ACE_BULK_RESERVE": "0"},
+                "qsplit_off": {"ACE_QSPLIT": "0"}, "qsplit_q": {"ACE_QSPLIT": "3"},
+                "qsplit_boundary": {"ACE_QSPLIT": "2"},
+                "heads3_qsplit_off": {"ACE_GROUP": "3", "ACE_HEADS": "1", "ACE_QSPLIT": "0"}}
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)
