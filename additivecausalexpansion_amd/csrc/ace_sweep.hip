@@ -3213,6 +3213,19 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   // beside both took 163 us instead of ~40 (C1 trace, profiles/r05_v4_*).
   const bool qfirst = q_first(naug);
   auto Eq = [&](int G) { return sy->ev[2 * steps + 1 + 2 * G]; };  // group G's Q done
+  // ACE_TAIL_LAST=1 (default): group G >= 1's last tail panel GEMM on the head stream
+  // after the tail path's last T update (Et(G), an event slot the direct-wait
+  // schedule leaves free); the next group's Q then follows it in stream order
+  // and waits for the tail path through Et(G) instead of E2(G)
+  static const bool tail_last_on = [] {
+    const char *e = getenv("ACE_TAIL_LAST");
+    return !(e && atoi(e) == 0);
+  }();
+  // (small n: the chain-bound schedule with the bulk queue)
+  auto tlast = [&](int G) {
+    return tail_last_on && qdirect && b.bq && b.breserve > 0 && G > 0 && zsize(G) >= 2;
+  };
+  auto Et = [&](int G) { return sy->ev[2 * G + 1]; };
   // group G's first head launch (k_gather / Q); the rest by produce(G)
   auto produce_q = [&](int G) -> hipError_t {
     const int kb = Z * G;
@@ -3245,13 +3258,21 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
     // tail may wait for the whole head path (sy->tail_split) -- on the CUs
     // the assembly leaves free the two would otherwise share them step by step
     const bool split = G == 0 && sy->tail_split;
+    const bool tl_ = tlast(G);
     auto head = [&](int j) -> hipError_t {
       const int k = kb + j;
       chain(k, side);
       hipError_t q;
-      if ((q = hipEventRecord(Esp(k), side)) != hipSuccess) return q;
+      // (the tail path waits for Esp(k) unless its last GEMM moved here, for
+      // Egh(k) only before a T launch: no marker packet nobody waits for)
+      const bool lastj = j + 1 == zb;
+      if (!(tl_ && lastj) && (q = hipEventRecord(Esp(k), side)) != hipSuccess) return q;
       pgemm(k, (k + 1) * KT, hend, true, side);
-      if ((q = hipEventRecord(Egh(k), side)) != hipSuccess) return q;
+      if (!lastj && (q = hipEventRecord(Egh(k), side)) != hipSuccess) return q;
+      if (tl_ && j + 1 == zb) {  // the last tail GEMM here, after the tail path's T_{zb-1}
+        if ((q = hipStreamWaitEvent(side, Et(G), 0)) != hipSuccess) return q;
+        pgemm(k, (k + 1) * KT, hend, false, side, true);
+      }
       if (j + 1 < zb) {
         list(G, 2 + j, tl, nt);
         qupd(1, k, tl, nt, gout(k + 1), side);  // panel k on Q_{j+1}
@@ -3261,12 +3282,14 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
     auto tail = [&](int j) -> hipError_t {
       const int k = kb + j;
       hipError_t q;
+      if (tl_ && j + 1 == zb) return hipSuccess;  // on the head stream (above)
       if ((q = hipStreamWaitEvent(side2, Esp(k), 0)) != hipSuccess) return q;
       pgemm(k, (k + 1) * KT, hend, false, side2, j + 1 == zb);
       if (j + 1 < zb) {
         if ((q = hipStreamWaitEvent(side2, Egh(k), 0)) != hipSuccess) return q;
         list(G, zb + j + 1, tl, nt);
         upd(j + 1, kb, -1, -1, tl, nt, gout(k + 1), side2);  // T_{j+1}
+        if (tl_ && j + 2 == zb && (q = hipEventRecord(Et(G), side2)) != hipSuccess) return q;
       }
       return hipSuccess;
     };
@@ -3306,7 +3329,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
       // head path through E2).  Without qdirect both wait for ev[2g+1], the
       // main stream's record after all three.
       if (qdirect) {
-        if ((e = hipStreamWaitEvent(side, E2(g), 0)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(side, tlast(g) ? Et(g) : E2(g), 0)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(side, Eb(g - 1), 0)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(side2, Eb(g - 1), 0)) != hipSuccess) return e;
       } else {

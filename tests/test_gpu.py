@@ -507,7 +507,9 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     queue) against four k_panel_split launches (0); the bulk tiles in
     Hilbert-curve pieces per XCD (ACE_BULK_CURVE=1); the small-n head
     launches on 32 x 32 pieces (ACE_QSPLIT, default 1) against 64 x 64 (0),
-    the Q launches only (3) and the group-boundary Q only (2)."""
+    the Q launches only (3) and the group-boundary Q only (2); each group's
+    last tail panel GEMM on the head stream (ACE_TAIL_LAST, default 1) or on
+    the tail stream (0)."""
     import os
     import subprocess
     import sys
@@ -550,7 +552,9 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
                 "bulk_curve_unreserved": {"ACE_BULK_CURVE": "1", "ACE_BULK_RESERVE": "0"},
                 "qsplit_off": {"ACE_QSPLIT": "0"}, "qsplit_q": {"ACE_QSPLIT": "3"},
                 "qsplit_boundary": {"ACE_QSPLIT": "2"},
-                "heads3_qsplit_off": {"ACE_GROUP": "3", "ACE_HEADS": "1", "ACE_QSPLIT": "0"}}
+                "heads3_qsplit_off": {"ACE_GROUP": "3", "ACE_HEADS": "1", "ACE_QSPLIT": "0"},
+                "tail_last_off": {"ACE_TAIL_LAST": "0"},
+                "tail_last_off_qsplit_off": {"ACE_TAIL_LAST": "0", "ACE_QSPLIT": "0"}}
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)
