@@ -3223,9 +3223,11 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   }();
   // (small n: the chain-bound schedule with the bulk queue)
   auto tlast = [&](int G) {
-    return tail_last_on && qdirect && b.bq && b.breserve > 0 && G > 0 && zsize(G) >= 2;
+    return tail_last_on && qdirect && b.bq && b.breserve > 0 && zsize(G) >= 2 &&
+           !(G == 0 && sy->tail_split);
   };
   auto Et = [&](int G) { return sy->ev[2 * G + 1]; };
+  hipEvent_t const Ef = sy->ev[2 * steps - 1];  // group 0's tail path + filler (odd: free too)
   // group G's first head launch (k_gather / Q); the rest by produce(G)
   auto produce_q = [&](int G) -> hipError_t {
     const int kb = Z * G;
@@ -3304,6 +3306,8 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
         if ((r = tail(j)) != hipSuccess) return r;
     }
     if (G == 0 && sy->fill && (r = sy->fill(sy->fill_arg, side2)) != hipSuccess) return r;
+    // (group 0: the next Q also needs the assembly's filler launch: Ef)
+    if (G == 0 && sy->fill && tl_ && (r = hipEventRecord(Ef, side2)) != hipSuccess) return r;
     // (qdirect: E2(G) also stands for the head path, so that the main stream
     // waits for one event before each bulk launch)
     if (qdirect && !split && (r = hipStreamWaitEvent(side2, sy->ev[2 * G], 0)) != hipSuccess)
@@ -3329,7 +3333,9 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
       // head path through E2).  Without qdirect both wait for ev[2g+1], the
       // main stream's record after all three.
       if (qdirect) {
-        if ((e = hipStreamWaitEvent(side, tlast(g) ? Et(g) : E2(g), 0)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(side, !tlast(g) ? E2(g) : (g == 0 && sy->fill) ? Ef : Et(g), 0)) !=
+            hipSuccess)
+          return e;
         if ((e = hipStreamWaitEvent(side, Eb(g - 1), 0)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(side2, Eb(g - 1), 0)) != hipSuccess) return e;
       } else {
