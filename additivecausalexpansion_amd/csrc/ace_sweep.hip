@@ -3270,7 +3270,7 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
       const bool lastj = j + 1 == zb;
       if (!(tl_ && lastj) && (q = hipEventRecord(Esp(k), side)) != hipSuccess) return q;
       pgemm(k, (k + 1) * KT, hend, true, side);
-      if (!lastj && (q = hipEventRecord(Egh(k), side)) != hipSuccess) return q;
+      if ((!lastj || !tl_) && (q = hipEventRecord(Egh(k), side)) != hipSuccess) return q;
       if (tl_ && j + 1 == zb) {  // the last tail GEMM here, after the tail path's T_{zb-1}
         if ((q = hipStreamWaitEvent(side, Et(G), 0)) != hipSuccess) return q;
         pgemm(k, (k + 1) * KT, hend, false, side, true);
