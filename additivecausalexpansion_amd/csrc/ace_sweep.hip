@@ -2468,12 +2468,19 @@ static bool pgemm_tiles() {
 static void panel_chain(const double *Pn, double *W, int64_t ld, int64_t k0, double *SW,
                         double *const S[2], double *piv, int *flag, int G, int r,
                         hipStream_t st, bool pivot0 = false, bool no_gemm = false,
-                        int *fuse_ctr = nullptr) {
+                        int *fuse_ctr = nullptr, unsigned xlds = 0) {
   const bool split = panel_split();
   double *const SWb[2] = {SW, SW + SUB * SUB};  // ping-pong by sub-step
   if (split && fuse_ctr && !(ACE_DIAG_SKIP & 1)) {
     if (!pivot0) launch_pivot(S[0], 0, SWb[0], piv, k0, flag, st);
-    hipLaunchKernelGGL(k_panel_split4, dim3(NB / SUB, NB / SUB), dim3(256), 0, st, W, ld, k0, SW,
+    if (xlds) {
+      static unsigned set = 0;
+      if (set != xlds && hipFuncSetAttribute((const void *)k_panel_split4,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)xlds) == hipSuccess)
+        set = xlds;
+    }
+    hipLaunchKernelGGL(k_panel_split4, dim3(NB / SUB, NB / SUB), dim3(256), xlds, st, W, ld, k0, SW,
                        S[0], S[1], piv, flag, fuse_ctr);
   }
   for (int s = 0; s < ((ACE_DIAG_SKIP & 1) || (split && fuse_ctr) ? 0 : NB / SUB); ++s) {
@@ -3186,9 +3193,32 @@ static hipError_t run_sweep_heads(const SweepBufs &b, hipStream_t st, const Swee
   // small n: each panel's four split sub-steps in one launch (k_panel_split4),
   // its barrier counter after the bulk queues
   int *const fctr = (b.bq && b.breserve > 0 && chain_fuse()) ? b.bq + (int64_t)ng * BQ_INTS : nullptr;
+  // Small n: each fused chain launch with 13 KB of extra LDS, so that no
+  // bulk / cross / tail workgroup (73.7 KB) fits beside a chain workgroup
+  // (77.3 KB): the chain runs alone on its 16 CUs instead of sharing each
+  // with an MFMA-bound workgroup (2x slower).  With the head launches on
+  // 32 x 32 pieces (ACE_QSPLIT) C1 3.34 -> 3.10 ms (profiles/r06_chain_xlds_ab.txt;
+  // before them only the contention moved, r06_c1_chain_isolation_ab.txt).
+  // Placement only: bit-identical.  ACE_CHAIN_XLDS=B overrides the bytes (0:
+  // off), ACE_CHAIN_XLDS_J the panel mask within a group (default all),
+  // ACE_CHAIN_XLDS_G0=0 leaves group 0's chains (beside the assembly) as they were.
+  static const unsigned xlds = [] {
+    const char *e = getenv("ACE_CHAIN_XLDS");
+    return e ? (unsigned)std::max(0, atoi(e)) : 13312u;
+  }();
+  static const int xlds_j = [] {
+    const char *e = getenv("ACE_CHAIN_XLDS_J");
+    return e ? atoi(e) : -1;
+  }();
+  static const bool xlds_g0 = [] {
+    const char *e = getenv("ACE_CHAIN_XLDS_G0");
+    return !(e && atoi(e) == 0);
+  }();
   auto chain = [&](int k, hipStream_t s_) {  // [pivot +] sub-steps of panel k (gathered)
+    const int j = k % Z, G = k / Z;
     panel_chain(b.P[slot(k)], b.W[slot(k)], b.ld, (int64_t)k * NB, b.SW, b.S, b.piv, b.flag, 1, 0,
-                s_, fused_pivot && k > 0, true, fctr ? fctr + 2 * k : nullptr);
+                s_, fused_pivot && k > 0, true, fctr ? fctr + 2 * k : nullptr,
+                (fctr && qctr && (G > 0 || xlds_g0) && ((xlds_j >> j) & 1)) ? xlds : 0u);
   };
   hipError_t e;
   if (b.bq && b.breserve > 0 &&

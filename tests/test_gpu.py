@@ -509,7 +509,8 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
     launches on 32 x 32 pieces (ACE_QSPLIT, default 1) against 64 x 64 (0),
     the Q launches only (3) and the group-boundary Q only (2); each group's
     last tail panel GEMM on the head stream (ACE_TAIL_LAST, default 1) or on
-    the tail stream (0)."""
+    the tail stream (0); the fused chains alone on their CUs (extra LDS,
+    ACE_CHAIN_XLDS, default) or sharing them (0)."""
     import os
     import subprocess
     import sys
@@ -554,7 +555,9 @@ def test_pair_steps_are_bitwise_neutral(A, tmp_path, n):
                 "qsplit_boundary": {"ACE_QSPLIT": "2"},
                 "heads3_qsplit_off": {"ACE_GROUP": "3", "ACE_HEADS": "1", "ACE_QSPLIT": "0"},
                 "tail_last_off": {"ACE_TAIL_LAST": "0"},
-                "tail_last_off_qsplit_off": {"ACE_TAIL_LAST": "0", "ACE_QSPLIT": "0"}}
+                "tail_last_off_qsplit_off": {"ACE_TAIL_LAST": "0", "ACE_QSPLIT": "0"},
+                "chain_xlds_off": {"ACE_CHAIN_XLDS": "0"},
+                "chain_xlds_first_only": {"ACE_CHAIN_XLDS_J": "1", "ACE_CHAIN_XLDS_G0": "0"}}
     for name, ev in variants.items():
         out = str(tmp_path / f"inv_{name}.npy")
         env = dict(os.environ, **ev)
